@@ -1,0 +1,244 @@
+/*
+ * rtx.h — C-ABI of librtx, the MI355X-native replacement for the hot path of
+ * a1exwang/raytracing_rb:  Camera#render_at -> RayTracer#trace_sync
+ * (src/camera.rb:70-110, src/ray_tracer.rb:16-164) together with the native
+ * Vec3 it runs on (ext/fast_4d_matrix/fast_4d_matrix.c) and the fork_jobs tile
+ * scheduler that parallelises it (src/fork_jobs.rb:1-33, camera.rb:41-68).
+ *
+ * Plain C: no Ruby, HIP or torch types.  Pointers are caller-owned.  All
+ * arithmetic is IEEE binary64 with the reference's operation order (no FMA).
+ *
+ * Reference interfaces replaced (file:line of the reference, read-only at
+ * /root/reference):
+ *   rtx_scene_upload      World.new(world.yml)         src/world.rb:15-34,
+ *                          ConfigurableObject            src/configurable_object.rb:43-49,
+ *                          Sphere/Plane/Box/Texture.new  src/objects/{sphere,plane,box,texture}.rb
+ *   rtx_camera_set        Camera.new(world, camera.yml) src/camera.rb:26-34
+ *   rtx_render            Camera#render_sync loops       src/camera.rb:101-110
+ *   rtx_render_device     (same, device-resident output, async on a HIP stream)
+ *   rtx_render_tiles_device  the per-child work of Camera#render_fork +
+ *                          fork_jobs                      src/camera.rb:53-65, src/fork_jobs.rb:5-22
+ *   rtx_render_at         Camera#render_at(x, y)         src/camera.rb:70-99
+ *   rtx_trace             RayTracer#trace_sync(x, y, ray) src/ray_tracer.rb:16-46
+ *   rtx_quantize          Camera#array_to_color + canvas.point  src/camera.rb:105,153-156
+ *   rtx_vec3_*            Fast4DMatrix::Vec3 methods     ext/fast_4d_matrix/fast_4d_matrix.c:29-55
+ *   rtx_status codes      the reference's raise sites    fast_4d_matrix.c:124,220,291;
+ *                          ray_tracer.rb:294-296; world_object.rb:106; sphere.rb:45-46
+ */
+#ifndef RTX_H
+#define RTX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTX_ABI_VERSION 1
+
+typedef enum rtx_status {
+  RTX_OK = 0,
+  RTX_EZERO_VEC = 1,   /* "zero vector detected" fast_4d_matrix.c:124,291; world_object.rb:106 */
+  RTX_ECOLOR_GT1 = 2,  /* "color greater than 1"  ray_tracer.rb:294-296 (also NaN channels)      */
+  RTX_EDOMAIN = 3,     /* Math::DomainError / FloatDomainError: sphere.rb:45-46, texture.rb:24-25 */
+  RTX_EHIP = 4,        /* HIP runtime failure                                                    */
+  RTX_ERCCL = 5,       /* collective failure (reported by the host layer)                        */
+  RTX_EINVAL = 6,      /* bad descriptor: the reference's NoMethodError/TypeError on missing keys */
+  RTX_ENOMEM = 7
+} rtx_status;
+
+enum rtx_object_type { RTX_SPHERE = 0, RTX_PLANE = 1, RTX_BOX = 2 };
+
+/* One entry of world.yml `world_objects:` (YAML order is significant: the
+ * first object wins distance ties, world.rb:48-50).  Field names are the YAML
+ * property names of src/objects/{world_object,sphere,plane,box}.rb. */
+typedef struct rtx_object_desc {
+  int32_t type;                      /* rtx_object_type                                      */
+  int32_t texture_id;                /* index into rtx_scene_desc.textures, -1 = none        */
+  int32_t has_refractive_rate;       /* Ruby truthiness of `refractive_rate` (plane.rb:57)   */
+  int32_t has_refractive_attenuation;
+  double diffuse_rate[3];
+  double ambient[3];
+  double reflective_attenuation[3];
+  double refractive_attenuation[3];
+  double refractive_rate;
+  /* Sphere (sphere.rb) */
+  double center[3];
+  double radius;
+  double north_pole_vec[3];
+  double greenwich_vec[3];
+  double texture_u_offset;           /* Texture u_off/v_off: spheres only (sphere.rb:25)     */
+  double texture_v_offset;
+  /* Plane (plane.rb) / Box (box.rb) */
+  double point[3];
+  double front[3];
+  double up[3];
+  double u_unit, v_unit;             /* plane                                                */
+  double width_front, width_up, width_left;   /* box                                       */
+  double texture_horizontal_scale;
+  double texture_vertical_scale;
+} rtx_object_desc;
+
+/* One entry of world.yml `lights:` (src/lights/light.rb:3-4, spot_light.rb:5). */
+typedef struct rtx_light_desc {
+  double position[3];
+  double color[3];
+  double radius;                     /* 0 = point light                                      */
+  double high_light_rate;
+  double high_light_angle;           /* degrees                                              */
+} rtx_light_desc;
+
+/* A decoded texture (texture.rb:12-20): RGB bytes, rows top-down, each byte the
+ * high byte of the 16-bit quantum (`pixel.red >> 8`); the library applies /256.0. */
+typedef struct rtx_texture_desc {
+  int32_t width;
+  int32_t height;
+  const uint8_t* rgb;
+} rtx_texture_desc;
+
+typedef struct rtx_scene_desc {
+  double max_distance;               /* world.yml max_distance         */
+  double soft_shadow_exponent;       /* world.yml soft_shadow_exponent */
+  int32_t n_objects;
+  int32_t n_lights;
+  int32_t n_textures;
+  int32_t reserved;
+  const rtx_object_desc* objects;
+  const rtx_light_desc* lights;
+  const rtx_texture_desc* textures;
+} rtx_scene_desc;
+
+/* camera.yml, 1:1 (src/camera.rb:17-24). */
+typedef struct rtx_camera_desc {
+  double position[3];
+  double up[3];
+  double front[3];
+  double retina_width;
+  double retina_height;
+  double aperture_radius;
+  double image_distance;
+  double focal_distance;
+  double variant_threshold;
+  int32_t width;
+  int32_t height;
+  int32_t pre_sample_times;
+  int32_t max_sample_times;
+  int32_t trace_depth;
+  int32_t monte_carlo_diffusion_times;
+} rtx_camera_desc;
+
+/* Vec3 value with its cached norm, as Vec3Type (fast_4d_matrix.c:57-60). */
+typedef struct rtx_vec3 {
+  double v[3];
+  double r;
+} rtx_vec3;
+
+typedef struct rtx_context rtx_context;
+
+/* ---- context ------------------------------------------------------------ */
+rtx_status  rtx_context_create(int32_t device, rtx_context** out);
+void        rtx_context_destroy(rtx_context* ctx);
+const char* rtx_last_error(const rtx_context* ctx);
+const char* rtx_status_string(rtx_status s);
+int32_t     rtx_abi_version(void);
+
+/* ---- scene / camera (World.new, Camera.new) ----------------------------- */
+rtx_status rtx_scene_upload(rtx_context* ctx, const rtx_scene_desc* scene);
+rtx_status rtx_camera_set(rtx_context* ctx, const rtx_camera_desc* camera);
+
+/* ---- rendering ---------------------------------------------------------- */
+/* Camera#render_sync: pixels [x0,x1) x [y0,y1) into the caller-owned host
+ * buffer out_rgb (row-major; out_rgb[(y-y0)*row_stride + (x-x0)*3 + c]) in final
+ * image orientation (row = y = top row first), before quantization.
+ * Synchronous.  RNG key: seed (main.rb:10 uses Random.srand(1)). */
+rtx_status rtx_render(rtx_context* ctx, int32_t x0, int32_t y0, int32_t x1, int32_t y1,
+                      uint64_t seed, double* out_rgb, size_t row_stride);
+
+/* As rtx_render, but d_out is DEVICE memory and the work is enqueued on
+ * `hip_stream` (a hipStream_t, NULL = default) without host synchronization.
+ * Reference raise sites are recorded on the device; read them with rtx_sync. */
+rtx_status rtx_render_device(rtx_context* ctx, int32_t x0, int32_t y0, int32_t x1, int32_t y1,
+                             uint64_t seed, double* d_out, size_t row_stride, void* hip_stream);
+
+/* One rank's share of a frame split into `tile_rows`-row tiles dealt
+ * round-robin: tile t belongs to rank t % nranks (the GPU replacement of
+ * camera.rb:53-65's contiguous column bands).  Packed output in device memory:
+ * local tile k of this rank = global tile k*nranks+rank is stored at rows
+ * [k*tile_rows, (k+1)*tile_rows) of d_packed (width*3 doubles per row);
+ * rows past the image bottom are left untouched.  Packed rows per rank:
+ * rtx_tiles_rows_per_rank(). */
+int32_t    rtx_tiles_rows_per_rank(int32_t height, int32_t tile_rows, int32_t nranks);
+rtx_status rtx_render_tiles_device(rtx_context* ctx, int32_t tile_rows, int32_t rank, int32_t nranks,
+                                   uint64_t seed, double* d_packed, void* hip_stream);
+
+/* Wait for `hip_stream` and report the first reference raise recorded by the
+ * device since the last rtx_sync (RTX_OK if none); details in rtx_last_error. */
+rtx_status rtx_sync(rtx_context* ctx, void* hip_stream);
+
+/* Camera#render_at(x, y): the averaged colour of one pixel. */
+rtx_status rtx_render_at(rtx_context* ctx, int32_t x, int32_t y, uint64_t seed, double rgb[3]);
+
+/* RayTracer#trace_sync(x, y, ray) for n rays at once (host buffers).
+ * rays[i*6 + 0..2] = Ray#front, rays[i*6 + 3..5] = Ray#position;
+ * keys[i*3 + 0..2] = (x, y, sample) — the RNG key of the ray tree. */
+rtx_status rtx_trace(rtx_context* ctx, int32_t n, const double* rays, const int32_t* keys,
+                     uint64_t seed, double* out_rgb);
+
+/* Camera#array_to_color (camera.rb:153-156) + PNG::Canvas#point: RGBA8,
+ * byte = trunc(min(256*c, 255)); png_gem_blend != 0 additionally applies the
+ * png gem's alpha blend over the black canvas ((v*255) >> 8).  Host buffers. */
+rtx_status rtx_quantize(const double* rgb, int32_t width, int32_t height, size_t row_stride,
+                        int32_t png_gem_blend, uint8_t* out_rgba);
+/* Device variant (async on hip_stream). */
+rtx_status rtx_quantize_device(const double* d_rgb, int32_t width, int32_t height, size_t row_stride,
+                               int32_t png_gem_blend, uint8_t* d_out_rgba, void* hip_stream);
+
+/* Algorithmic work counters of one frame (brute-force reference algorithm),
+ * for the roofline: see DESIGN.md "Algorithmic FP64 ops".  counts[RTX_NCOUNT]. */
+enum {
+  RTX_CNT_RAYS = 0,          /* rt_map calls that passed the cutoff                     */
+  RTX_CNT_SPHERE_TESTS,      /* Sphere#intersect calls from World#intersect            */
+  RTX_CNT_SPHERE_HITS,
+  RTX_CNT_PLANE_TESTS,
+  RTX_CNT_BOX_TESTS,
+  RTX_CNT_SHADE_HITS,        /* rays with a nearest hit                                 */
+  RTX_CNT_COVER_SPHERE,      /* Sphere#cover_area calls                                 */
+  RTX_CNT_COVER_PLANE,
+  RTX_CNT_COVER_BOX,
+  RTX_CNT_HIGHLIGHT_TESTS,   /* per ray x light                                         */
+  RTX_CNT_PRIMARY,           /* lens_func samples                                       */
+  RTX_NCOUNT
+};
+rtx_status rtx_count_work(rtx_context* ctx, uint64_t seed, uint64_t counts[RTX_NCOUNT]);
+
+/* Kernel-variant control for experiments; 0 = default. */
+rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
+
+/* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
+rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */
+double     rtx_vec3_r(rtx_vec3 a);                                          /* :275-279 */
+double     rtx_vec3_r2(rtx_vec3 a);                                         /* :280-284 */
+double     rtx_vec3_dot(rtx_vec3 a, rtx_vec3 b);                            /* :98-107  */
+rtx_status rtx_vec3_cos(rtx_vec3 a, rtx_vec3 b, double* out);               /* :109-129 */
+rtx_vec3   rtx_vec3_cross(rtx_vec3 a, rtx_vec3 b);                          /* :131-141 */
+rtx_vec3   rtx_vec3_add(rtx_vec3 a, rtx_vec3 b);                            /* :166-176 */
+rtx_vec3   rtx_vec3_sub(rtx_vec3 a, rtx_vec3 b);                            /* :178-188 */
+rtx_vec3   rtx_vec3_mul(rtx_vec3 a, rtx_vec3 b);                            /* :190-208 */
+rtx_vec3   rtx_vec3_scale(rtx_vec3 a, double s);                            /* :190-208 */
+rtx_vec3   rtx_vec3_div(rtx_vec3 a, double s);                              /* :209-224 */
+rtx_vec3   rtx_vec3_neg(rtx_vec3 a);                                        /* :154-164 */
+rtx_vec3   rtx_vec3_pos(rtx_vec3 a);                                        /* :143-152 */
+rtx_status rtx_vec3_normalize(rtx_vec3 a, rtx_vec3* out);                   /* :286-293 */
+rtx_vec3   rtx_vec3_add_bang(rtx_vec3 a, rtx_vec3 b);                       /* :230-240 */
+rtx_vec3   rtx_vec3_sub_bang(rtx_vec3 a, rtx_vec3 b);                       /* :242-251 */
+rtx_vec3   rtx_vec3_mul_bang(rtx_vec3 a, rtx_vec3 b);                       /* :253-273 */
+rtx_vec3   rtx_vec3_mul_bang_scalar(rtx_vec3 a, double s);                  /* :253-273 */
+
+/* The counter RNG contract (DESIGN.md "RNG"): u in [0,1). */
+double rtx_rand(uint64_t seed, int32_t x, int32_t y, int32_t sample, uint64_t path, int32_t draw);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTX_H */

@@ -1,0 +1,44 @@
+"""Build librtx.so in-tree with hipcc for gfx950 (no JIT cache, no pip install).
+
+    python -m raytracing_rb_amd._build [--force]
+"""
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "librtx.so")
+SOURCES = [os.path.join(CSRC, f) for f in ("rtx_kernels.hip", "rtx_capi.cpp")]
+HEADERS = [os.path.join(CSRC, f) for f in ("rtx_scene.h", "rtx_vec3.h", "rtx_launch.h")] + [
+    os.path.join(ROOT, "include", "rtx.h")]
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -ffp-contract=off: no FMA contraction anywhere — every binary64 operation rounds
+# exactly like the reference's Ruby + C-extension arithmetic.
+FLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fno-fast-math", "-std=c++17", "-fPIC",
+         "-shared", "-Wall", "-Wno-unused-result", "-Wno-unused-value"]
+
+
+def stale():
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS + [__file__])
+
+
+def build(force=False, verbose=False):
+    if not force and not stale():
+        return OUT
+    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp"] + SOURCES
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,591 @@
+// rtx_capi.cpp — the C-ABI of librtx (include/rtx.h): scene/camera upload,
+// render entry points, Vec3 helpers.  Host code; kernels in rtx_kernels.hip.
+//
+// Scene preparation restates the constructors of the reference
+// (src/world.rb:15-34, src/objects/{sphere,plane,box,texture}.rb,
+// src/camera.rb:26-34,129-151) with the same operation order, so every
+// constant the device uses has the bits the Ruby code would compute.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rtx.h"
+#include "rtx_launch.h"
+#include "rtx_scene.h"
+#include "rtx_vec3.h"
+
+using namespace rtx;
+
+struct rtx_context {
+  int device = 0;
+  std::string err;
+  // device scene
+  ObjInfo* d_info = nullptr;
+  double* d_geo = nullptr;
+  Material* d_mat = nullptr;
+  LightDev* d_light = nullptr;
+  TexDev* d_tex = nullptr;
+  uint8_t* d_texels = nullptr;
+  SceneDev scene{};
+  SceneDev* d_scene = nullptr;
+  bool have_scene = false;
+  // camera
+  CameraDev cam{};
+  CameraDev* d_cam = nullptr;
+  bool have_cam = false;
+  // work buffers
+  ErrState* d_err = nullptr;
+  unsigned long long* d_counts = nullptr;
+  double* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  int64_t opt_force_stack = 0;
+  int64_t opt_wps = 2;
+};
+
+static rtx_status fail(rtx_context* c, rtx_status s, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return s;
+}
+
+#define HIPCHK(c, expr)                                                                     \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return fail(c, RTX_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+static void free_scene(rtx_context* c) {
+  (void)hipFree(c->d_info);
+  (void)hipFree(c->d_geo);
+  (void)hipFree(c->d_mat);
+  (void)hipFree(c->d_light);
+  (void)hipFree(c->d_tex);
+  (void)hipFree(c->d_texels);
+  c->d_info = nullptr;
+  c->d_geo = nullptr;
+  c->d_mat = nullptr;
+  c->d_light = nullptr;
+  c->d_tex = nullptr;
+  c->d_texels = nullptr;
+  c->have_scene = false;
+}
+
+extern "C" {
+
+int32_t rtx_abi_version(void) { return RTX_ABI_VERSION; }
+
+const char* rtx_status_string(rtx_status s) {
+  switch (s) {
+    case RTX_OK: return "ok";
+    case RTX_EZERO_VEC: return "zero vector detected";
+    case RTX_ECOLOR_GT1: return "color greater than 1";
+    case RTX_EDOMAIN: return "domain error";
+    case RTX_EHIP: return "HIP error";
+    case RTX_ERCCL: return "RCCL error";
+    case RTX_EINVAL: return "invalid argument";
+    case RTX_ENOMEM: return "out of memory";
+  }
+  return "unknown";
+}
+
+const char* rtx_last_error(const rtx_context* c) { return c ? c->err.c_str() : "null context"; }
+
+rtx_status rtx_context_create(int32_t device, rtx_context** out) {
+  if (!out) return RTX_EINVAL;
+  *out = nullptr;
+  rtx_context* c = new rtx_context();
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc(&c->d_err, sizeof(ErrState));
+  if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(unsigned long long) * RTX_NCOUNT);
+  if (e == hipSuccess) e = hipMalloc(&c->d_scene, sizeof(SceneDev));
+  if (e == hipSuccess) e = hipMalloc(&c->d_cam, sizeof(CameraDev));
+  if (e == hipSuccess) e = hipMemset(c->d_err, 0, sizeof(unsigned int) * 2);
+  if (e == hipSuccess) e = hipMemset(((char*)c->d_err) + 8, 0xFF, sizeof(unsigned long long) * 4);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    fprintf(stderr, "rtx_context_create: %s\n", hipGetErrorString(e));
+    delete c;
+    return RTX_EHIP;
+  }
+  *out = c;
+  return RTX_OK;
+}
+
+void rtx_context_destroy(rtx_context* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  free_scene(c);
+  hipFree(c->d_err);
+  hipFree(c->d_counts);
+  hipFree(c->d_scene);
+  hipFree(c->d_cam);
+  hipFree(c->d_scratch);
+  delete c;
+}
+
+rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
+  if (!c || !key) return RTX_EINVAL;
+  if (!strcmp(key, "force_stack")) {
+    c->opt_force_stack = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "waves_per_simd")) {    // k_render occupancy variant (1..4; 16-entry stack only)
+    if (value < 1 || value > 4) return fail(c, RTX_EINVAL, "waves_per_simd must be 1..4");
+    c->opt_wps = value;
+    return RTX_OK;
+  }
+  return fail(c, RTX_EINVAL, "unknown option '%s'", key);
+}
+
+// ------------------------------------------------------------------ scene
+static void put3(std::vector<double>& g, V3 v) {
+  g.push_back(v.x);
+  g.push_back(v.y);
+  g.push_back(v.z);
+}
+static void set3(double* d, V3 v) {
+  d[0] = v.x;
+  d[1] = v.y;
+  d[2] = v.z;
+}
+
+// Plane record (plane.rb:21-23 reinit + get_uv's re-normalizations :82-83).
+static void put_plane(std::vector<double>& g, V3 P, V3 F, V3 U, double uu, double vu, uint32_t& err) {
+  V3 left = vnorm(vcross(F, U), err);
+  put3(g, P);
+  put3(g, F);
+  put3(g, vnorm(left, err));
+  put3(g, vnorm(U, err));
+  g.push_back(uu);
+  g.push_back(vu);
+}
+
+rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
+  if (!c || !sd) return fail(c, RTX_EINVAL, "null argument");
+  if (sd->n_objects < 0 || sd->n_lights < 0 || sd->n_textures < 0)
+    return fail(c, RTX_EINVAL, "negative counts");
+  if (sd->n_lights > 32) return fail(c, RTX_EINVAL, "at most 32 lights are supported");
+  if ((sd->n_objects && !sd->objects) || (sd->n_lights && !sd->lights) || (sd->n_textures && !sd->textures))
+    return fail(c, RTX_EINVAL, "null array with nonzero count");
+  hipSetDevice(c->device);
+  uint32_t err = 0;
+  std::vector<ObjInfo> info(sd->n_objects);
+  std::vector<Material> mat(sd->n_objects);
+  std::vector<double> geo;
+  int ns = 0, np = 0, nb = 0;
+  for (int i = 0; i < sd->n_objects; i++) {
+    const rtx_object_desc& o = sd->objects[i];
+    Material& m = mat[i];
+    memset(&m, 0, sizeof m);
+    set3(m.diffuse, v3p(o.diffuse_rate));
+    set3(m.ambient, v3p(o.ambient));
+    set3(m.refl_att, v3p(o.reflective_attenuation));
+    set3(m.refr_att, v3p(o.refractive_attenuation));
+    m.rr = o.refractive_rate;
+    m.has_rr = o.has_refractive_rate != 0;
+    m.tex = o.texture_id;
+    m.hs = o.texture_horizontal_scale;
+    m.vs = o.texture_vertical_scale;
+    if (o.texture_id >= sd->n_textures) return fail(c, RTX_EINVAL, "object %d: bad texture id", i);
+    info[i].type = o.type;
+    info[i].geo = (int32_t)geo.size();
+    if (o.type == RTX_SPHERE) {
+      if (!o.has_refractive_rate) return fail(c, RTX_EINVAL, "object %d: sphere needs refractive_rate", i);
+      ns++;
+      const V3 C = v3p(o.center);
+      put3(geo, C);
+      geo.push_back(o.radius);
+      geo.push_back(o.radius * o.radius);
+      geo.push_back(fabs(C.x) + fabs(C.y) + fabs(C.z) + o.radius);
+      m.u_off = o.texture_u_offset;
+      m.v_off = o.texture_v_offset;
+      if (o.texture_id >= 0) {                     // sphere.rb:18, 113-115
+        const V3 north = v3p(o.north_pole_vec), gw = v3p(o.greenwich_vec);
+        set3(m.gw_n, vnorm(gw, err));
+        set3(m.east_n, vnorm(vcross(north, gw), err));
+        set3(m.north_n, vnorm(north, err));
+      }
+    } else if (o.type == RTX_PLANE) {
+      np++;
+      put_plane(geo, v3p(o.point), v3p(o.front), v3p(o.up), o.u_unit, o.v_unit, err);
+    } else if (o.type == RTX_BOX) {                 // box.rb:15-73
+      nb++;
+      m.tex = -1;                                    // loaded, never used for shading
+      const V3 P = v3p(o.point), F = v3p(o.front), U = v3p(o.up);
+      const double wf = o.width_front, wu = o.width_up, wl = o.width_left;
+      const V3 left = vnorm(vcross(F, U), err);
+      put_plane(geo, vadd(P, vsc(vsc(U, wu), 0.5)), U, left, wf, wl, err);
+      put_plane(geo, vsub(P, vsc(vsc(U, wu), 0.5)), vneg(U), left, wf, wl, err);
+      put_plane(geo, vadd(P, vsc(vsc(F, wf), 0.5)), F, U, wl, wu, err);
+      put_plane(geo, vsub(P, vsc(vsc(F, wf), 0.5)), vneg(F), U, wl, wu, err);
+      put_plane(geo, vadd(P, vsc(vsc(left, wl), 0.5)), left, U, wf, wu, err);
+      put_plane(geo, vsub(P, vsc(vsc(left, wl), 0.5)), vneg(left), U, wf, wu, err);
+    } else {
+      return fail(c, RTX_EINVAL, "object %d: unknown type %d", i, o.type);
+    }
+  }
+  if (err) return fail(c, RTX_EZERO_VEC, "zero vector detected while building the scene");
+  std::vector<LightDev> lights(sd->n_lights);
+  for (int i = 0; i < sd->n_lights; i++) {
+    const rtx_light_desc& l = sd->lights[i];
+    LightDev& d = lights[i];
+    memset(&d, 0, sizeof d);
+    set3(d.pos, v3p(l.position));
+    set3(d.color, v3p(l.color));
+    d.radius = l.radius;
+    d.hl_rate = l.high_light_rate;
+    d.hl_angle_rad = l.high_light_angle / 180.0 * 3.141592653589793;   // world.rb:91
+    const double th = d.hl_angle_rad;
+    if (!(th > 0)) {
+      d.hl_mode = 2;                                 // acos(c) >= 0 can never be < th
+    } else if (th < 1e-6 || th > 1.5) {
+      d.hl_mode = 1;
+    } else {
+      const double ct = cos(th), lo = ct - 1e-7, hi = ct + 1e-7;
+      d.hl_mode = (hi >= 1.0 || lo <= 0.0) ? 1 : 0;
+      d.cos_lo2 = lo * lo;
+      d.cos_hi2 = hi * hi;
+    }
+  }
+  std::vector<TexDev> tex(sd->n_textures);
+  std::vector<uint8_t> texels;
+  for (int i = 0; i < sd->n_textures; i++) {
+    const rtx_texture_desc& t = sd->textures[i];
+    if (t.width <= 0 || t.height <= 0 || !t.rgb) return fail(c, RTX_EINVAL, "texture %d: empty", i);
+    tex[i].w = t.width;
+    tex[i].h = t.height;
+    tex[i].off = (int64_t)texels.size();
+    texels.insert(texels.end(), t.rgb, t.rgb + (size_t)t.width * t.height * 3);
+  }
+  free_scene(c);
+  auto up = [&](void** dst, const void* src, size_t bytes) -> hipError_t {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(dst, bytes);
+    if (e == hipSuccess && src) e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+    return e;
+  };
+  geo.resize(geo.size() + 8, 0.0);
+  HIPCHK(c, up((void**)&c->d_info, info.data(), info.size() * sizeof(ObjInfo)));
+  HIPCHK(c, up((void**)&c->d_geo, geo.data(), geo.size() * sizeof(double)));
+  HIPCHK(c, up((void**)&c->d_mat, mat.data(), mat.size() * sizeof(Material)));
+  HIPCHK(c, up((void**)&c->d_light, lights.data(), lights.size() * sizeof(LightDev)));
+  HIPCHK(c, up((void**)&c->d_tex, tex.data(), tex.size() * sizeof(TexDev)));
+  HIPCHK(c, up((void**)&c->d_texels, texels.empty() ? nullptr : texels.data(), texels.size()));
+  SceneDev& S = c->scene;
+  S.info = c->d_info;
+  S.geo = c->d_geo;
+  S.mat = c->d_mat;
+  S.light = c->d_light;
+  S.tex = c->d_tex;
+  S.texels = c->d_texels;
+  S.n_obj = sd->n_objects;
+  S.n_light = sd->n_lights;
+  S.n_sphere = ns;
+  S.n_plane = np;
+  S.n_box = nb;
+  S.n_geo = (int32_t)geo.size();
+  S.max_distance = sd->max_distance;
+  S.sse = sd->soft_shadow_exponent;
+  S.sse_is_two = sd->soft_shadow_exponent == 2.0;     // glibc pow(x, 2.0) == x*x
+  HIPCHK(c, hipMemcpy(c->d_scene, &S, sizeof S, hipMemcpyHostToDevice));
+  c->have_scene = true;
+  return RTX_OK;
+}
+
+rtx_status rtx_camera_set(rtx_context* c, const rtx_camera_desc* d) {
+  if (!c || !d) return fail(c, RTX_EINVAL, "null argument");
+  if (d->width <= 0 || d->height <= 0) return fail(c, RTX_EINVAL, "width/height must be positive");
+  if (d->pre_sample_times < 1 || d->pre_sample_times > 16)
+    return fail(c, RTX_EINVAL, "pre_sample_times must be in [1, 16]");
+  if (d->max_sample_times < 0) return fail(c, RTX_EINVAL, "max_sample_times must be >= 0");
+  if (d->trace_depth < 0 || d->trace_depth > 1000) return fail(c, RTX_EINVAL, "bad trace_depth");
+  if (d->monte_carlo_diffusion_times < 1) return fail(c, RTX_EINVAL, "monte_carlo_diffusion_times must be >= 1");
+  uint32_t err = 0;
+  CameraDev& k = c->cam;
+  memset(&k, 0, sizeof k);
+  const V3 pos = v3p(d->position), up = v3p(d->up), front = v3p(d->front);
+  const V3 left = vnorm(vcross(up, front), err);                       // camera.rb:130
+  set3(k.pos, pos);
+  set3(k.left, left);
+  set3(k.left_n, vnorm(left, err));                                    // :136
+  set3(k.up_n, vnorm(up, err));                                        // :134,136
+  set3(k.front, front);
+  set3(k.retina_center, vsub(pos, vsc(vnorm(front, err), d->image_distance)));   // :131
+  const double od = d->focal_distance * d->image_distance / (d->image_distance - d->focal_distance);  // :139
+  set3(k.pofp, vadd(pos, vsc(vnorm(front, err), od)));                // :142
+  k.retina_width = d->retina_width;
+  k.retina_height = d->retina_height;
+  k.aperture_radius = d->aperture_radius;
+  k.variant_threshold = d->variant_threshold;
+  k.width = d->width;
+  k.height = d->height;
+  k.pre = d->pre_sample_times;
+  k.max_samples = d->max_sample_times;
+  k.depth = d->trace_depth;
+  k.pt = d->monte_carlo_diffusion_times;
+  if (err) return fail(c, RTX_EZERO_VEC, "zero vector detected while building the camera");
+  HIPCHK(c, hipMemcpy(c->d_cam, &k, sizeof k, hipMemcpyHostToDevice));
+  c->have_cam = true;
+  return RTX_OK;
+}
+
+// ------------------------------------------------------------------ render
+static int required_stack(const rtx_context* c) {
+  // LIFO depth-first walk: a node at depth d >= 2 pushes <= 2 + pt children.
+  const long need = 1 + (long)(c->cam.depth > 1 ? c->cam.depth - 1 : 0) * (1 + c->cam.pt);
+  if (c->opt_force_stack) return stack_bucket((int)c->opt_force_stack);
+  return need > 64 ? -1 : stack_bucket((int)need);
+}
+
+static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
+  if (!c->have_scene) return fail(c, RTX_EINVAL, "no scene uploaded");
+  if (!c->have_cam) return fail(c, RTX_EINVAL, "no camera set");
+  memset(&p, 0, sizeof p);
+  p.scene = c->d_scene;
+  p.cam = c->d_cam;
+  p.seed = seed;
+  p.err = c->d_err;
+  p.counts = c->d_counts;
+  return RTX_OK;
+}
+
+rtx_status rtx_render_device(rtx_context* c, int32_t x0, int32_t y0, int32_t x1, int32_t y1, uint64_t seed,
+                             double* d_out, size_t row_stride, void* stream) {
+  if (!c) return RTX_EINVAL;
+  KParams p;
+  rtx_status s = prep(c, p, seed);
+  if (s) return s;
+  if (x0 < 0 || y0 < 0 || x1 > c->cam.width || y1 > c->cam.height || x0 > x1 || y0 > y1)
+    return fail(c, RTX_EINVAL, "region [%d,%d)x[%d,%d) outside the %dx%d image", x0, x1, y0, y1,
+                c->cam.width, c->cam.height);
+  if (row_stride < (size_t)(x1 - x0) * 3) return fail(c, RTX_EINVAL, "row_stride too small");
+  const int maxs = required_stack(c);
+  if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  hipSetDevice(c->device);
+  p.x0 = x0;
+  p.nx = x1 - x0;
+  p.y0 = y0;
+  p.nrows = y1 - y0;
+  p.out = d_out;
+  p.stride = row_stride;
+  HIPCHK(c, launch_render(p, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
+  return RTX_OK;
+}
+
+int32_t rtx_tiles_rows_per_rank(int32_t height, int32_t tile_rows, int32_t nranks) {
+  if (tile_rows <= 0 || nranks <= 0) return 0;
+  const int32_t tiles = (height + tile_rows - 1) / tile_rows;
+  return ((tiles + nranks - 1) / nranks) * tile_rows;
+}
+
+rtx_status rtx_render_tiles_device(rtx_context* c, int32_t tile_rows, int32_t rank, int32_t nranks,
+                                   uint64_t seed, double* d_packed, void* stream) {
+  if (!c) return RTX_EINVAL;
+  KParams p;
+  rtx_status s = prep(c, p, seed);
+  if (s) return s;
+  if (tile_rows <= 0 || nranks <= 0 || rank < 0 || rank >= nranks) return fail(c, RTX_EINVAL, "bad tiling");
+  const int maxs = required_stack(c);
+  if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  hipSetDevice(c->device);
+  p.x0 = 0;
+  p.nx = c->cam.width;
+  p.nrows = rtx_tiles_rows_per_rank(c->cam.height, tile_rows, nranks);
+  p.tile_rows = tile_rows;
+  p.rank = rank;
+  p.nranks = nranks;
+  p.out = d_packed;
+  p.stride = (size_t)c->cam.width * 3;
+  HIPCHK(c, launch_render(p, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
+  return RTX_OK;
+}
+
+rtx_status rtx_sync(rtx_context* c, void* stream) {
+  if (!c) return RTX_EINVAL;
+  hipSetDevice(c->device);
+  ErrState e;
+  HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+  HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof e, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemset(c->d_err, 0, 8));
+  HIPCHK(c, hipMemset(((char*)c->d_err) + 8, 0xFF, 32));
+  HIPCHK(c, hipDeviceSynchronize());
+  if (!e.flags) return RTX_OK;
+  static const rtx_status order[3] = {RTX_EZERO_VEC, RTX_ECOLOR_GT1, RTX_EDOMAIN};
+  rtx_status first = RTX_OK;
+  unsigned long long pix = ~0ull;
+  for (rtx_status code : order)
+    if ((e.flags >> code & 1) && e.first[code] < pix) {
+      pix = e.first[code];
+      first = code;
+    }
+  const long long W = c->have_cam ? c->cam.width : 1;
+  return fail(c, first, "%s at pixel (%lld,%lld)%s", rtx_status_string(first), (long long)(pix % W),
+              (long long)(pix / W), __builtin_popcount(e.flags) > 1 ? " (and other errors)" : "");
+}
+
+static rtx_status ensure_scratch(rtx_context* c, size_t bytes) {
+  if (bytes <= c->scratch_bytes) return RTX_OK;
+  hipFree(c->d_scratch);
+  c->d_scratch = nullptr;
+  c->scratch_bytes = 0;
+  HIPCHK(c, hipMalloc(&c->d_scratch, bytes));
+  c->scratch_bytes = bytes;
+  return RTX_OK;
+}
+
+rtx_status rtx_render(rtx_context* c, int32_t x0, int32_t y0, int32_t x1, int32_t y1, uint64_t seed,
+                      double* out, size_t row_stride) {
+  if (!c || !out) return fail(c, RTX_EINVAL, "null argument");
+  const int w = x1 - x0, h = y1 - y0;
+  if (w < 0 || h < 0) return fail(c, RTX_EINVAL, "empty region");
+  if (row_stride < (size_t)w * 3) return fail(c, RTX_EINVAL, "row_stride too small");
+  if (w == 0 || h == 0) return RTX_OK;
+  rtx_status s = rtx_sync(c, nullptr);               // clear stale device errors
+  (void)s;
+  hipSetDevice(c->device);
+  if ((s = ensure_scratch(c, sizeof(double) * 3 * (size_t)w * h))) return s;
+  if ((s = rtx_render_device(c, x0, y0, x1, y1, seed, c->d_scratch, (size_t)w * 3, nullptr))) return s;
+  HIPCHK(c, hipMemcpy2D(out, row_stride * sizeof(double), c->d_scratch, (size_t)w * 3 * sizeof(double),
+                        (size_t)w * 3 * sizeof(double), h, hipMemcpyDeviceToHost));
+  return rtx_sync(c, nullptr);
+}
+
+rtx_status rtx_render_at(rtx_context* c, int32_t x, int32_t y, uint64_t seed, double rgb[3]) {
+  return rtx_render(c, x, y, x + 1, y + 1, seed, rgb, 3);
+}
+
+rtx_status rtx_trace(rtx_context* c, int32_t n, const double* rays, const int32_t* keys, uint64_t seed,
+                     double* out) {
+  if (!c || n < 0 || (n && (!rays || !keys || !out))) return fail(c, RTX_EINVAL, "bad arguments");
+  if (n == 0) return RTX_OK;
+  KParams p;
+  rtx_status s = prep(c, p, seed);
+  if (s) return s;
+  const int maxs = required_stack(c);
+  if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  rtx_sync(c, nullptr);
+  hipSetDevice(c->device);
+  const size_t rb = sizeof(double) * 6 * n, kb = sizeof(int32_t) * 3 * n, ob = sizeof(double) * 3 * n;
+  if ((s = ensure_scratch(c, rb + kb + ob + 64))) return s;
+  char* base = (char*)c->d_scratch;
+  double* d_rays = (double*)base;
+  double* d_out = (double*)(base + rb);
+  int32_t* d_keys = (int32_t*)(base + rb + ob);
+  HIPCHK(c, hipMemcpy(d_rays, rays, rb, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(d_keys, keys, kb, hipMemcpyHostToDevice));
+  p.out = d_out;
+  HIPCHK(c, launch_trace(p, d_rays, d_keys, n, maxs, nullptr));
+  HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
+  return rtx_sync(c, nullptr);
+}
+
+rtx_status rtx_count_work(rtx_context* c, uint64_t seed, uint64_t counts[RTX_NCOUNT]) {
+  if (!c || !counts) return fail(c, RTX_EINVAL, "null argument");
+  KParams p;
+  rtx_status s = prep(c, p, seed);
+  if (s) return s;
+  const int maxs = required_stack(c);
+  if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  hipSetDevice(c->device);
+  const int W = c->cam.width, H = c->cam.height;
+  if ((s = ensure_scratch(c, sizeof(double) * 3 * (size_t)W * H))) return s;
+  HIPCHK(c, hipMemset(c->d_counts, 0, sizeof(unsigned long long) * RTX_NCOUNT));
+  p.x0 = 0;
+  p.nx = W;
+  p.nrows = H;
+  p.out = c->d_scratch;
+  p.stride = (size_t)W * 3;
+  HIPCHK(c, launch_render(p, true, maxs, 2, nullptr));
+  HIPCHK(c, hipDeviceSynchronize());
+  unsigned long long tmp[RTX_NCOUNT];
+  HIPCHK(c, hipMemcpy(tmp, c->d_counts, sizeof tmp, hipMemcpyDeviceToHost));
+  for (int k = 0; k < RTX_NCOUNT; k++) counts[k] = tmp[k];
+  return rtx_sync(c, nullptr);
+}
+
+rtx_status rtx_quantize_device(const double* d_rgb, int32_t w, int32_t h, size_t stride, int32_t blend,
+                               uint8_t* d_out, void* stream) {
+  if (w < 0 || h < 0 || stride < (size_t)w * 3 || (w * h && (!d_rgb || !d_out))) return RTX_EINVAL;
+  return launch_quantize(d_rgb, w, h, stride, blend, d_out, (hipStream_t)stream) == hipSuccess ? RTX_OK
+                                                                                                 : RTX_EHIP;
+}
+
+rtx_status rtx_quantize(const double* rgb, int32_t w, int32_t h, size_t stride, int32_t blend, uint8_t* out) {
+  if (w < 0 || h < 0 || stride < (size_t)w * 3 || (w * h && (!rgb || !out))) return RTX_EINVAL;
+  if (w * h == 0) return RTX_OK;
+  double* d_in = nullptr;
+  uint8_t* d_o = nullptr;
+  const size_t ib = sizeof(double) * stride * h, ob = (size_t)w * h * 4;
+  rtx_status s = RTX_OK;
+  if (hipMalloc(&d_in, ib) != hipSuccess || hipMalloc(&d_o, ob) != hipSuccess ||
+      hipMemcpy(d_in, rgb, ib, hipMemcpyHostToDevice) != hipSuccess ||
+      launch_quantize(d_in, w, h, stride, blend, d_o, nullptr) != hipSuccess ||
+      hipMemcpy(out, d_o, ob, hipMemcpyDeviceToHost) != hipSuccess)
+    s = RTX_EHIP;
+  hipFree(d_in);
+  hipFree(d_o);
+  return s;
+}
+
+// ------------------------------------------------------------------ Vec3 API
+static rtx_vec3 mk(V3 a) {
+  rtx_vec3 r;
+  r.v[0] = a.x;
+  r.v[1] = a.y;
+  r.v[2] = a.z;
+  r.r = sqrt(a.x * a.x + a.y * a.y + a.z * a.z);      // Vec3_c_create (fast_4d_matrix.c:62-73)
+  return r;
+}
+static V3 un(rtx_vec3 a) { return v3(a.v[0], a.v[1], a.v[2]); }
+
+rtx_vec3 rtx_vec3_from_a(double x, double y, double z) { return mk(v3(x, y, z)); }
+double rtx_vec3_r(rtx_vec3 a) { return a.r; }
+double rtx_vec3_r2(rtx_vec3 a) { return a.r * a.r; }
+double rtx_vec3_dot(rtx_vec3 a, rtx_vec3 b) { return vdot(un(a), un(b)); }
+rtx_status rtx_vec3_cos(rtx_vec3 a, rtx_vec3 b, double* out) {
+  uint32_t err = 0;
+  double v = vcos(un(a), un(b), err);
+  if (out) *out = v;
+  return err ? RTX_EZERO_VEC : RTX_OK;
+}
+rtx_vec3 rtx_vec3_cross(rtx_vec3 a, rtx_vec3 b) { return mk(vcross(un(a), un(b))); }
+rtx_vec3 rtx_vec3_add(rtx_vec3 a, rtx_vec3 b) { return mk(vadd(un(a), un(b))); }
+rtx_vec3 rtx_vec3_sub(rtx_vec3 a, rtx_vec3 b) { return mk(vsub(un(a), un(b))); }
+rtx_vec3 rtx_vec3_mul(rtx_vec3 a, rtx_vec3 b) { return mk(vmul(un(a), un(b))); }
+rtx_vec3 rtx_vec3_scale(rtx_vec3 a, double s) { return mk(vsc(un(a), s)); }
+rtx_vec3 rtx_vec3_div(rtx_vec3 a, double s) { return mk(vdiv(un(a), s)); }
+rtx_vec3 rtx_vec3_neg(rtx_vec3 a) { return mk(vneg(un(a))); }
+rtx_vec3 rtx_vec3_pos(rtx_vec3 a) { return mk(un(a)); }
+rtx_status rtx_vec3_normalize(rtx_vec3 a, rtx_vec3* out) {
+  uint32_t err = 0;
+  V3 v = vnorm(un(a), err);
+  if (err) return RTX_EZERO_VEC;
+  if (out) *out = mk(v);
+  return RTX_OK;
+}
+// The bang forms mutate in place and recompute r (Vec3_c_recalc_r, :226-229);
+// as values they equal the non-bang results.
+rtx_vec3 rtx_vec3_add_bang(rtx_vec3 a, rtx_vec3 b) { return mk(vadd(un(a), un(b))); }
+rtx_vec3 rtx_vec3_sub_bang(rtx_vec3 a, rtx_vec3 b) { return mk(vsub(un(a), un(b))); }
+rtx_vec3 rtx_vec3_mul_bang(rtx_vec3 a, rtx_vec3 b) { return mk(vmul(un(a), un(b))); }
+rtx_vec3 rtx_vec3_mul_bang_scalar(rtx_vec3 a, double s) { return mk(vsc(un(a), s)); }
+
+double rtx_rand(uint64_t seed, int32_t x, int32_t y, int32_t sample, uint64_t path, int32_t draw) {
+  return rand01(seed, x, y, sample, path, draw);
+}
+
+}  // extern "C"

@@ -1,0 +1,38 @@
+// rtx_launch.h — kernel parameter block and launchers shared by the C-ABI
+// (rtx_capi.cpp) and the kernels (rtx_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rtx_scene.h"
+
+namespace rtx {
+
+// Reference raise sites recorded by the device (codes: ERR_* in rtx_vec3.h).
+struct ErrState {
+  unsigned int flags;              // bit (1 << code) for every code raised
+  unsigned int pad;
+  unsigned long long first[4];     // per code: min linear pixel index (y*W + x)
+};
+
+struct KParams {
+  const SceneDev* scene;           // device copies (uploaded by rtx_scene_upload / rtx_camera_set)
+  const CameraDev* cam;
+  uint64_t seed;
+  int32_t x0, nx, nrows;           // columns [x0, x0+nx); packed output rows
+  int32_t y0, tile_rows, rank, nranks;   // tile_rows == 0: rows y0 .. y0+nrows-1
+  double* out;
+  size_t stride;                   // doubles per output row
+  ErrState* err;
+  unsigned long long* counts;      // RTX_NCOUNT counters (counting launches only)
+};
+
+int stack_bucket(int need);
+hipError_t launch_render(const KParams& p, bool count, int maxs, int wps, hipStream_t s);
+hipError_t launch_trace(const KParams& p, const double* rays, const int32_t* keys, int n, int maxs,
+                        hipStream_t s);
+hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,
+                           hipStream_t s);
+
+}  // namespace rtx

@@ -1,0 +1,147 @@
+"""Thin Python handle over librtx (``include/rtx.h``).
+
+``Renderer`` owns one ``rtx_context`` (one HIP device) with an uploaded scene
+and camera.  Host-buffer calls are synchronous; ``*_device`` calls take raw
+device pointers (e.g. ``torch.Tensor.data_ptr()``) and a HIP stream handle and
+return immediately.  Errors raise ``RtxError`` carrying the reference's raise
+site (``rtx_status``).  There is no CPU fallback: without librtx.so nothing here
+works.
+"""
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import RTX_NCOUNT, COUNTER_NAMES, load_library
+
+
+class RtxError(RuntimeError):
+    KINDS = {1: "zero_vec", 2: "color_gt1", 3: "domain", 4: "hip", 5: "rccl", 6: "invalid", 7: "nomem"}
+
+    def __init__(self, status, msg):
+        super().__init__("%s (rtx_status %d)" % (msg, status))
+        self.status = status
+        self.kind = self.KINDS.get(status, "unknown")
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Renderer:
+    def __init__(self, scene, camera, device=0):
+        """scene: config.SceneDescriptor; camera: _abi.CameraDesc."""
+        self.lib = load_library()
+        self.h = C.c_void_p()
+        st = self.lib.rtx_context_create(device, C.byref(self.h))
+        if st:
+            raise RtxError(st, "rtx_context_create failed")
+        self.device = device
+        self._scene = scene
+        self.camera = camera
+        self._check(self.lib.rtx_scene_upload(self.h, C.byref(scene.desc)))
+        self._check(self.lib.rtx_camera_set(self.h, C.byref(camera)))
+
+    # ------------------------------------------------------------ plumbing
+    def _check(self, st):
+        if st:
+            raise RtxError(st, self.lib.rtx_last_error(self.h).decode())
+
+    def close(self):
+        if self.h:
+            self.lib.rtx_context_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def width(self):
+        return self.camera.width
+
+    @property
+    def height(self):
+        return self.camera.height
+
+    def set_camera(self, camera):
+        self.camera = camera
+        self._check(self.lib.rtx_camera_set(self.h, C.byref(camera)))
+
+    def set_option(self, key, value):
+        self._check(self.lib.rtx_set_option(self.h, key.encode(), int(value)))
+
+    # ------------------------------------------------------------ host API
+    def render(self, x0=0, y0=0, x1=None, y1=None, seed=1):
+        """Float64 framebuffer [y1-y0, x1-x0, 3] (row = y, top first)."""
+        x1 = self.width if x1 is None else x1
+        y1 = self.height if y1 is None else y1
+        out = np.empty((y1 - y0, x1 - x0, 3), np.float64)
+        self._check(self.lib.rtx_render(self.h, x0, y0, x1, y1, seed, _dp(out), (x1 - x0) * 3))
+        return out
+
+    def render_at(self, x, y, seed=1):
+        out = np.empty(3, np.float64)
+        self._check(self.lib.rtx_render_at(self.h, x, y, seed, _dp(out)))
+        return out
+
+    def trace(self, rays, keys, seed=1):
+        rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)
+        keys = np.ascontiguousarray(keys, np.int32).reshape(-1, 3)
+        out = np.empty((len(rays), 3), np.float64)
+        self._check(self.lib.rtx_trace(self.h, len(rays), _dp(rays),
+                                       keys.ctypes.data_as(C.POINTER(C.c_int32)), seed, _dp(out)))
+        return out
+
+    def count_work(self, seed=1):
+        cnt = (C.c_uint64 * RTX_NCOUNT)()
+        self._check(self.lib.rtx_count_work(self.h, seed, cnt))
+        return dict(zip(COUNTER_NAMES, [int(v) for v in cnt]))
+
+    # ------------------------------------------------------------ device API
+    def render_device(self, d_out, seed=1, x0=0, y0=0, x1=None, y1=None, row_stride=None, stream=None):
+        x1 = self.width if x1 is None else x1
+        y1 = self.height if y1 is None else y1
+        row_stride = (x1 - x0) * 3 if row_stride is None else row_stride
+        self._check(self.lib.rtx_render_device(self.h, x0, y0, x1, y1, seed, C.c_void_p(d_out), row_stride,
+                                               C.c_void_p(stream or 0)))
+
+    def rows_per_rank(self, tile_rows, nranks):
+        return self.lib.rtx_tiles_rows_per_rank(self.height, tile_rows, nranks)
+
+    def render_tiles_device(self, d_packed, tile_rows, rank, nranks, seed=1, stream=None):
+        self._check(self.lib.rtx_render_tiles_device(self.h, tile_rows, rank, nranks, seed, C.c_void_p(d_packed),
+                                                     C.c_void_p(stream or 0)))
+
+    def sync(self, stream=None):
+        self._check(self.lib.rtx_sync(self.h, C.c_void_p(stream or 0)))
+
+    def quantize_device(self, d_rgb, d_rgba, png_gem_blend=True, stream=None, width=None, height=None):
+        w = self.width if width is None else width
+        h = self.height if height is None else height
+        st = self.lib.rtx_quantize_device(C.c_void_p(d_rgb), w, h, w * 3, int(png_gem_blend), C.c_void_p(d_rgba),
+                                          C.c_void_p(stream or 0))
+        if st:
+            raise RtxError(st, "rtx_quantize_device failed")
+
+
+def quantize(rgb, png_gem_blend=True):
+    """array_to_color + canvas point (camera.rb:105,153-156) on the GPU -> RGBA8 [H, W, 4]."""
+    lib = load_library()
+    rgb = np.ascontiguousarray(rgb, np.float64)
+    h, w, _ = rgb.shape
+    out = np.empty((h, w, 4), np.uint8)
+    st = lib.rtx_quantize(_dp(rgb), w, h, w * 3, int(png_gem_blend), out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    if st:
+        raise RtxError(st, "rtx_quantize failed")
+    return out
+
+
+def vec3_lib():
+    return load_library()
+
+
+__all__ = ["Renderer", "RtxError", "quantize", "_abi"]
