@@ -99,6 +99,23 @@ class Vec3:
     def __pos__(self):
         return Vec3(self.x, self.y, self.z)
 
+    # in-place forms recompute the cached r (Vec3_c_recalc_r, :226-273)
+    def add_bang(self, o):
+        self.__init__(self.x + o.x, self.y + o.y, self.z + o.z)
+        return self
+
+    def sub_bang(self, o):
+        self.__init__(self.x - o.x, self.y - o.y, self.z - o.z)
+        return self
+
+    def mul_bang(self, o):
+        if isinstance(o, Vec3):
+            self.__init__(self.x * o.x, self.y * o.y, self.z * o.z)
+        else:
+            o = float(o)
+            self.__init__(self.x * o, self.y * o, self.z * o)
+        return self
+
     def normalize(self):
         r = math.sqrt(self.x * self.x + self.y * self.y + self.z * self.z)
         if r == 0:

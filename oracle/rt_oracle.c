@@ -34,6 +34,8 @@
 
 #define EPS 1e-5 /* src/libs/algebra.rb:2 */
 
+static int rto_debug = -1;   /* RTO_DEBUG=1: trace leaves/areas to stderr (debugging only) */
+
 /* ------------------------------------------------------------ Vec3 (L0) */
 typedef struct { double x, y, z; } V;
 
@@ -177,7 +179,9 @@ void rto_destroy(Scene* s) {
   free(s);
 }
 
+static void dbg_init(void) { if (rto_debug < 0) rto_debug = getenv("RTO_DEBUG") != NULL; }
 Scene* rto_create(const rtx_scene_desc* sd, const rtx_camera_desc* cd, char* err, size_t errlen) {
+  dbg_init();
   Scene* s = (Scene*)calloc(1, sizeof(Scene));
   T t; memset(&t, 0, sizeof t);
   s->max_distance = sd->max_distance;
@@ -406,6 +410,7 @@ static V texcolor(const Tex* x, double hs, double vs, double uo, double vo, doub
   if (iu < 0) iu += x->w;
   if (iv < 0) iv += x->h;
   const double* p = &x->texel[((size_t)iv * x->w + iu) * 3];
+  if (rto_debug > 0) fprintf(stderr, "tex uv %.17g %.17g -> %ld %ld\n", uu, vv, iu, iv);
   return vmk(p[0], p[1], p[2]);
 }
 
@@ -421,6 +426,7 @@ static V local_lighting(const Obj* o, V pos, const Lit* lit, int nl, const Scene
     if (ldn > 1) ldn = 1.0;
     else if (ldn < 0) ldn = 0.0;
     lc = vadd(lc, vsc(lit[k].color, ldn));
+    if (rto_debug > 0) fprintf(stderr, "ldn %.17g lcol %.17g n %.17g %.17g %.17g\n", ldn, lit[k].color.x, n.x, n.y, n.z);
   }
   if (nl > 0) lc = vdiv(lc, (double)nl);
   if (has_filter) return vadd(vmul(vmul(lc, o->diffuse), filter), o->ambient);
@@ -469,6 +475,7 @@ static void push(Stack* st, Item it) {
 typedef struct { const Scene* s; uint64_t seed; int x, y, sample; Stack st; Lit* lit; } Tr;
 
 static void add_leaf(V* sum, V c, T* t) {                          /* ray_tracer.rb:292-298 */
+  if (rto_debug > 0) fprintf(stderr, "leaf %.17g %.17g %.17g\n", c.x, c.y, c.z);
   *sum = vadd(*sum, c);
   if (!(sum->x <= 1 && sum->y <= 1 && sum->z <= 1)) raise_(t, RTX_ECOLOR_GT1, "color greater than 1");
 }
@@ -526,6 +533,7 @@ static void rt_map(Tr* tr, Item it, V* sum, T* t) {                /* ray_tracer
   int nl = 0;
   for (int l = 0; l < s->nlight; l++) {
     double area = lit_area(s, target, s->light[l].pos, s->light[l].radius, t);
+    if (rto_debug > 0) fprintf(stderr, "area obj=%d %.17g target %.17g %.17g %.17g\n", oi, area, target.x, target.y, target.z);
     if (area > 0) {
       tr->lit[nl].light = l;
       tr->lit[nl].color = vsc(s->light[l].color, pow(area, s->sse) / s->nlight);

@@ -83,11 +83,10 @@ class Texture:
 
 
 def load_texture_rows(path):
+    import numpy as np
     from PIL import Image
-    im = Image.open(path).convert("RGB")
-    w, h = im.size
-    px = list(im.getdata())
-    return [px[r * w:(r + 1) * w] for r in range(h)]
+    a = np.asarray(Image.open(path).convert("RGB"))
+    return [[tuple(int(c) for c in px) for px in row] for row in a]
 
 
 # ---------------------------------------------------------------- objects

@@ -1,0 +1,99 @@
+"""Frame sharding across GPUs — the replacement of Camera#render_fork +
+fork_jobs (src/camera.rb:41-68, src/fork_jobs.rb:1-33).
+
+The reference forks N processes, gives child i the contiguous column band
+[floor(i/N*W), floor((i+1)/N*W)) and merges the children's JSON files.  Here
+the frame is cut into ``tile_rows``-row tiles dealt round-robin (tile t ->
+rank t % N, which balances glass/mirror-heavy regions that contiguous bands
+pile onto one child), each rank renders its tiles into a packed device buffer
+(``rtx_render_tiles_device``), and ONE gather over RCCL/xGMI brings the packed
+buffers to rank 0, which scatters the rows into the frame.  Pixels are
+independent and every pixel's result is keyed only by (seed, x, y, sample,
+path), so the frame is bit-identical for every N.
+"""
+
+import numpy as np
+
+DEFAULT_TILE_ROWS = 8
+
+
+def rows_per_rank(height, tile_rows, nranks):
+    tiles = (height + tile_rows - 1) // tile_rows
+    return ((tiles + nranks - 1) // nranks) * tile_rows
+
+
+def rank_rows(height, tile_rows, rank, nranks):
+    """Image row y of every packed row of `rank` (-1 = padding past the bottom)."""
+    n = rows_per_rank(height, tile_rows, nranks)
+    k = np.arange(n) // tile_rows
+    y = (k * nranks + rank) * tile_rows + np.arange(n) % tile_rows
+    y[y >= height] = -1
+    return y
+
+
+def unpack_index(height, tile_rows, nranks):
+    """For the rank-major concatenation of all packed buffers: (source row, image row) pairs."""
+    src, dst = [], []
+    n = rows_per_rank(height, tile_rows, nranks)
+    for r in range(nranks):
+        y = rank_rows(height, tile_rows, r, nranks)
+        keep = y >= 0
+        src.append(np.nonzero(keep)[0] + r * n)
+        dst.append(y[keep])
+    return np.concatenate(src), np.concatenate(dst)
+
+
+def unpack(gathered, height, tile_rows, nranks):
+    """gathered: [nranks * rows_per_rank, W, 3] (numpy or torch) -> frame [H, W, 3]."""
+    src, dst = unpack_index(height, tile_rows, nranks)
+    try:
+        import torch
+        if isinstance(gathered, torch.Tensor):
+            out = torch.empty((height,) + tuple(gathered.shape[1:]), dtype=gathered.dtype, device=gathered.device)
+            s = torch.as_tensor(src, device=gathered.device)
+            d = torch.as_tensor(dst, device=gathered.device)
+            out.index_copy_(0, d, gathered.index_select(0, s))
+            return out
+    except ImportError:
+        pass
+    out = np.empty((height,) + tuple(gathered.shape[1:]), dtype=gathered.dtype)
+    out[dst] = gathered[src]
+    return out
+
+
+class DistributedFrame:
+    """One rank's share of tile-sharded rendering + the RCCL gather to rank 0.
+
+    Needs an initialized torch.distributed process group (``nccl`` = RCCL on
+    ROCm, or ``gloo`` for CPU tests).  ``render_fn(packed)`` must fill this
+    rank's packed buffer ([rows_per_rank, W, 3] float64)."""
+
+    def __init__(self, width, height, tile_rows, rank, nranks, device):
+        import torch
+        self.width, self.height = width, height
+        self.tile_rows, self.rank, self.nranks = tile_rows, rank, nranks
+        self.rows = rows_per_rank(height, tile_rows, nranks)
+        self.packed = torch.zeros((self.rows, width, 3), dtype=torch.float64, device=device)
+        self.gathered = None
+        if rank == 0:
+            self.gathered = torch.zeros((nranks * self.rows, width, 3), dtype=torch.float64, device=device)
+            src, dst = unpack_index(height, tile_rows, nranks)
+            self.src = torch.as_tensor(src, device=device)
+            self.dst = torch.as_tensor(dst, device=device)
+            self.frame = torch.zeros((height, width, 3), dtype=torch.float64, device=device)
+
+    def gather(self):
+        """ONE collective: every rank's packed tiles to rank 0; rank 0 returns the frame."""
+        import torch.distributed as dist
+        if self.nranks == 1:
+            chunks = None
+            self.gathered = self.packed
+        elif self.rank == 0:
+            chunks = list(self.gathered.chunk(self.nranks, 0))
+            dist.gather(self.packed, chunks, dst=0)
+        else:
+            dist.gather(self.packed, None, dst=0)
+        if self.rank == 0:
+            self.frame.index_copy_(0, self.dst, self.gathered.index_select(0, self.src))
+            return self.frame
+        return None

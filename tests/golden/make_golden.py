@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures from the pure-Python restatement
+(oracle/rt_ref.py — a line-by-line restatement of the Ruby reference; the
+reference itself cannot run here: no Ruby interpreter).
+
+Fixtures (numpy .npz, data only):
+  frame_<name>.npz  float64 framebuffer [H, W, 3] + per-pixel raise status for a
+                    committed scene at a reduced size (scene YAML sha256 kept to
+                    detect drift)
+  vectors.npz       counter-RNG values, Camera#lens_func rays, trace_sync colours
+
+    python tests/golden/make_golden.py
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import rt_ref  # noqa: E402
+from oracle.rb_vec3 import RtxError  # noqa: E402
+from oracle.rng import rtx_rand  # noqa: E402
+
+SC = os.path.join(ROOT, "scenes")
+
+# name -> (world, camera, overrides)
+FRAMES = {
+    "c1_64x36": ("c1_world.yml", "c1_camera.yml", {"width": 64, "height": 36}),
+    "c0_48x27": ("c0_world.yml", "camera.yml", {"width": 48, "height": 27}),      # pre 3 / max 10: adaptive
+    "c2_32x18": ("c2_world.yml", "c2_camera.yml", {"width": 32, "height": 18}),
+    "mix_24x14": ("mix_world.yml", "mix_camera.yml", {"width": 24, "height": 14}),
+}
+
+
+def sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def render(world, camera, ov, seed=1):
+    w, cam = rt_ref.load_scene(os.path.join(SC, world), os.path.join(SC, camera), seed=seed, overrides=ov)
+    W, H = cam.width, cam.height
+    fb = np.zeros((H, W, 3), np.float64)
+    st = np.zeros((H, W), np.int32)
+    codes = {"zero_vec": 1, "color_gt1": 2, "domain": 3}
+    for x in range(W):
+        for y in range(H):
+            try:
+                fb[y, x] = cam.render_at(x, y).to_a()
+            except RtxError as e:
+                st[y, x] = codes[e.kind]
+    return fb, st
+
+
+def vectors():
+    rs = np.random.RandomState(5)
+    keys = np.stack([rs.randint(0, 4000, 300), rs.randint(0, 3000, 300), rs.randint(0, 16, 300),
+                     rs.randint(0, 2 ** 31, 300).astype(np.int64) * 977, rs.randint(0, 8, 300)], 1)
+    rng = np.array([rtx_rand(1, int(k[0]), int(k[1]), int(k[2]), int(k[3]), int(k[4])) for k in keys])
+    w, cam = rt_ref.load_scene(os.path.join(SC, "c2_world.yml"), os.path.join(SC, "c2_camera.yml"), seed=1)
+    pix = np.stack([rs.randint(0, 1920, 64), rs.randint(0, 1080, 64), rs.randint(0, 4, 64)], 1).astype(np.int32)
+    lens = []
+    for x, y, j in pix:
+        r = cam.lens_func(int(x), int(y), int(j))
+        lens.append(r.front.to_a() + r.position.to_a())
+    lens = np.array(lens)
+    trace = np.array([cam.ray_tracer.trace_sync(int(x), int(y), cam.lens_func(int(x), int(y), int(j)),
+                                                int(j)).to_a() for x, y, j in pix])
+    return dict(rng_keys=keys, rng=rng, lens_keys=pix, lens=lens, trace=trace,
+                scene_sha=sha(os.path.join(SC, "c2_world.yml")))
+
+
+def main(only=None):
+    for name, (world, camera, ov) in FRAMES.items():
+        if only and name not in only:
+            continue
+        fb, st = render(world, camera, ov)
+        np.savez_compressed(os.path.join(HERE, "frame_%s.npz" % name), frame=fb, status=st,
+                            world=world, camera=camera, overrides=repr(ov),
+                            scene_sha=sha(os.path.join(SC, world)), seed=1)
+        print(name, fb.shape, "errors", int((st != 0).sum()), "mean", fb.mean(axis=(0, 1)))
+    if not only or "vectors" in only:
+        np.savez_compressed(os.path.join(HERE, "vectors.npz"), **vectors())
+        print("vectors")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,121 @@
+"""The oracle itself: C restatement vs committed goldens (made by the Python
+restatement) and vs the Python restatement on fresh inputs — bit for bit."""
+
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, SCENES
+from oracle import rt_ref
+from oracle.c_oracle import Oracle, lib as oracle_lib
+from oracle.rng import child_path, rtx_rand
+from raytracing_rb_amd import config
+
+FRAMES = ["c1_64x36", "c0_48x27", "c2_32x18", "mix_24x14"]
+
+
+def _load(name):
+    z = np.load(os.path.join(GOLDEN, "frame_%s.npz" % name))      # allow_pickle=False
+    return z
+
+
+def _sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def _oracle_for(z):
+    ov = eval(str(z["overrides"]), {})                             # our own repr() of a small dict
+    sd, cd = config.load_scene(os.path.join(SCENES, str(z["world"])), os.path.join(SCENES, str(z["camera"])),
+                               camera_overrides=ov)
+    return Oracle(sd, cd), ov
+
+
+@pytest.mark.parametrize("name", FRAMES)
+def test_c_oracle_matches_golden(oracle_lib, name):
+    z = _load(name)
+    assert _sha(os.path.join(SCENES, str(z["world"]))) == str(z["scene_sha"]), "scene file drifted from fixture"
+    o, _ = _oracle_for(z)
+    fb, st, rc = o.render(seed=int(z["seed"]))
+    assert np.array_equal(st, z["status"])
+    assert np.array_equal(fb.view(np.uint64), z["frame"].view(np.uint64)), "C oracle != golden (bitwise)"
+
+
+@pytest.mark.parametrize("world,camera,ov", [
+    ("c2_world.yml", "c2_camera.yml", {"width": 20, "height": 12}),
+    ("c0_world.yml", "camera.yml", {"width": 24, "height": 14}),
+    ("mix_world.yml", "mix_camera.yml", {"width": 16, "height": 9}),
+])
+def test_python_and_c_restatements_agree_fresh_seed(oracle_lib, world, camera, ov):
+    seed = 12345
+    sd, cd = config.load_scene(os.path.join(SCENES, world), os.path.join(SCENES, camera), camera_overrides=ov)
+    fb, st, rc = Oracle(sd, cd).render(seed=seed)
+    _, cam = rt_ref.load_scene(os.path.join(SCENES, world), os.path.join(SCENES, camera), seed=seed, overrides=ov)
+    py = np.array(cam.render(), dtype=np.float64)
+    assert rc == 0
+    assert np.array_equal(py.view(np.uint64), fb.view(np.uint64))
+
+
+def test_rng_contract_three_implementations(oracle_lib):
+    from raytracing_rb_amd import _abi
+    L = _abi.load_library()
+    z = np.load(os.path.join(GOLDEN, "vectors.npz"))
+    for k, v in zip(z["rng_keys"], z["rng"]):
+        k = [int(a) for a in k]
+        assert rtx_rand(1, *k) == v
+        assert oracle_lib.lib().rto_rand(1, *k) == v
+        assert L.rtx_rand(1, *k) == v
+    assert 0.0 <= z["rng"].min() and z["rng"].max() < 1.0
+    assert child_path(1, 2, 1) == 6 and child_path(5, 3, 2) == 28
+
+
+def test_lens_and_trace_vectors(oracle_lib):
+    z = np.load(os.path.join(GOLDEN, "vectors.npz"))
+    assert _sha(os.path.join(SCENES, "c2_world.yml")) == str(z["scene_sha"])
+    sd, cd = config.load_scene(os.path.join(SCENES, "c2_world.yml"), os.path.join(SCENES, "c2_camera.yml"))
+    o = Oracle(sd, cd)
+    for (x, y, j), ray in zip(z["lens_keys"], z["lens"]):
+        assert np.array_equal(o.lens(int(x), int(y), int(j)), ray)
+    out, st, rc = o.trace(z["lens"], z["lens_keys"])
+    assert rc == 0
+    assert np.array_equal(out.view(np.uint64), z["trace"].view(np.uint64))
+
+
+def test_fork_baseline_equals_serial(oracle_lib):
+    sd, cd = config.load_scene(os.path.join(SCENES, "c2_world.yml"), os.path.join(SCENES, "c2_camera.yml"),
+                               camera_overrides={"width": 30, "height": 10})
+    o = Oracle(sd, cd)
+    a = o.render_fork(4, col_stride=1)
+    b, st, rc = o.render()
+    assert np.array_equal(a, b)
+    c = o.render_fork(3, col_stride=4)
+    assert np.array_equal(c[:, ::4], b[:, ::4])
+
+
+def _bright_scene(tmp_path):
+    """A scene violating the <= 1 bound: rt_reduce must raise (ray_tracer.rb:294-296)."""
+    src = open(os.path.join(SCENES, "c1_world.yml")).read()
+    src = src.replace("diffuse_rate:           [0.5, 0.5, 0.5]", "diffuse_rate:           [0.99, 0.99, 0.99]")
+    src = src.replace("ambient:                [0.05, 0.05, 0.05]", "ambient:                [0.3, 0.3, 0.3]", 1)
+    p = tmp_path / "bright.yml"
+    p.write_text(src)
+    return str(p)
+
+
+def test_color_gt1_raise_site(oracle_lib, tmp_path):
+    world = _bright_scene(tmp_path)
+    ov = {"width": 24, "height": 14}
+    sd, cd = config.load_scene(world, os.path.join(SCENES, "c1_camera.yml"), camera_overrides=ov)
+    fb, st, rc = Oracle(sd, cd).render()
+    assert rc == 2 and (st == 2).any()
+    _, cam = rt_ref.load_scene(world, os.path.join(SCENES, "c1_camera.yml"), overrides=ov)
+    pys = np.zeros_like(st)
+    for x in range(24):
+        for y in range(14):
+            try:
+                cam.render_at(x, y)
+            except Exception as e:
+                pys[y, x] = {"color_gt1": 2, "zero_vec": 1, "domain": 3}[e.kind]
+    assert np.array_equal(pys, st)
