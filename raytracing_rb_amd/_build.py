@@ -29,15 +29,16 @@ def stale():
     return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS + [__file__])
 
 
-def build(force=False, verbose=False):
-    if not force and not stale():
+def build(force=False, verbose=False, out=None, defines=()):
+    out = out or OUT
+    if not force and out == OUT and not stale():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp"] + SOURCES
+    cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-o", out + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

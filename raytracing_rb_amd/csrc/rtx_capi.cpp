@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+
+#include <cmath>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -27,12 +29,7 @@ struct rtx_context {
   int device = 0;
   std::string err;
   // device scene
-  ObjInfo* d_info = nullptr;
-  double* d_geo = nullptr;
-  Material* d_mat = nullptr;
-  LightDev* d_light = nullptr;
-  TexDev* d_tex = nullptr;
-  uint8_t* d_texels = nullptr;
+  std::vector<void*> d_bufs;         // every device allocation of the scene
   SceneDev scene{};
   SceneDev* d_scene = nullptr;
   bool have_scene = false;
@@ -68,18 +65,8 @@ static rtx_status fail(rtx_context* c, rtx_status s, const char* fmt, ...) {
   } while (0)
 
 static void free_scene(rtx_context* c) {
-  (void)hipFree(c->d_info);
-  (void)hipFree(c->d_geo);
-  (void)hipFree(c->d_mat);
-  (void)hipFree(c->d_light);
-  (void)hipFree(c->d_tex);
-  (void)hipFree(c->d_texels);
-  c->d_info = nullptr;
-  c->d_geo = nullptr;
-  c->d_mat = nullptr;
-  c->d_light = nullptr;
-  c->d_tex = nullptr;
-  c->d_texels = nullptr;
+  for (void* b : c->d_bufs) (void)hipFree(b);
+  c->d_bufs.clear();
   c->have_scene = false;
 }
 
@@ -183,10 +170,12 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
     return fail(c, RTX_EINVAL, "null array with nonzero count");
   hipSetDevice(c->device);
   uint32_t err = 0;
-  std::vector<ObjInfo> info(sd->n_objects);
+  std::vector<Run> runs;
   std::vector<Material> mat(sd->n_objects);
-  std::vector<double> geo;
-  int ns = 0, np = 0, nb = 0;
+  std::vector<Sphere64> sph64;
+  std::vector<float> sph32;
+  std::vector<double> planes, boxes;
+  float sph_scale = 0.0f;
   for (int i = 0; i < sd->n_objects; i++) {
     const rtx_object_desc& o = sd->objects[i];
     Material& m = mat[i];
@@ -200,17 +189,35 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
     m.tex = o.texture_id;
     m.hs = o.texture_horizontal_scale;
     m.vs = o.texture_vertical_scale;
+    m.type = o.type;
     if (o.texture_id >= sd->n_textures) return fail(c, RTX_EINVAL, "object %d: bad texture id", i);
-    info[i].type = o.type;
-    info[i].geo = (int32_t)geo.size();
+    if (o.type != RTX_SPHERE && o.type != RTX_PLANE && o.type != RTX_BOX)
+      return fail(c, RTX_EINVAL, "object %d: unknown type %d", i, o.type);
+    if (runs.empty() || runs.back().type != o.type) {
+      Run r;
+      r.type = o.type;
+      r.obj0 = i;
+      r.count = 0;
+      r.rec0 = o.type == RTX_SPHERE ? (int)sph64.size()
+             : o.type == RTX_PLANE ? (int)(planes.size() / PLANE_GEO) : (int)(boxes.size() / BOX_GEO);
+      runs.push_back(r);
+    }
+    runs.back().count++;
     if (o.type == RTX_SPHERE) {
       if (!o.has_refractive_rate) return fail(c, RTX_EINVAL, "object %d: sphere needs refractive_rate", i);
-      ns++;
-      const V3 C = v3p(o.center);
-      put3(geo, C);
-      geo.push_back(o.radius);
-      geo.push_back(o.radius * o.radius);
-      geo.push_back(fabs(C.x) + fabs(C.y) + fabs(C.z) + o.radius);
+      m.rec = (int)sph64.size();
+      Sphere64 sp;
+      set3(sp.c, v3p(o.center));
+      sp.r = o.radius;
+      sph64.push_back(sp);
+      // float32 pre-test record {cx, cy, cz, R^2}; scale = max(|C|_1 + R) (exact culls)
+      sph32.push_back((float)o.center[0]);
+      sph32.push_back((float)o.center[1]);
+      sph32.push_back((float)o.center[2]);
+      sph32.push_back((float)(o.radius * o.radius));
+      const double sc = fabs(o.center[0]) + fabs(o.center[1]) + fabs(o.center[2]) + fabs(o.radius);
+      const float scf = (float)(sc * (1.0 + 1e-6));
+      if (scf > sph_scale) sph_scale = scf;
       m.u_off = o.texture_u_offset;
       m.v_off = o.texture_v_offset;
       if (o.texture_id >= 0) {                     // sphere.rb:18, 113-115
@@ -220,25 +227,24 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
         set3(m.north_n, vnorm(north, err));
       }
     } else if (o.type == RTX_PLANE) {
-      np++;
-      put_plane(geo, v3p(o.point), v3p(o.front), v3p(o.up), o.u_unit, o.v_unit, err);
-    } else if (o.type == RTX_BOX) {                 // box.rb:15-73
-      nb++;
+      m.rec = (int)(planes.size() / PLANE_GEO);
+      put_plane(planes, v3p(o.point), v3p(o.front), v3p(o.up), o.u_unit, o.v_unit, err);
+    } else {                                         // box.rb:15-73
+      m.rec = (int)(boxes.size() / BOX_GEO);
       m.tex = -1;                                    // loaded, never used for shading
       const V3 P = v3p(o.point), F = v3p(o.front), U = v3p(o.up);
       const double wf = o.width_front, wu = o.width_up, wl = o.width_left;
       const V3 left = vnorm(vcross(F, U), err);
-      put_plane(geo, vadd(P, vsc(vsc(U, wu), 0.5)), U, left, wf, wl, err);
-      put_plane(geo, vsub(P, vsc(vsc(U, wu), 0.5)), vneg(U), left, wf, wl, err);
-      put_plane(geo, vadd(P, vsc(vsc(F, wf), 0.5)), F, U, wl, wu, err);
-      put_plane(geo, vsub(P, vsc(vsc(F, wf), 0.5)), vneg(F), U, wl, wu, err);
-      put_plane(geo, vadd(P, vsc(vsc(left, wl), 0.5)), left, U, wf, wu, err);
-      put_plane(geo, vsub(P, vsc(vsc(left, wl), 0.5)), vneg(left), U, wf, wu, err);
-    } else {
-      return fail(c, RTX_EINVAL, "object %d: unknown type %d", i, o.type);
+      put_plane(boxes, vadd(P, vsc(vsc(U, wu), 0.5)), U, left, wf, wl, err);
+      put_plane(boxes, vsub(P, vsc(vsc(U, wu), 0.5)), vneg(U), left, wf, wl, err);
+      put_plane(boxes, vadd(P, vsc(vsc(F, wf), 0.5)), F, U, wl, wu, err);
+      put_plane(boxes, vsub(P, vsc(vsc(F, wf), 0.5)), vneg(F), U, wl, wu, err);
+      put_plane(boxes, vadd(P, vsc(vsc(left, wl), 0.5)), left, U, wf, wu, err);
+      put_plane(boxes, vsub(P, vsc(vsc(left, wl), 0.5)), vneg(left), U, wf, wu, err);
     }
   }
   if (err) return fail(c, RTX_EZERO_VEC, "zero vector detected while building the scene");
+  if (!std::isfinite(sph_scale)) return fail(c, RTX_EINVAL, "non-finite sphere coordinates");
   std::vector<LightDev> lights(sd->n_lights);
   for (int i = 0; i < sd->n_lights; i++) {
     const rtx_light_desc& l = sd->lights[i];
@@ -272,34 +278,36 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
     texels.insert(texels.end(), t.rgb, t.rgb + (size_t)t.width * t.height * 3);
   }
   free_scene(c);
-  auto up = [&](void** dst, const void* src, size_t bytes) -> hipError_t {
-    if (bytes == 0) bytes = 16;
-    hipError_t e = hipMalloc(dst, bytes);
-    if (e == hipSuccess && src) e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+  auto up = [&](const void* src, size_t bytes, void** dst) -> hipError_t {
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+    if (e != hipSuccess) return e;
+    c->d_bufs.push_back(p);
+    if (bytes) e = hipMemcpy(p, src, bytes, hipMemcpyHostToDevice);
+    *dst = p;
     return e;
   };
-  geo.resize(geo.size() + 8, 0.0);
-  HIPCHK(c, up((void**)&c->d_info, info.data(), info.size() * sizeof(ObjInfo)));
-  HIPCHK(c, up((void**)&c->d_geo, geo.data(), geo.size() * sizeof(double)));
-  HIPCHK(c, up((void**)&c->d_mat, mat.data(), mat.size() * sizeof(Material)));
-  HIPCHK(c, up((void**)&c->d_light, lights.data(), lights.size() * sizeof(LightDev)));
-  HIPCHK(c, up((void**)&c->d_tex, tex.data(), tex.size() * sizeof(TexDev)));
-  HIPCHK(c, up((void**)&c->d_texels, texels.empty() ? nullptr : texels.data(), texels.size()));
   SceneDev& S = c->scene;
-  S.info = c->d_info;
-  S.geo = c->d_geo;
-  S.mat = c->d_mat;
-  S.light = c->d_light;
-  S.tex = c->d_tex;
-  S.texels = c->d_texels;
+  memset(&S, 0, sizeof S);
+  void* ptr;
+  HIPCHK(c, up(runs.data(), runs.size() * sizeof(Run), &ptr));           S.runs = (const Run*)ptr;
+  HIPCHK(c, up(sph64.data(), sph64.size() * sizeof(Sphere64), &ptr));    S.sph64 = (const Sphere64*)ptr;
+  HIPCHK(c, up(sph32.data(), sph32.size() * sizeof(float), &ptr));       S.sph32 = (const float*)ptr;
+  HIPCHK(c, up(planes.data(), planes.size() * sizeof(double), &ptr));    S.planes = (const double*)ptr;
+  HIPCHK(c, up(boxes.data(), boxes.size() * sizeof(double), &ptr));      S.boxes = (const double*)ptr;
+  HIPCHK(c, up(mat.data(), mat.size() * sizeof(Material), &ptr));        S.mat = (const Material*)ptr;
+  HIPCHK(c, up(lights.data(), lights.size() * sizeof(LightDev), &ptr));  S.light = (const LightDev*)ptr;
+  HIPCHK(c, up(tex.data(), tex.size() * sizeof(TexDev), &ptr));          S.tex = (const TexDev*)ptr;
+  HIPCHK(c, up(texels.data(), texels.size(), &ptr));                     S.texels = (const uint8_t*)ptr;
   S.n_obj = sd->n_objects;
   S.n_light = sd->n_lights;
-  S.n_sphere = ns;
-  S.n_plane = np;
-  S.n_box = nb;
-  S.n_geo = (int32_t)geo.size();
+  S.n_sphere = (int)sph64.size();
+  S.n_plane = (int)(planes.size() / PLANE_GEO);
+  S.n_box = (int)(boxes.size() / BOX_GEO);
+  S.n_runs = (int)runs.size();
   S.max_distance = sd->max_distance;
   S.sse = sd->soft_shadow_exponent;
+  S.sph_scale = sph_scale;
   S.sse_is_two = sd->soft_shadow_exponent == 2.0;     // glibc pow(x, 2.0) == x*x
   HIPCHK(c, hipMemcpy(c->d_scene, &S, sizeof S, hipMemcpyHostToDevice));
   c->have_scene = true;
@@ -355,7 +363,7 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
   if (!c->have_scene) return fail(c, RTX_EINVAL, "no scene uploaded");
   if (!c->have_cam) return fail(c, RTX_EINVAL, "no camera set");
   memset(&p, 0, sizeof p);
-  p.scene = c->d_scene;
+  p.scene = c->scene;
   p.cam = c->d_cam;
   p.seed = seed;
   p.err = c->d_err;
@@ -382,7 +390,7 @@ rtx_status rtx_render_device(rtx_context* c, int32_t x0, int32_t y0, int32_t x1,
   p.nrows = y1 - y0;
   p.out = d_out;
   p.stride = row_stride;
-  HIPCHK(c, launch_render(p, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
+  HIPCHK(c, launch_render(p, c->scene.n_sphere, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
   return RTX_OK;
 }
 
@@ -410,7 +418,7 @@ rtx_status rtx_render_tiles_device(rtx_context* c, int32_t tile_rows, int32_t ra
   p.nranks = nranks;
   p.out = d_packed;
   p.stride = (size_t)c->cam.width * 3;
-  HIPCHK(c, launch_render(p, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
+  HIPCHK(c, launch_render(p, c->scene.n_sphere, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
   return RTX_OK;
 }
 
@@ -488,7 +496,7 @@ rtx_status rtx_trace(rtx_context* c, int32_t n, const double* rays, const int32_
   HIPCHK(c, hipMemcpy(d_rays, rays, rb, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(d_keys, keys, kb, hipMemcpyHostToDevice));
   p.out = d_out;
-  HIPCHK(c, launch_trace(p, d_rays, d_keys, n, maxs, nullptr));
+  HIPCHK(c, launch_trace(p, c->scene.n_sphere, d_rays, d_keys, n, maxs, nullptr));
   HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
   return rtx_sync(c, nullptr);
 }
@@ -509,7 +517,7 @@ rtx_status rtx_count_work(rtx_context* c, uint64_t seed, uint64_t counts[RTX_NCO
   p.nrows = H;
   p.out = c->d_scratch;
   p.stride = (size_t)W * 3;
-  HIPCHK(c, launch_render(p, true, maxs, 2, nullptr));
+  HIPCHK(c, launch_render(p, c->scene.n_sphere, true, maxs, 2, nullptr));
   HIPCHK(c, hipDeviceSynchronize());
   unsigned long long tmp[RTX_NCOUNT];
   HIPCHK(c, hipMemcpy(tmp, c->d_counts, sizeof tmp, hipMemcpyDeviceToHost));

@@ -4,25 +4,30 @@
 //   Camera#lens_func  (src/camera.rb:129-151) thin-lens primary ray
 //   RayTracer#trace_sync / #rt_map (src/ray_tracer.rb:16-164, 292-298)
 //   World#intersect / #lit_area / #local_lights / #high_lights (src/world.rb:37-98)
-//   Sphere / Plane / Box / Texture (src/objects/*.rb)
+//   Sphere / Plane / Box / Texture (src/objects/{sphere,plane,box,texture}.rb)
 //
-// Design: one pixel per lane, binary64 everywhere, built with
-// -ffp-contract=off so every operation rounds exactly as the Ruby + C-extension
-// program does.  Each lane runs ONE flat loop over the work of its pixel —
-// pop a pending ray / start the next camera sample / finish the pixel — so a
-// lane whose sample tree is done immediately starts its next sample instead
-// of idling until the wave's deepest tree finishes.  The ray tree is walked
-// depth-first with the reference's LIFO order (children pushed reflection,
-// refraction, path-tracing rays; last pushed is processed first) on a
-// per-lane stack, and leaf colours are summed in emission order, which is the
-// reference's FIFO drain order (ray_tracer.rb:31-45), so sums are bit-exact.
+// Design: one pixel per lane, binary64 for every value the
+// reference computes, built with -ffp-contract=off so each operation rounds
+// exactly as the Ruby + C-extension program does.
 //
-// The scene loops (World#intersect over every object, World#lit_area over
-// every object per light) run in YAML order on a wave-uniform index, so the
-// object records are wave-uniform loads (scalar/broadcast).  Spheres that the
-// exact test would reject are skipped by a division-free conservative
-// pre-test whose margins are proven safe in DESIGN.md ("exact culls"); it
-// changes no bit of any result.
+// Each lane runs a small state machine.  Every loop iteration executes ONE
+// "query" — an ordered walk over all objects of the scene with one ray — for
+// every active lane at once: either the nearest-hit walk of World#intersect
+// (EXTEND) or the cover-area walk of World#lit_area for one light (SHADOW).
+// Both kinds run in the same object loop, so lanes at different stages of
+// their ray trees stay converged in the expensive part.  Between queries a
+// lane does its divergent-but-short work: pop the next ray of its tree (LIFO,
+// as RayTracer#trace_sync), start the next camera sample, the highlight test,
+// shading and child-ray generation.  The last child generated is kept in
+// registers (it is the next one the LIFO would pop); only its older siblings
+// go to the per-lane stack.  Leaf colours are summed in emission order —
+// the reference's FIFO drain order (ray_tracer.rb:31-45) — so sums are exact.
+//
+// Spheres are first tested with a float32 conservative pre-test from a
+// 16-byte record staged in LDS; only spheres it cannot rule out run the exact
+// binary64 Sphere#intersect.  The pre-test margins are proven in DESIGN.md
+// ("exact culls"): it never rejects a sphere the exact test would accept,
+// so it changes no bit of any result.
 #include <hip/hip_runtime.h>
 
 #include "rtx_launch.h"
@@ -33,6 +38,7 @@ namespace rtx {
 
 constexpr double PI = 3.141592653589793;   // Math::PI == M_PI
 constexpr double EPS = 1e-5;               // Alex::EPSILON (src/libs/algebra.rb:2)
+constexpr float CULL_M = 2e-5f;            // pre-test margin (exact culls)
 
 struct Ray {
   V3 o, d;                          // Alex::Ray#position, #front
@@ -46,91 +52,89 @@ struct Item {                       // one queue entry of RayTracer (ray_tracer.
   int32_t pad;
 };
 
-// Per-ray constants shared by every object test of the ray.
-struct RayC {
-  V3 o, d;
-  V3 dn;        // front.normalize (recomputed by the reference per call; same bits)
-  double r2;    // front.r2 = r*r
-  double dd;    // d.d, cull only
-  double so;    // |o|_1, cull only
-};
-
 enum { C_RAYS = 0, C_SPHERE_TESTS, C_SPHERE_HITS, C_PLANE_TESTS, C_BOX_TESTS, C_SHADE_HITS,
        C_COVER_SPHERE, C_COVER_PLANE, C_COVER_BOX, C_HIGHLIGHT_TESTS, C_PRIMARY, C_N };
 
-__device__ __forceinline__ RayC make_rayc(V3 o, V3 d) {
-  RayC c;
-  c.o = o;
-  c.d = d;
-  double r = vr(d);
-  c.r2 = r * r;
-  c.dn = r == 0 ? d : v3(d.x / r, d.y / r, d.z / r);
-  c.dd = vsq(d);
-  c.so = fabs(o.x) + fabs(o.y) + fabs(o.z);
-  return c;
+enum { M_NEED = 0, M_EXTEND = 1, M_SHADOW = 2, M_DONE = 3 };
+
+// Out-of-line the rarely-executed shading blocks (1) or inline everything (0).
+#ifndef RTX_OUTLINE_SHADING
+#define RTX_OUTLINE_SHADING 0
+#endif
+#if RTX_OUTLINE_SHADING
+#define RTX_SHADE_FN __device__ __noinline__
+#else
+#define RTX_SHADE_FN __device__ __forceinline__
+#endif
+
+// The scene is read-only for the whole launch: reading it through the constant
+// address space (4) lets wave-uniform indices become scalar loads (s_load) into
+// SGPRs instead of per-lane vector loads.
+#define RTX_CONST __attribute__((address_space(4)))
+template <typename T>
+__device__ __forceinline__ const RTX_CONST T* cptr(const T* p) {
+  return (const RTX_CONST T*)(p);
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+enum { SRC_PIXELS = 0, SRC_RAYS = 1 };
+
+__device__ __forceinline__ void seterr(uint32_t& err, uint32_t code) {
+  if (!err) err = code;
 }
 
 // ----------------------------------------------------------------- spheres
-// Exact Sphere#intersect (sphere.rb:60-85) preceded by the conservative cull.
-// Returns true and the hit point if the reference returns non-nil.
-__device__ __forceinline__ bool sphere_hit(const double* __restrict__ g, const RayC& rc, V3& hit,
-                                           bool& in, double& tq) {
-  const V3 C = v3(g[0], g[1], g[2]);
-  const double R = g[3];
-  const V3 oc = vsub(C, rc.o);                    // (center - ray.position)
-  const double q = vdot(oc, rc.d);                // .dot(ray.front)
-  const double s = vsq(oc);                       // == |position - center|^2, same bits
-  // cull 1: the ray's line misses the sphere by a margin (exact culls)
-  const double S = rc.so + g[5];
-  if (s * rc.dd - q * q > rc.dd * (g[4] + 1e-10 * (S * S))) return false;
-  // cull 2: sphere behind an origin that is outside it
-  if (q < -1e-200 && s > g[4] * (1.0 + 1e-9)) return false;
-  const double t = q / rc.r2;
-  const V3 np = vadd(rc.o, vsc(rc.d, t));
+// Exact Sphere#intersect (sphere.rb:60-85); r2 = front.r2, dn = front.normalize.
+__device__ __forceinline__ bool sphere_exact(V3 C, double R, V3 o, V3 d, V3 dn, double r2, V3& hit, bool& in) {
+  const V3 oc = vsub(C, o);                       // center - ray.position
+  const double q = vdot(oc, d);
+  const double t = q / r2;
+  const V3 np = vadd(o, vsc(d, t));
   const double nd = vr(vsub(np, C));
   if (!(nd <= R)) return false;                   // inner?(nearest_point)
   const double h = sqrt(R * R - nd * nd);         // radius**2 - nearest_dis**2
-  const V3 vec = vsc(rc.dn, h);
-  const bool from_inner = sqrt(s) <= R;           // inner?(ray.position)
+  const V3 vec = vsc(dn, h);
+  const bool from_inner = vr(oc) <= R;            // inner?(ray.position): |oc| has |o - C|'s bits
   in = !from_inner;
   hit = in ? vsub(np, vec) : vadd(np, vec);
   if (!from_inner && t < 0) return false;
-  tq = t;
   return true;
 }
 
 // ----------------------------------------------------------------- planes
 // Plane#intersect (plane.rb:38-51).  p = plane record (PLANE_GEO doubles).
-__device__ __forceinline__ bool plane_hit(const double* __restrict__ p, const RayC& rc, V3& hit) {
+template <typename P>
+__device__ __forceinline__ bool plane_hit(P p, V3 o, V3 d, V3& hit) {
   const V3 F = v3(p[3], p[4], p[5]);
-  const double den = vdot(F, rc.d);
+  const double den = vdot(F, d);
   if (den == 0) return false;
-  const double t = vdot(vsub(v3(p[0], p[1], p[2]), rc.o), F) / den;
-  hit = vadd(rc.o, vsc(rc.d, t));
+  const double t = vdot(vsub(v3(p[0], p[1], p[2]), o), F) / den;
+  hit = vadd(o, vsc(d, t));
   if (t < 0) return false;
   return true;
 }
 
-__device__ __forceinline__ void plane_uv(const double* __restrict__ p, V3 pos, double& u, double& v) {
+template <typename P>
+__device__ __forceinline__ void plane_uv(P p, V3 pos, double& u, double& v) {
   const V3 a = vsub(pos, v3(p[0], p[1], p[2]));   // plane.rb:81-85
   u = vdot(a, v3(p[6], p[7], p[8])) / p[12];
   v = vdot(a, v3(p[9], p[10], p[11])) / p[13];
 }
 
 // Box#intersect (box.rb:79-97): nearest face hit inside its u,v square.
-__device__ __forceinline__ bool box_hit(const double* __restrict__ b, const RayC& rc, V3& hit, int& face) {
+template <typename P>
+__device__ __forceinline__ bool box_hit(P b, V3 o, V3 d, V3& hit, int& face) {
   double nearest = __builtin_inf();
   bool found = false;
   for (int i = 0; i < 6; i++) {
-    const double* p = b + i * PLANE_GEO;
+    const P p = b + i * PLANE_GEO;
     V3 h;
-    if (plane_hit(p, rc, h)) {
+    if (plane_hit(p, o, d, h)) {
       double u, v;
       plane_uv(p, h, u, v);
       if (-0.5 <= u && u <= 0.5 && -0.5 <= v && v <= 0.5) {
-        const double d = vr(vsub(h, rc.o));
-        if (d < nearest) {
-          nearest = d;
+        const double dd = vr(vsub(h, o));
+        if (dd < nearest) {
+          nearest = dd;
           hit = h;
           face = i;
           found = true;
@@ -141,69 +145,125 @@ __device__ __forceinline__ bool box_hit(const double* __restrict__ b, const RayC
   return found;
 }
 
-// ----------------------------------------------------------------- errors
-__device__ __forceinline__ void seterr(uint32_t& err, uint32_t code) {
-  if (!err) err = code;
+// Sphere#cover_area's penumbra (sphere.rb:31-56) once the binary factor is 1.
+RTX_SHADE_FN double penumbra(V3 C, double R, V3 T, V3 lt, double radius, uint32_t& err) {
+  const double t = vdot(vsub(C, T), lt) / vr2(lt);
+  const V3 x1 = vadd(T, vsc(lt, t));
+  const double r1 = radius * (vr(vsub(x1, T)) / vr(lt));
+  const double d = vr(vsub(x1, C));
+  if (d >= r1 + R) return 0.0;
+  const double s1 = PI * r1 * r1;
+  if (d > fabs(R - r1)) {
+    double c1 = (r1 * r1 + d * d - R * R) / (2.0 * r1 * d);
+    double c2 = (R * R + d * d - r1 * r1) / (2.0 * R * d);
+    if (c1 > 1.0) c1 = 1.0;
+    if (c2 > 1.0) c2 = 1.0;
+    if (c1 < -1.0 || c2 < -1.0) seterr(err, ERR_DOMAIN);     // Math::DomainError
+    const double th1 = acos(c1), th2 = acos(c2);
+    const double ds = ((th1 - sin(th1)) * r1 * r1 + (th2 - sin(th2)) * R * R) / 2.0;
+    return 1.0 * ds / s1;
+  }
+  if (r1 > R) return 1.0 * PI * R * R / s1;
+  return 1.0;
 }
 
-// ----------------------------------------------------------------- lit_area
-// World#lit_area (world.rb:62-69) for target T and light L: 1 - sum of
-// cover_area over every object in YAML order, clamped at 0.  Objects whose
-// cover is zero are skipped (subtracting 0 is exact).
+// ----------------------------------------------------------------- the query
+// One ordered walk over every object with ray (o, d), for every active lane.
+//   EXTEND: World#intersect — nearest hit (strict <, YAML order) -> best/besti.
+//   SHADOW: World#lit_area for light L (o = target T, d = L - T) -> total
+//           (1 - ordered sum of cover areas; zero covers skipped: exact).
 template <bool COUNT>
-__device__ double lit_area(const SceneDev& S, V3 T, V3 L, double radius, uint32_t& err,
-                           unsigned long long* cnt) {
-  const RayC rc = make_rayc(T, vsub(L, T));      // Ray(light - target, target)
-  const V3 TL = vsub(T, L);
-  double total = 1.0;
+__device__ __forceinline__ void query(const SceneDev& S, const float4* __restrict__ sph, bool ext, V3 o, V3 d,
+                                      V3 L, double radius, double& best, int& besti, double& total,
+                                      uint32_t& err, unsigned long long* cnt) {
+  const double r = vr(d);
+  const double r2 = r * r;                        // front.r2
+  const V3 dn = r == 0 ? d : v3(d.x / r, d.y / r, d.z / r);   // front.normalize
+  // float32 pre-test constants (exact culls)
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float dd = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+  const float Sx = fabsf(ox) + fabsf(oy) + fabsf(oz) + S.sph_scale;
+  const float ms2 = CULL_M * Sx * Sx;
+  const float kline = dd * ms2;
+  const float qneg = -CULL_M * Sx * sqrtf(dd);
   if (COUNT) {
-    cnt[C_COVER_SPHERE] += S.n_sphere;
-    cnt[C_COVER_PLANE] += S.n_plane;
-    cnt[C_COVER_BOX] += S.n_box;
-  }
-  for (int i = 0; i < S.n_obj; i++) {
-    const ObjInfo oi = S.info[i];
-    const double* __restrict__ g = S.geo + oi.geo;
-    V3 hit;
-    if (oi.type == OBJ_SPHERE) {
-      bool in;
-      double tq;
-      if (!sphere_hit(g, rc, hit, in, tq)) continue;
-      if (!(vdot(vsub(hit, L), TL) > 0)) continue;             // factor == 0
-      // Sphere#cover_area penumbra (sphere.rb:31-56), factor == 1
-      const V3 C = v3(g[0], g[1], g[2]);
-      const double R = g[3];
-      const V3 lt = rc.d;
-      const double t = vdot(vsub(C, T), lt) / vr2(lt);
-      const V3 x1 = vadd(T, vsc(lt, t));
-      const double r1 = radius * (vr(vsub(x1, T)) / vr(lt));
-      const double d = vr(vsub(x1, C));
-      if (d >= r1 + R) continue;
-      const double s1 = PI * r1 * r1;
-      double cover;
-      if (d > fabs(R - r1)) {
-        double c1 = (r1 * r1 + d * d - R * R) / (2.0 * r1 * d);
-        double c2 = (R * R + d * d - r1 * r1) / (2.0 * R * d);
-        if (c1 > 1.0) c1 = 1.0;
-        if (c2 > 1.0) c2 = 1.0;
-        if (c1 < -1.0 || c2 < -1.0) seterr(err, ERR_DOMAIN);   // Math::DomainError
-        const double th1 = acos(c1), th2 = acos(c2);
-        const double ds = ((th1 - sin(th1)) * r1 * r1 + (th2 - sin(th2)) * R * R) / 2.0;
-        cover = 1.0 * ds / s1;
-      } else if (r1 > R) {
-        cover = 1.0 * PI * R * R / s1;
-      } else {
-        cover = 1.0;
-      }
-      total -= cover;
-    } else if (oi.type == OBJ_PLANE) {
-      if (plane_hit(g, rc, hit) && vdot(vsub(hit, L), TL) > 0) total -= 1.0;
+    if (ext) {
+      cnt[C_SPHERE_TESTS] += S.n_sphere;
+      cnt[C_PLANE_TESTS] += S.n_plane;
+      cnt[C_BOX_TESTS] += S.n_box;
     } else {
-      int face;
-      if (box_hit(g, rc, hit, face) && vdot(vsub(hit, L), TL) > 0) total -= 1.0;
+      cnt[C_COVER_SPHERE] += S.n_sphere;
+      cnt[C_COVER_PLANE] += S.n_plane;
+      cnt[C_COVER_BOX] += S.n_box;
     }
   }
-  return total > 0 ? total : 0.0;
+  const RTX_CONST Run* runs = cptr(S.runs);
+  const RTX_CONST Sphere64* sph64 = cptr(S.sph64);
+  const int n_runs = uni(S.n_runs);
+  for (int ri = 0; ri < n_runs; ri++) {
+    Run run;
+    run.type = uni(runs[ri].type);
+    run.obj0 = uni(runs[ri].obj0);
+    run.count = uni(runs[ri].count);
+    run.rec0 = uni(runs[ri].rec0);
+    if (run.type == OBJ_SPHERE) {
+      for (int k = 0; k < run.count; k++) {
+        const float4 c = sph[run.rec0 + k];        // {cx, cy, cz, R^2}, wave-uniform
+        const float ocx = c.x - ox, ocy = c.y - oy, ocz = c.z - oz;
+        const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+        const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
+        const bool miss_line = __builtin_fmaf(s, dd, -q * q) > __builtin_fmaf(dd, c.w, kline);
+        const bool behind = q < qneg && s > c.w + ms2;
+        if (miss_line || behind) continue;
+        const RTX_CONST Sphere64& sp = sph64[run.rec0 + k];
+        const V3 C = v3(sp.c[0], sp.c[1], sp.c[2]);
+        const double sr = sp.r;
+        V3 hit;
+        bool in;
+        if (!sphere_exact(C, sr, o, d, dn, r2, hit, in)) continue;
+        if (ext) {
+          if (COUNT) cnt[C_SPHERE_HITS]++;
+          const double dist = vr(vsub(o, hit));    // Ray#distance
+          if (dist < best) {
+            best = dist;
+            besti = run.obj0 + k;
+          }
+        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
+          total -= penumbra(C, sr, o, d, radius, err);
+        }
+      }
+    } else if (run.type == OBJ_PLANE) {
+      for (int k = 0; k < run.count; k++) {
+        V3 hit;
+        if (!plane_hit(cptr(S.planes) + (size_t)(run.rec0 + k) * PLANE_GEO, o, d, hit)) continue;
+        if (ext) {
+          const double dist = vr(vsub(o, hit));
+          if (dist < best) {
+            best = dist;
+            besti = run.obj0 + k;
+          }
+        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {
+          total -= 1.0;
+        }
+      }
+    } else {
+      for (int k = 0; k < run.count; k++) {
+        V3 hit;
+        int face;
+        if (!box_hit(cptr(S.boxes) + (size_t)(run.rec0 + k) * BOX_GEO, o, d, hit, face)) continue;
+        if (ext) {
+          const double dist = vr(vsub(o, hit));
+          if (dist < best) {
+            best = dist;
+            besti = run.obj0 + k;
+          }
+        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {
+          total -= 1.0;
+        }
+      }
+    }
+  }
 }
 
 // ----------------------------------------------------------------- shading
@@ -259,10 +319,38 @@ __device__ __forceinline__ V3 vertical_vector(V3 n, uint32_t& err) {   // world_
   return v3(-(n.y + n.z) / n.x, 1.0, 1.0);
 }
 
-struct Pixel {
-  uint64_t seed;
-  int32_t x, y, sample;
-};
+// Geometry of the winning hit: position, delta, normal n and the :in flag of
+// intersect_parameters (sphere.rb:60-101, plane.rb:38-67, box.rb:100-105).
+// Re-evaluated with the same operations as in the walk, hence the same bits.
+RTX_SHADE_FN void hit_info(const SceneDev& S, int obj, const Ray& ray, V3& hit, V3& delta, V3& n,
+                                      bool& in) {
+  const Material& m = S.mat[obj];
+  in = true;
+  if (m.type == OBJ_SPHERE) {
+    const Sphere64 sp = S.sph64[m.rec];
+    const V3 C = v3p(sp.c);
+    const double r = vr(ray.d);
+    const V3 dn = r == 0 ? ray.d : v3(ray.d.x / r, ray.d.y / r, ray.d.z / r);
+    sphere_exact(C, sp.r, ray.o, ray.d, dn, r * r, hit, in);
+    delta = vsc(vsc(vsub(hit, C), EPS), in ? 1.0 : -1.0);
+    n = in ? vsub(hit, C) : vsub(C, hit);
+    return;
+  }
+  const double* plane;
+  if (m.type == OBJ_PLANE) {
+    plane = S.planes + (size_t)m.rec * PLANE_GEO;
+    plane_hit(plane, ray.o, ray.d, hit);
+  } else {
+    int face = 0;
+    box_hit(S.boxes + (size_t)m.rec * BOX_GEO, ray.o, ray.d, hit, face);
+    plane = S.boxes + (size_t)m.rec * BOX_GEO + face * PLANE_GEO;
+  }
+  const V3 F = v3(plane[3], plane[4], plane[5]);
+  const double fd = vdot(F, ray.d);
+  const double nfd = -fd;
+  delta = vsc(vsc(F, EPS), nfd > 0 ? 1.0 : (nfd < 0 ? -1.0 : 0.0));   // (-f.d <=> 0).to_f
+  n = fd > 0 ? vneg(F) : F;
+}
 
 template <int MAXS>
 struct Stack {
@@ -270,45 +358,128 @@ struct Stack {
   int n;
 };
 
-// Push a child unless rt_map would discard it on pop (ray_tracer.rb:52):
-// skipping a dead item changes nothing (no leaf, no RNG draw).
-template <int MAXS>
-__device__ __forceinline__ void push_child(Stack<MAXS>& st, const Ray& r, V3 att, uint64_t path, int depth) {
-  if (depth <= 0 || vr(att) < 0.0001) return;
-  if (st.n < MAXS) {
-    Item& it = st.a[st.n++];
-    it.ray = r;
-    it.att = att;
-    it.path = path;
-    it.depth = depth;
-  }
-}
-
 __device__ __forceinline__ void add_leaf(V3& sum, V3 c, uint32_t& err) {   // ray_tracer.rb:292-298
   sum = vadd(sum, c);
   if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) seterr(err, ERR_COLOR_GT1);
 }
 
-// RayTracer#rt_map (ray_tracer.rb:50-164) for one live item: leaves go into
-// `sum`, children onto the stack.
-template <bool COUNT, int MAXS>
-__device__ void rt_map(const SceneDev& S, const CameraDev& cam, const Pixel& px, const Item& it,
-                       Stack<MAXS>& st, V3& sum, uint32_t& err, unsigned long long* cnt) {
-  if (it.depth <= 0 || vr(it.att) < 0.0001) return;
-  if (COUNT) {
-    cnt[C_RAYS]++;
-    cnt[C_HIGHLIGHT_TESTS] += S.n_light;
+// Children are generated in the reference's push order; the most recent live
+// one is held in `pend` (it is what Array#pop returns next) and only older
+// siblings are written to the stack.  A child rt_map would discard on pop
+// (ray_tracer.rb:52) is dropped here: no leaf, no RNG draw, no effect.
+template <int MAXS>
+__device__ __forceinline__ void emit(Stack<MAXS>& st, Item& pend, bool& has, uint32_t& err, const Ray& r,
+                                     V3 att, uint64_t path, int depth) {
+  if (depth <= 0 || vr(att) < 0.0001) return;
+  if (has) {
+    if (st.n < MAXS) st.a[st.n++] = pend;
+    else seterr(err, ERR_DOMAIN);                // cannot happen: stack sized on the host
   }
-  const Ray& ray = it.ray;
-  // ---- World#high_lights (world.rb:83-98); the `&& lit_area(...)` is always
-  // truthy in Ruby and is not evaluated.
+  pend.ray = r;
+  pend.att = att;
+  pend.path = path;
+  pend.depth = depth;
+  has = true;
+}
+
+// The rest of rt_map once every light's lit area is known (ray_tracer.rb:80-158):
+// reflection / refraction children, then path-tracing children (no lit light)
+// or the local-lighting leaf.  Returns true with the next ray in `cur`.
+template <int MAXS>
+RTX_SHADE_FN bool shade_finish(const SceneDev& S, const CameraDev& cam, uint64_t seed, int x, int y,
+                                          int sample, int obj, bool in, V3 hit, V3 delta, V3 n, V3 lc, int nl,
+                                          Item& cur, Stack<MAXS>& st, V3& sum, uint32_t& err) {
+  const Material& m = S.mat[obj];
+  Item pend;
+  bool has = false;
+  const uint64_t R = (uint64_t)cam.pt + 3;
+  const Ray refl = reflection(cur.ray, n, hit, delta, err);
+  emit<MAXS>(st, pend, has, err, refl, vmul(cur.att, v3p(m.refl_att)), cur.path * R + 1, cur.depth - 1);
+  Ray refr;
+  bool has_refr = false;
+  if (m.type == OBJ_SPHERE)                                  // sphere.rb:92-94: rate inverted leaving
+    has_refr = refraction(cur.ray, n, hit, refl.d, in ? m.rr : 1.0 / m.rr, refr, err);
+  else if (m.has_rr)                                         // plane.rb:57-61: same rate both ways
+    has_refr = refraction(cur.ray, n, hit, refl.d, m.rr, refr, err);
+  if (has_refr)
+    emit<MAXS>(st, pend, has, err, refr, vmul(cur.att, v3p(m.refr_att)), cur.path * R + 2, cur.depth - 1);
+  if (nl == 0) {
+    // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
+    const int pt = cam.pt;
+    const V3 att = vmul(cur.att, vdiv(v3p(m.diffuse), (double)pt));
+    const V3 front = vnorm(n, err);
+    const V3 left = vnorm(vertical_vector(n, err), err);
+    const V3 up = vcross(front, left);
+    Ray r;
+    r.o = vadd(hit, delta);
+    for (int k = 0; k < pt; k++) {
+      const double theta = rand01(seed, x, y, sample, cur.path, 2 * k) * PI / 2.0;
+      const double phi = rand01(seed, x, y, sample, cur.path, 2 * k + 1) * PI * 2.0;
+      r.d = vadd(vsc(front, sin(theta)), vsc(vadd(vsc(left, cos(phi)), vsc(up, sin(phi))), cos(theta)));
+      emit<MAXS>(st, pend, has, err, r, att, cur.path * R + 3 + (uint64_t)k, cur.depth - 1);
+    }
+  } else {
+    lc = vdiv(lc, (double)nl);
+    V3 color;
+    if (m.type == OBJ_BOX) {
+      color = vadd(vmul(lc, v3p(m.diffuse)), v3p(m.ambient));
+    } else {
+      V3 filter = v3(1.0, 1.0, 1.0);
+      if (m.tex >= 0) {
+        if (m.type == OBJ_SPHERE) {                   // Sphere#get_uv (sphere.rb:111-120)
+          const Sphere64 sp = S.sph64[m.rec];
+          const V3 vec = vsub(hit, v3p(sp.c));
+          const double x0 = vdot(vec, v3p(m.gw_n)) / sp.r;
+          const double y0 = vdot(vec, v3p(m.east_n)) / sp.r;
+          const double z0 = vdot(vec, v3p(m.north_n)) / sp.r;
+          const double mm2 = x0 * x0 + y0 * y0 + z0 * z0 + 2.0 * x0 + 1.0;
+          if (mm2 < 0) seterr(err, ERR_DOMAIN);
+          const double mm = sqrt(mm2);
+          filter = vmul(texcolor(S, m.tex, m.hs, m.vs, m.u_off, m.v_off, (y0 / mm + 1.0) / 2.0,
+                                 (-z0 / mm + 1.0) / 2.0, err), filter);
+        } else {
+          double u, v;
+          plane_uv(S.planes + (size_t)m.rec * PLANE_GEO, hit, u, v);
+          filter = vmul(texcolor(S, m.tex, m.hs, m.vs, 0.0, 0.0, u, v, err), filter);
+        }
+      }
+      color = vadd(vmul(vmul(lc, v3p(m.diffuse)), filter), v3p(m.ambient));
+    }
+    add_leaf(sum, vmul(cur.att, color), err);
+  }
+  if (has) cur = pend;
+  return has;
+}
+
+// Camera#lens_func (camera.rb:129-151) with the per-camera constants hoisted.
+__device__ __forceinline__ Ray lens(const CameraDev& c, int x, int y, int j, uint64_t seed) {
+  const V3 rp = vadd(vadd(v3p(c.retina_center), vsc(v3p(c.left), 2.0 * ((double)x / c.width - 0.5) * c.retina_width)),
+                     vsc(v3p(c.up_n), 2.0 * ((double)y / c.height - 0.5) * c.retina_height));
+  const double theta = rand01(seed, x, y, j, 0, 0);
+  const V3 rv = vsc(vadd(vsc(v3p(c.left_n), cos(theta)), vsc(v3p(c.up_n), sin(theta))), c.aperture_radius);
+  const V3 pos = v3p(c.pos);
+  const V3 ap = vadd(pos, rv);
+  const V3 rd = vsub(pos, rp);                                  // Ray(position - retina, retina)
+  const double t = vdot(vsub(v3p(c.pofp), rp), v3p(c.front)) / vdot(v3p(c.front), rd);
+  const V3 target = vadd(rp, vsc(rd, t));
+  Ray r;
+  r.o = ap;
+  r.d = vsub(target, ap);
+  return r;
+}
+
+// World#high_lights (world.rb:83-98) for `ray`; fired leaves go into `sum`.
+// Returns true if any light fired (the ray then stops, ray_tracer.rb:77).
+// The `&& lit_area(...)` is always truthy in Ruby and is not evaluated.
+__device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3& sum, uint32_t& err) {
   uint32_t fired = 0;
   int nfired = 0;
+  const RTX_CONST LightDev* lights = cptr(S.light);
   for (int l = 0; l < S.n_light; l++) {
-    const LightDev& L = S.light[l];
-    const V3 a = vsub(v3p(L.pos), ray.o);
-    const double dot = vdot(ray.d, a);
-    const double r1 = vsq(ray.d), r2 = vsq(a);
+    const RTX_CONST LightDev& L = lights[l];
+    const V3 a = vsub(v3(L.pos[0], L.pos[1], L.pos[2]), it.ray.o);
+    const double dot = vdot(it.ray.d, a);
+    const double r1 = vsq(it.ray.d), r2 = vsq(a);
     if (r1 == 0 || r2 == 0) {
       seterr(err, ERR_ZERO_VEC);
       continue;
@@ -332,168 +503,13 @@ __device__ void rt_map(const SceneDev& S, const CameraDev& cam, const Pixel& px,
       nfired++;
     }
   }
-  if (nfired) {
-    for (int l = 0; l < S.n_light; l++) {
-      if (!(fired >> l & 1)) continue;
-      const LightDev& L = S.light[l];
-      add_leaf(sum, vdiv(vmul(it.att, vsc(v3p(L.color), L.hl_rate)), (double)nfired), err);
-    }
-    return;
-  }
-  // ---- World#intersect (world.rb:37-59): nearest hit, YAML order, strict <.
-  const RayC rc = make_rayc(ray.o, ray.d);
-  double best = S.max_distance;
-  int besti = -1;
-  if (COUNT) {
-    cnt[C_SPHERE_TESTS] += S.n_sphere;
-    cnt[C_PLANE_TESTS] += S.n_plane;
-    cnt[C_BOX_TESTS] += S.n_box;
-  }
-  for (int i = 0; i < S.n_obj; i++) {
-    const ObjInfo oi = S.info[i];
-    const double* __restrict__ g = S.geo + oi.geo;
-    V3 hit;
-    bool ok;
-    if (oi.type == OBJ_SPHERE) {
-      bool in;
-      double tq;
-      ok = sphere_hit(g, rc, hit, in, tq);
-      if (COUNT && ok) cnt[C_SPHERE_HITS]++;
-    } else if (oi.type == OBJ_PLANE) {
-      ok = plane_hit(g, rc, hit);
-    } else {
-      int face;
-      ok = box_hit(g, rc, hit, face);
-    }
-    if (ok) {
-      const double d = vr(vsub(rc.o, hit));         // Ray#distance
-      if (d < best) {
-        best = d;
-        besti = i;
-      }
-    }
-  }
-  if (besti < 0) return;                            // "light_dead": contributes nothing
-  if (COUNT) cnt[C_SHADE_HITS]++;
-  // ---- re-evaluate the winner fully (same operations => same bits)
-  const ObjInfo oi = S.info[besti];
-  const double* __restrict__ g = S.geo + oi.geo;
-  const Material& m = S.mat[besti];
-  V3 hit, delta, n;
-  Ray refl, refr;
-  bool has_refr;
-  const double* plane = nullptr;
-  if (oi.type == OBJ_SPHERE) {                      // sphere.rb:60-101
-    bool in;
-    double tq;
-    sphere_hit(g, rc, hit, in, tq);
-    const V3 C = v3(g[0], g[1], g[2]);
-    delta = vsc(vsc(vsub(hit, C), EPS), in ? 1.0 : -1.0);
-    n = in ? vsub(hit, C) : vsub(C, hit);
-    refl = reflection(ray, n, hit, delta, err);
-    has_refr = refraction(ray, n, hit, refl.d, in ? m.rr : 1.0 / m.rr, refr, err);
-  } else {                                          // plane.rb:38-67, box.rb:100-105
-    if (oi.type == OBJ_PLANE) {
-      plane = g;
-      plane_hit(g, rc, hit);
-    } else {
-      int face = 0;
-      box_hit(g, rc, hit, face);
-      plane = g + face * PLANE_GEO;
-    }
-    const V3 F = v3(plane[3], plane[4], plane[5]);
-    const double fd = vdot(F, ray.d);
-    const double nfd = -fd;
-    delta = vsc(vsc(F, EPS), nfd > 0 ? 1.0 : (nfd < 0 ? -1.0 : 0.0));   // (-f.d <=> 0).to_f
-    n = fd > 0 ? vneg(F) : F;
-    refl = reflection(ray, n, hit, delta, err);
-    has_refr = m.has_rr ? refraction(ray, n, hit, refl.d, m.rr, refr, err) : false;
-  }
-  const uint64_t R = (uint64_t)cam.pt + 3;
-  push_child<MAXS>(st, refl, vmul(it.att, v3p(m.refl_att)), it.path * R + 1, it.depth - 1);
-  if (has_refr) push_child<MAXS>(st, refr, vmul(it.att, v3p(m.refr_att)), it.path * R + 2, it.depth - 1);
-  // ---- World#local_lights (world.rb:72-80) at hit + delta, fused with the
-  // light loop of WorldObject#local_lighting (world_object.rb:51-74): same
-  // light order, same sums.
-  const V3 T = vadd(hit, delta);
-  V3 lc = v3(0.0, 0.0, 0.0);
-  int nl = 0;
+  if (!nfired) return false;
   for (int l = 0; l < S.n_light; l++) {
-    const LightDev& L = S.light[l];
-    const double area = lit_area<COUNT>(S, T, v3p(L.pos), L.radius, err, cnt);
-    if (area > 0) {
-      nl++;
-      const double p = S.sse_is_two ? area * area : pow(area, S.sse);
-      const V3 lcol = vsc(v3p(L.color), p / (double)S.n_light);
-      const V3 nn = vnorm(n, err);
-      const V3 ll = vnorm(vsub(v3p(L.pos), hit), err);
-      double ldn = vdot(ll, nn);
-      if (ldn > 1) ldn = 1.0;
-      else if (ldn < 0) ldn = 0.0;
-      lc = vadd(lc, vsc(lcol, ldn));
-    }
+    if (!(fired >> l & 1)) continue;
+    const RTX_CONST LightDev& L = lights[l];
+    add_leaf(sum, vdiv(vmul(it.att, vsc(v3(L.color[0], L.color[1], L.color[2]), L.hl_rate)), (double)nfired), err);
   }
-  if (nl == 0) {
-    // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
-    const int pt = cam.pt;
-    const V3 att = vdiv(v3p(m.diffuse), (double)pt);
-    const V3 front = vnorm(n, err);
-    const V3 left = vnorm(vertical_vector(n, err), err);
-    const V3 up = vcross(front, left);
-    for (int k = 0; k < pt; k++) {
-      const double theta = rand01(px.seed, px.x, px.y, px.sample, it.path, 2 * k) * PI / 2.0;
-      const double phi = rand01(px.seed, px.x, px.y, px.sample, it.path, 2 * k + 1) * PI * 2.0;
-      Ray r;
-      r.o = T;
-      r.d = vadd(vsc(front, sin(theta)), vsc(vadd(vsc(left, cos(phi)), vsc(up, sin(phi))), cos(theta)));
-      push_child<MAXS>(st, r, vmul(it.att, att), it.path * R + 3 + (uint64_t)k, it.depth - 1);
-    }
-    return;
-  }
-  lc = vdiv(lc, (double)nl);
-  V3 color;
-  if (oi.type == OBJ_BOX) {
-    color = vadd(vmul(lc, v3p(m.diffuse)), v3p(m.ambient));
-  } else {
-    V3 filter = v3(1.0, 1.0, 1.0);
-    if (m.tex >= 0) {
-      if (oi.type == OBJ_SPHERE) {                  // Sphere#get_uv (sphere.rb:111-120)
-        const V3 vec = vsub(hit, v3(g[0], g[1], g[2]));
-        const double R0 = g[3];
-        const double x = vdot(vec, v3p(m.gw_n)) / R0;
-        const double y = vdot(vec, v3p(m.east_n)) / R0;
-        const double z = vdot(vec, v3p(m.north_n)) / R0;
-        const double mm2 = x * x + y * y + z * z + 2.0 * x + 1.0;
-        if (mm2 < 0) seterr(err, ERR_DOMAIN);
-        const double mm = sqrt(mm2);
-        filter = vmul(texcolor(S, m.tex, m.hs, m.vs, m.u_off, m.v_off, (y / mm + 1.0) / 2.0,
-                               (-z / mm + 1.0) / 2.0, err), filter);
-      } else {
-        double u, v;
-        plane_uv(plane, hit, u, v);
-        filter = vmul(texcolor(S, m.tex, m.hs, m.vs, 0.0, 0.0, u, v, err), filter);
-      }
-    }
-    color = vadd(vmul(vmul(lc, v3p(m.diffuse)), filter), v3p(m.ambient));
-  }
-  add_leaf(sum, vmul(it.att, color), err);
-}
-
-// Camera#lens_func (camera.rb:129-151) with the per-camera constants hoisted.
-__device__ __forceinline__ Ray lens(const CameraDev& c, int x, int y, int j, uint64_t seed) {
-  const V3 rp = vadd(vadd(v3p(c.retina_center), vsc(v3p(c.left), 2.0 * ((double)x / c.width - 0.5) * c.retina_width)),
-                     vsc(v3p(c.up_n), 2.0 * ((double)y / c.height - 0.5) * c.retina_height));
-  const double theta = rand01(seed, x, y, j, 0, 0);
-  const V3 rv = vsc(vadd(vsc(v3p(c.left_n), cos(theta)), vsc(v3p(c.up_n), sin(theta))), c.aperture_radius);
-  const V3 pos = v3p(c.pos);
-  const V3 ap = vadd(pos, rv);
-  const V3 rd = vsub(pos, rp);                                  // Ray(position - retina, retina)
-  const double t = vdot(vsub(v3p(c.pofp), rp), v3p(c.front)) / vdot(v3p(c.front), rd);
-  const V3 target = vadd(rp, vsc(rd, t));
-  Ray r;
-  r.o = ap;
-  r.d = vsub(target, ap);
-  return r;
+  return true;
 }
 
 __device__ __forceinline__ void record_error(ErrState* e, uint32_t code, int x, int y, int W) {
@@ -507,129 +523,200 @@ __device__ __forceinline__ int row_to_y(const KParams& p, int row) {
   return (k * p.nranks + p.rank) * p.tile_rows + (row - k * p.tile_rows);
 }
 
-// One lane per pixel; a wave covers an 8x8 pixel tile, a 256-thread block 4 tiles.
-template <bool COUNT, int MAXS, int MAXPRE, int WPS>
-__global__ __launch_bounds__(256, WPS) void k_render(KParams p) {
-  const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int tiles_x = (p.nx + 7) >> 3;
-  const int px_ = (tile % tiles_x) * 8 + (lane & 7);
-  const int row = (tile / tiles_x) * 8 + (lane >> 3);
-  if (px_ >= p.nx || row >= p.nrows) return;
-  const int y = row_to_y(p, row);
-  if (y >= p.cam->height) return;
-  const int x = p.x0 + px_;
-  const SceneDev& S = *p.scene;
+// SRC_PIXELS: one lane per pixel (a wave covers an 8x8 tile) running
+// Camera#render_at.  SRC_RAYS: one lane per explicit ray running
+// RayTracer#trace_sync (rtx_trace).
+template <bool COUNT, int MAXS, int MAXPRE, int WPS, bool LDS, int SRC>
+__global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __restrict__ rays,
+                                                     const int32_t* __restrict__ keys, int nrays) {
+  const SceneDev& S = p.scene;                // kernel argument: scalar loads
   const CameraDev& cam = *p.cam;
+  extern __shared__ float4 lds_sph[];
+  const float4* sph;
+  if (LDS) {
+    for (int i = threadIdx.x; i < S.n_sphere; i += blockDim.x)
+      lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
+    __syncthreads();
+    sph = lds_sph;
+  } else {
+    sph = reinterpret_cast<const float4*>(S.sph32);
+  }
+
+  int x, y, row, px_ = 0;
+  if (SRC == SRC_PIXELS) {
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int tiles_x = (p.nx + 7) >> 3;
+    px_ = (tile % tiles_x) * 8 + (lane & 7);
+    row = (tile / tiles_x) * 8 + (lane >> 3);
+    if (px_ >= p.nx || row >= p.nrows) return;
+    y = row_to_y(p, row);
+    if (y >= cam.height) return;
+    x = p.x0 + px_;
+  } else {
+    row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= nrays) return;
+    x = keys[3 * row];
+    y = keys[3 * row + 1];
+  }
 
   unsigned long long cnt[C_N];
   if (COUNT)
     for (int k = 0; k < C_N; k++) cnt[k] = 0;
 
-  Pixel pix;
-  pix.seed = p.seed;
-  pix.x = x;
-  pix.y = y;
   Stack<MAXS> st;
   st.n = 0;
   V3 smp[MAXPRE];
   uint32_t err = 0;
   const int pre = cam.pre;
-  int ntot = pre;
+  int ntot = SRC == SRC_PIXELS ? pre : 1;
   bool extra = false;
-  V3 avg = v3(0.0, 0.0, 0.0), cv = v3(0.0, 0.0, 0.0), sum = v3(0.0, 0.0, 0.0);
-  int j = 0;
-  // Camera#render_at (camera.rb:70-99) as one flat loop over all its rays.
+  V3 avg = v3(0.0, 0.0, 0.0), cv = avg, sum = avg;
+  int j = -1;                        // current camera sample
+  int sample = 0;                    // RNG key of the current tree
   Item cur;
-  cur.ray = lens(cam, x, y, 0, p.seed);
-  cur.att = v3(1.0, 1.0, 1.0);
-  cur.path = 1;
-  cur.depth = cam.depth;
-  pix.sample = 0;
-  if (COUNT) cnt[C_PRIMARY]++;
-  bool have = true;
+  bool have = false;                 // `cur` holds a ray not yet processed
+  int mode = M_NEED;
+  // shading state of the ray being shaded
+  int besti = -1, li = 0, nl = 0;
+  bool hin = true;
+  double best = 0.0, total = 0.0;
+  V3 hit = avg, delta = avg, n = avg, lc = avg;
+  V3 qo = avg, qd = avg, qL = avg;
+  double qrad = 0.0;
+
   while (true) {
-    if (!have) {
-      if (st.n > 0) {
+    // ---- A: find this lane's next query (divergent, short)
+    while (mode == M_NEED) {
+      if (have) {
+        have = false;
+      } else if (st.n > 0) {
         cur = st.a[--st.n];
       } else {
-        // sample j is complete
-        if (j < pre) {
-          smp[j] = sum;
-          avg = vadd(avg, sum);
-        } else {
-          cv = vadd(cv, sum);
+        // the current tree (camera sample) is complete
+        if (j >= 0) {
+          if (SRC == SRC_RAYS) {
+            mode = M_DONE;
+            break;
+          }
+          if (j < pre) {
+            smp[j] = sum;
+            avg = vadd(avg, sum);
+          } else {
+            cv = vadd(cv, sum);
+          }
+          if (j + 1 == pre) {                 // camera.rb:80-85: mean and variance
+            avg = vdiv(avg, (double)pre);
+            double variance = 0.0;
+            for (int k = 0; k < pre; k++) {
+              const V3 dd = vsub(smp[k], avg);
+              double mx = dd.x;
+              if (dd.y > mx) mx = dd.y;
+              if (dd.z > mx) mx = dd.z;
+              variance += mx * mx;              // .max ** 2
+            }
+            variance /= (double)pre;
+            if (variance >= cam.variant_threshold) {
+              extra = true;
+              ntot = cam.max_samples;
+            }
+          }
         }
         j++;
-        if (j == pre) {
-          avg = vdiv(avg, (double)pre);
-          double variance = 0.0;
-          for (int k = 0; k < pre; k++) {
-            const V3 dd = vsub(smp[k], avg);
-            double mx = dd.x;
-            if (dd.y > mx) mx = dd.y;
-            if (dd.z > mx) mx = dd.z;
-            variance += mx * mx;               // .max ** 2
-          }
-          variance /= (double)pre;
-          if (variance >= cam.variant_threshold) {
-            extra = true;
-            ntot = cam.max_samples;
-          }
+        if (j >= ntot) {
+          mode = M_DONE;
+          break;
         }
-        if (j >= ntot) break;
         sum = v3(0.0, 0.0, 0.0);
-        cur.ray = lens(cam, x, y, j, p.seed);
+        if (SRC == SRC_PIXELS) {
+          cur.ray = lens(cam, x, y, j, p.seed);
+          sample = j;
+          if (COUNT) cnt[C_PRIMARY]++;
+        } else {
+          cur.ray.d = v3p(rays + 6 * row);
+          cur.ray.o = v3p(rays + 6 * row + 3);
+          sample = keys[3 * row + 2];
+        }
         cur.att = v3(1.0, 1.0, 1.0);
         cur.path = 1;
         cur.depth = cam.depth;
-        pix.sample = j;
-        if (COUNT) cnt[C_PRIMARY]++;
       }
+      // rt_map prologue (ray_tracer.rb:52-75)
+      if (cur.depth <= 0 || vr(cur.att) < 0.0001) continue;
+      if (COUNT) {
+        cnt[C_RAYS]++;
+        cnt[C_HIGHLIGHT_TESTS] += S.n_light;
+      }
+      if (highlights(S, cur, sum, err)) continue;
+      mode = M_EXTEND;
+      qo = cur.ray.o;
+      qd = cur.ray.d;
+      best = S.max_distance;
+      besti = -1;
     }
-    have = false;
-    rt_map<COUNT, MAXS>(S, cam, pix, cur, st, sum, err, cnt);
+    if (mode == M_DONE) break;
+
+    // ---- B: the object walk, shared by EXTEND and SHADOW lanes
+    query<COUNT>(S, sph, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err, cnt);
+
+    // ---- C: consume the query result
+    if (mode == M_EXTEND) {
+      if (besti < 0) {                       // "light_dead": nothing hit
+        mode = M_NEED;
+        continue;
+      }
+      if (COUNT) cnt[C_SHADE_HITS]++;
+      hit_info(S, besti, cur.ray, hit, delta, n, hin);
+      li = 0;
+      nl = 0;
+      lc = v3(0.0, 0.0, 0.0);
+    } else {
+      // World#local_lights (world.rb:72-80) fused with the light loop of
+      // WorldObject#local_lighting (world_object.rb:51-74): same order, same sums.
+      const double area = total > 0 ? total : 0.0;
+      if (area > 0) {
+        const LightDev& L = S.light[li];
+        nl++;
+        const double pw = S.sse_is_two ? area * area : pow(area, S.sse);
+        const V3 lcol = vsc(v3p(L.color), pw / (double)S.n_light);
+        const V3 nn = vnorm(n, err);
+        const V3 ll = vnorm(vsub(v3p(L.pos), hit), err);
+        double ldn = vdot(ll, nn);
+        if (ldn > 1) ldn = 1.0;
+        else if (ldn < 0) ldn = 0.0;
+        lc = vadd(lc, vsc(lcol, ldn));
+      }
+      li++;
+    }
+    if (li < S.n_light) {                    // next light: a SHADOW query from hit + delta
+      const LightDev& L = S.light[li];
+      mode = M_SHADOW;
+      qo = vadd(hit, delta);
+      qL = v3p(L.pos);
+      qd = vsub(qL, qo);                     // Ray(light - target, target)
+      qrad = L.radius;
+      total = 1.0;
+      continue;
+    }
+    have = shade_finish<MAXS>(S, cam, p.seed, x, y, sample, besti, hin, hit, delta, n, lc, nl, cur, st, sum, err);
+    mode = M_NEED;
   }
-  if (extra) avg = vdiv(vadd(vsc(avg, (double)pre), cv), (double)cam.max_samples);
-  double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
-  o[0] = avg.x;
-  o[1] = avg.y;
-  o[2] = avg.z;
-  if (err) record_error(p.err, err, x, y, cam.width);
+
+  if (SRC == SRC_PIXELS) {
+    if (extra) avg = vdiv(vadd(vsc(avg, (double)pre), cv), (double)cam.max_samples);
+    double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
+    o[0] = avg.x;
+    o[1] = avg.y;
+    o[2] = avg.z;
+    if (err) record_error(p.err, err, x, y, cam.width);
+  } else {
+    p.out[3 * row] = sum.x;
+    p.out[3 * row + 1] = sum.y;
+    p.out[3 * row + 2] = sum.z;
+    if (err) record_error(p.err, err, row, 0, 0x7fffffff);
+  }
   if (COUNT)
     for (int k = 0; k < C_N; k++) atomicAdd(&p.counts[k], cnt[k]);
-}
-
-// RayTracer#trace_sync(x, y, ray) for explicit rays: rays[i] = (front, position).
-template <int MAXS>
-__global__ __launch_bounds__(256) void k_trace(KParams p, const double* __restrict__ rays,
-                                               const int32_t* __restrict__ keys, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  Pixel pix;
-  pix.seed = p.seed;
-  pix.x = keys[3 * i];
-  pix.y = keys[3 * i + 1];
-  pix.sample = keys[3 * i + 2];
-  Stack<MAXS> st;
-  st.n = 0;
-  uint32_t err = 0;
-  V3 sum = v3(0.0, 0.0, 0.0);
-  Item cur;
-  cur.ray.d = v3p(rays + 6 * i);
-  cur.ray.o = v3p(rays + 6 * i + 3);
-  cur.att = v3(1.0, 1.0, 1.0);
-  cur.path = 1;
-  cur.depth = p.cam->depth;
-  while (true) {
-    rt_map<false, MAXS>(*p.scene, *p.cam, pix, cur, st, sum, err, nullptr);
-    if (st.n == 0) break;
-    cur = st.a[--st.n];
-  }
-  p.out[3 * i] = sum.x;
-  p.out[3 * i + 1] = sum.y;
-  p.out[3 * i + 2] = sum.z;
-  if (err) record_error(p.err, err, i, 0, 0x7fffffff);
 }
 
 // Camera#array_to_color (camera.rb:153-156) + PNG::Canvas#point over black.
@@ -659,15 +746,27 @@ int stack_bucket(int need) {
   return -1;
 }
 
-hipError_t launch_render(const KParams& p, bool count, int maxs, int wps, hipStream_t s) {
+// Spheres staged in LDS when they fit this budget (keeps 4+ workgroups/CU).
+constexpr int LDS_SPHERE_BYTES = 32 * 1024;
+
+template <bool COUNT, int MAXS, int WPS, int SRC>
+static hipError_t launch_one(const KParams& p, int n_sphere, dim3 grid, const double* rays, const int32_t* keys,
+                             int n, hipStream_t s) {
+  const size_t lds = (size_t)n_sphere * 16;
+  if (lds <= (size_t)LDS_SPHERE_BYTES)
+    hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, WPS, true, SRC>), grid, dim3(256), lds ? lds : 16, s, p, rays,
+                       keys, n);
+  else
+    hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, WPS, false, SRC>), grid, dim3(256), 0, s, p, rays, keys, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_render(const KParams& p, int n_sphere, bool count, int maxs, int wps, hipStream_t s) {
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
-  const dim3 grid((tiles + 3) / 4), block(256);
+  const dim3 grid((tiles + 3) / 4);
   if (tiles == 0) return hipSuccess;
-#define RTX_L(C, M, W)                                                   \
-  if (count == C && maxs == M && wps == W) {                             \
-    hipLaunchKernelGGL((k_render<C, M, 16, W>), grid, block, 0, s, p);  \
-    return hipGetLastError();                                            \
-  }
+#define RTX_L(C, M, W) \
+  if (count == C && maxs == M && wps == W) return launch_one<C, M, W, SRC_PIXELS>(p, n_sphere, grid, nullptr, nullptr, 0, s);
   RTX_L(false, 8, 2) RTX_L(false, 16, 2) RTX_L(false, 32, 2) RTX_L(false, 64, 2)
   RTX_L(false, 16, 1) RTX_L(false, 16, 3) RTX_L(false, 16, 4)
   RTX_L(true, 8, 2) RTX_L(true, 16, 2) RTX_L(true, 32, 2) RTX_L(true, 64, 2)
@@ -675,18 +774,17 @@ hipError_t launch_render(const KParams& p, bool count, int maxs, int wps, hipStr
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_trace(const KParams& p, const double* rays, const int32_t* keys, int n, int maxs,
+hipError_t launch_trace(const KParams& p, int n_sphere, const double* rays, const int32_t* keys, int n, int maxs,
                         hipStream_t s) {
-  const dim3 grid((n + 255) / 256), block(256);
   if (n == 0) return hipSuccess;
+  const dim3 grid((n + 255) / 256);
   switch (maxs) {
-    case 8: hipLaunchKernelGGL((k_trace<8>), grid, block, 0, s, p, rays, keys, n); break;
-    case 16: hipLaunchKernelGGL((k_trace<16>), grid, block, 0, s, p, rays, keys, n); break;
-    case 32: hipLaunchKernelGGL((k_trace<32>), grid, block, 0, s, p, rays, keys, n); break;
-    case 64: hipLaunchKernelGGL((k_trace<64>), grid, block, 0, s, p, rays, keys, n); break;
-    default: return hipErrorInvalidValue;
+    case 8: return launch_one<false, 8, 2, SRC_RAYS>(p, n_sphere, grid, rays, keys, n, s);
+    case 16: return launch_one<false, 16, 2, SRC_RAYS>(p, n_sphere, grid, rays, keys, n, s);
+    case 32: return launch_one<false, 32, 2, SRC_RAYS>(p, n_sphere, grid, rays, keys, n, s);
+    case 64: return launch_one<false, 64, 2, SRC_RAYS>(p, n_sphere, grid, rays, keys, n, s);
   }
-  return hipGetLastError();
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,

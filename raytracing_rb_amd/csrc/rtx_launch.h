@@ -17,8 +17,8 @@ struct ErrState {
 };
 
 struct KParams {
-  const SceneDev* scene;           // device copies (uploaded by rtx_scene_upload / rtx_camera_set)
-  const CameraDev* cam;
+  SceneDev scene;                  // by value: read by scalar loads from the kernarg segment
+  const CameraDev* cam;            // device copy (uploaded by rtx_camera_set)
   uint64_t seed;
   int32_t x0, nx, nrows;           // columns [x0, x0+nx); packed output rows
   int32_t y0, tile_rows, rank, nranks;   // tile_rows == 0: rows y0 .. y0+nrows-1
@@ -29,8 +29,8 @@ struct KParams {
 };
 
 int stack_bucket(int need);
-hipError_t launch_render(const KParams& p, bool count, int maxs, int wps, hipStream_t s);
-hipError_t launch_trace(const KParams& p, const double* rays, const int32_t* keys, int n, int maxs,
+hipError_t launch_render(const KParams& p, int n_sphere, bool count, int maxs, int wps, hipStream_t s);
+hipError_t launch_trace(const KParams& p, int n_sphere, const double* rays, const int32_t* keys, int n, int maxs,
                         hipStream_t s);
 hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,
                            hipStream_t s);

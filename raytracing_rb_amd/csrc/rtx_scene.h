@@ -1,12 +1,15 @@
 // rtx_scene.h — device-resident scene layout of librtx (host + device).
 //
-// The YAML scene of World.new (src/world.rb:15-34) flattened into two tiers:
-//   * hot  : ObjInfo[n] + a flat double array of per-object geometry, read by
-//            every lane in the same order (uniform index => scalar loads /
-//            LDS broadcast), YAML order preserved (first object wins ties,
-//            world.rb:48-50; cover areas are subtracted in that order,
-//            world.rb:64-67);
-//   * cold : Material[n], lights, textures — touched once per shaded hit.
+// The YAML scene of World.new (src/world.rb:15-34) flattened for the GPU:
+//   * runs   : maximal runs of consecutive objects of one type, in YAML order.
+//              Every object loop walks the runs in order, so the reference's
+//              order semantics hold exactly (first object wins distance ties,
+//              world.rb:48-50; cover areas subtracted in order, world.rb:64-67).
+//   * spheres: a binary64 record for the exact Sphere#intersect and a float32
+//              record {cx, cy, cz, R} for the conservative pre-test, staged in
+//              LDS by every workgroup (16 B per sphere).
+//   * planes / box faces: binary64 records.
+//   * Material[n_obj], lights, textures — read once per shaded hit.
 // Every derived constant (normalized axes, box faces, ...) is computed on the
 // host with the reference's operation order (rtx_capi.cpp), so the device sees
 // bit-identical values to what the Ruby code recomputes on every call.
@@ -17,18 +20,22 @@ namespace rtx {
 
 enum : int32_t { OBJ_SPHERE = 0, OBJ_PLANE = 1, OBJ_BOX = 2 };
 
-// Geometry records (offsets in doubles into SceneDev::geo).
-//   sphere : [0..2] C, [3] R, [4] R*R (cull only), [5] |C|_1 + R (cull scale)
-//   plane  : [0..2] P, [3..5] F, [6..8] left.normalize, [9..11] up.normalize, [12] u_unit, [13] v_unit
-//   box    : 6 faces x 14 doubles (plane layout), face order of box.rb:62-67
-constexpr int SPHERE_GEO = 6;
+// Plane record (doubles): [0..2] P, [3..5] F, [6..8] left.normalize,
+// [9..11] up.normalize, [12] u_unit, [13] v_unit.  A box = 6 plane records
+// in the face order of box.rb:62-67.
 constexpr int PLANE_GEO = 14;
 constexpr int BOX_GEO = 6 * PLANE_GEO;
 
-struct ObjInfo {
+struct Run {
   int32_t type;
-  int32_t geo;      // offset into geo[]
-  int32_t pad0, pad1;
+  int32_t obj0;     // global (YAML) index of the run's first object
+  int32_t count;
+  int32_t rec0;     // index of the first record in the type's array
+};
+
+struct Sphere64 {
+  double c[3];
+  double r;
 };
 
 struct Material {
@@ -41,8 +48,9 @@ struct Material {
   double u_off, v_off;    // sphere texture offsets
   double gw_n[3], east_n[3], north_n[3];   // sphere texture axes (normalized)
   int32_t has_rr;         // Ruby truthiness of refractive_rate
-  int32_t tex;            // -1 = none (ignored for boxes, box.rb never shades with it)
-  int32_t face_rr_pad0, face_rr_pad1;
+  int32_t tex;            // -1 = none (boxes never shade with theirs, box.rb)
+  int32_t type;
+  int32_t rec;            // index into the type's record array
 };
 
 struct LightDev {
@@ -62,17 +70,20 @@ struct TexDev {
 };
 
 struct SceneDev {
-  const ObjInfo* info;
-  const double* geo;
+  const Run* runs;
+  const Sphere64* sph64;
+  const float* sph32;     // 4 floats per sphere: cx, cy, cz, R
+  const double* planes;   // PLANE_GEO doubles per plane
+  const double* boxes;    // BOX_GEO doubles per box
   const Material* mat;
   const LightDev* light;
   const TexDev* tex;
   const uint8_t* texels;
-  int32_t n_obj, n_light, n_sphere, n_plane, n_box, n_geo;
+  int32_t n_obj, n_light, n_sphere, n_plane, n_box, n_runs;
   double max_distance;
   double sse;             // soft_shadow_exponent
-  int32_t sse_is_two;     // pow(area, 2.0) == area*area fast path
-  int32_t pad;
+  float sph_scale;        // max over spheres of |C|_1 + R (pre-test margin scale)
+  int32_t sse_is_two;     // pow(area, 2.0) == area*area (glibc, checked)
 };
 
 struct CameraDev {
