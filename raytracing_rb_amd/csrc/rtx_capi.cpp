@@ -44,6 +44,7 @@ struct rtx_context {
   size_t scratch_bytes = 0;
   int64_t opt_force_stack = 0;
   int64_t opt_wps = 2;
+  int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
 };
 
 static rtx_status fail(rtx_context* c, rtx_status s, const char* fmt, ...) {
@@ -128,6 +129,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!c || !key) return RTX_EINVAL;
   if (!strcmp(key, "force_stack")) {
     c->opt_force_stack = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "sphere_src")) {        // sphere pre-test records: 0 = LDS, 1 = scalar loads
+    if (value < 0 || value > 1) return fail(c, RTX_EINVAL, "sphere_src must be 0 or 1");
+    c->opt_sphere_src = value;
     return RTX_OK;
   }
   if (!strcmp(key, "waves_per_simd")) {    // k_render occupancy variant (1..4; 16-entry stack only)
@@ -245,6 +251,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   }
   if (err) return fail(c, RTX_EZERO_VEC, "zero vector detected while building the scene");
   if (!std::isfinite(sph_scale)) return fail(c, RTX_EINVAL, "non-finite sphere coordinates");
+  for (int k = 0; k < 16; k++) sph32.push_back(0.0f);   // 4 padding records: group loads stay in bounds
   std::vector<LightDev> lights(sd->n_lights);
   for (int i = 0; i < sd->n_lights; i++) {
     const rtx_light_desc& l = sd->lights[i];
@@ -390,7 +397,7 @@ rtx_status rtx_render_device(rtx_context* c, int32_t x0, int32_t y0, int32_t x1,
   p.nrows = y1 - y0;
   p.out = d_out;
   p.stride = row_stride;
-  HIPCHK(c, launch_render(p, c->scene.n_sphere, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
+  HIPCHK(c, launch_render(p, c->scene.n_sphere, (int)c->opt_sphere_src, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
   return RTX_OK;
 }
 
@@ -418,7 +425,7 @@ rtx_status rtx_render_tiles_device(rtx_context* c, int32_t tile_rows, int32_t ra
   p.nranks = nranks;
   p.out = d_packed;
   p.stride = (size_t)c->cam.width * 3;
-  HIPCHK(c, launch_render(p, c->scene.n_sphere, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
+  HIPCHK(c, launch_render(p, c->scene.n_sphere, (int)c->opt_sphere_src, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
   return RTX_OK;
 }
 
@@ -496,7 +503,7 @@ rtx_status rtx_trace(rtx_context* c, int32_t n, const double* rays, const int32_
   HIPCHK(c, hipMemcpy(d_rays, rays, rb, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(d_keys, keys, kb, hipMemcpyHostToDevice));
   p.out = d_out;
-  HIPCHK(c, launch_trace(p, c->scene.n_sphere, d_rays, d_keys, n, maxs, nullptr));
+  HIPCHK(c, launch_trace(p, c->scene.n_sphere, (int)c->opt_sphere_src, d_rays, d_keys, n, maxs, nullptr));
   HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
   return rtx_sync(c, nullptr);
 }
@@ -517,7 +524,7 @@ rtx_status rtx_count_work(rtx_context* c, uint64_t seed, uint64_t counts[RTX_NCO
   p.nrows = H;
   p.out = c->d_scratch;
   p.stride = (size_t)W * 3;
-  HIPCHK(c, launch_render(p, c->scene.n_sphere, true, maxs, 2, nullptr));
+  HIPCHK(c, launch_render(p, c->scene.n_sphere, (int)c->opt_sphere_src, true, maxs, 2, nullptr));
   HIPCHK(c, hipDeviceSynchronize());
   unsigned long long tmp[RTX_NCOUNT];
   HIPCHK(c, hipMemcpy(tmp, c->d_counts, sizeof tmp, hipMemcpyDeviceToHost));

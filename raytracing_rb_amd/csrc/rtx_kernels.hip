@@ -78,6 +78,28 @@ __device__ __forceinline__ const RTX_CONST T* cptr(const T* p) {
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 enum { SRC_PIXELS = 0, SRC_RAYS = 1 };
 
+// Diagnostic build only (-DRTX_STAMPS=1): per-wave shader-clock time spent in
+// each phase of the lane state machine, summed into rtx_stamps[] (read with
+// rtxdbg_read_stamps).  The shipped library is built without it.
+#ifndef RTX_DIAG_NOEXACT
+#define RTX_DIAG_NOEXACT 0
+#endif
+#ifndef RTX_STAMPS
+#define RTX_STAMPS 0
+#endif
+__device__ unsigned long long rtx_stamps[8];
+__device__ __forceinline__ unsigned long long stamp() {
+#if RTX_STAMPS
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+#else
+  return 0;
+#endif
+}
+
 __device__ __forceinline__ void seterr(uint32_t& err, uint32_t code) {
   if (!err) err = code;
 }
@@ -88,12 +110,17 @@ __device__ __forceinline__ bool sphere_exact(V3 C, double R, V3 o, V3 d, V3 dn, 
   const V3 oc = vsub(C, o);                       // center - ray.position
   const double q = vdot(oc, d);
   const double t = q / r2;
+  const double s = vsq(oc);                       // |position - center|^2 (same bits)
+  // The reference returns nil when the origin is outside and t < 0 (sphere.rb:80).
+  // s > R*R*(1 + 1e-12) proves |o - C|.r > R without the sqrt, so
+  // this exit is taken only where the full evaluation below would return nil.
+  if (t < 0 && s > R * R * (1.0 + 1e-12)) return false;
   const V3 np = vadd(o, vsc(d, t));
   const double nd = vr(vsub(np, C));
   if (!(nd <= R)) return false;                   // inner?(nearest_point)
   const double h = sqrt(R * R - nd * nd);         // radius**2 - nearest_dis**2
   const V3 vec = vsc(dn, h);
-  const bool from_inner = vr(oc) <= R;            // inner?(ray.position): |oc| has |o - C|'s bits
+  const bool from_inner = sqrt(s) <= R;           // inner?(ray.position)
   in = !from_inner;
   hit = in ? vsub(np, vec) : vadd(np, vec);
   if (!from_inner && t < 0) return false;
@@ -172,13 +199,16 @@ RTX_SHADE_FN double penumbra(V3 C, double R, V3 T, V3 lt, double radius, uint32_
 //   EXTEND: World#intersect — nearest hit (strict <, YAML order) -> best/besti.
 //   SHADOW: World#lit_area for light L (o = target T, d = L - T) -> total
 //           (1 - ordered sum of cover areas; zero covers skipped: exact).
-template <bool COUNT>
-__device__ __forceinline__ void query(const SceneDev& S, const float4* __restrict__ sph, bool ext, V3 o, V3 d,
+template <bool COUNT, typename SPH>
+__device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o, V3 d,
                                       V3 L, double radius, double& best, int& besti, double& total,
                                       uint32_t& err, unsigned long long* cnt) {
   const double r = vr(d);
   const double r2 = r * r;                        // front.r2
-  const V3 dn = r == 0 ? d : v3(d.x / r, d.y / r, d.z / r);   // front.normalize
+  // front.normalize is needed only by a sphere that passes the pre-test:
+  // computed on first use (same bits wherever it is computed).
+  V3 dn = d;
+  bool have_dn = false;
   // float32 pre-test constants (exact culls)
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
   const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
@@ -208,29 +238,65 @@ __device__ __forceinline__ void query(const SceneDev& S, const float4* __restric
     run.count = uni(runs[ri].count);
     run.rec0 = uni(runs[ri].rec0);
     if (run.type == OBJ_SPHERE) {
-      for (int k = 0; k < run.count; k++) {
-        const float4 c = sph[run.rec0 + k];        // {cx, cy, cz, R^2}, wave-uniform
-        const float ocx = c.x - ox, ocy = c.y - oy, ocz = c.z - oz;
-        const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
-        const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
-        const bool miss_line = __builtin_fmaf(s, dd, -q * q) > __builtin_fmaf(dd, c.w, kline);
-        const bool behind = q < qneg && s > c.w + ms2;
-        if (miss_line || behind) continue;
-        const RTX_CONST Sphere64& sp = sph64[run.rec0 + k];
-        const V3 C = v3(sp.c[0], sp.c[1], sp.c[2]);
-        const double sr = sp.r;
-        V3 hit;
-        bool in;
-        if (!sphere_exact(C, sr, o, d, dn, r2, hit, in)) continue;
-        if (ext) {
-          if (COUNT) cnt[C_SPHERE_HITS]++;
-          const double dist = vr(vsub(o, hit));    // Ray#distance
-          if (dist < best) {
-            best = dist;
-            besti = run.obj0 + k;
+      // Pre-test 4 spheres at a time (4 LDS reads in flight), then run the
+      // exact test, in order, for those this lane cannot rule out.
+      for (int k0 = 0; k0 < run.count; k0 += 4) {
+        // The record table is padded to a multiple of 4 (rtx_capi.cpp), so
+        // the group loads are unconditional; records past the run are masked.
+        float4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {                // {cx, cy, cz, R^2}, wave-uniform
+          const int b = 4 * (run.rec0 + k0 + u);
+          c[u].x = sph[b];
+          c[u].y = sph[b + 1];
+          c[u].z = sph[b + 2];
+          c[u].w = sph[b + 3];
+        }
+        uint32_t keep = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const float ocx = c[u].x - ox, ocy = c[u].y - oy, ocz = c[u].z - oz;
+          const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+          const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
+          const bool miss_line = __builtin_fmaf(s, dd, -q * q) > __builtin_fmaf(dd, c[u].w, kline);
+          const bool behind = q < qneg && s > c[u].w + ms2;
+          keep |= (miss_line || behind) ? 0u : (1u << u);
+        }
+        if (k0 + 4 > run.count) keep &= (1u << (run.count - k0)) - 1u;
+#if RTX_STAMPS
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
+          for (int u = 0; u < 4; u++) atomicAdd(&rtx_stamps[6], __ballot(keep >> u & 1) ? 1ull : 0ull);
+        }
+        atomicAdd(&rtx_stamps[7], (unsigned long long)__builtin_popcount(keep));
+#endif
+#if RTX_DIAG_NOEXACT
+        keep = 0;                                    // diagnostic only: wrong results
+#endif
+        if (!keep) continue;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (!(keep >> u & 1)) continue;
+          const int k = k0 + u;
+          const RTX_CONST Sphere64& sp = sph64[run.rec0 + k];
+          const V3 C = v3(sp.c[0], sp.c[1], sp.c[2]);
+          const double sr = sp.r;
+          if (!have_dn) {
+            if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r);
+            have_dn = true;
           }
-        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
-          total -= penumbra(C, sr, o, d, radius, err);
+          V3 hit;
+          bool in;
+          if (!sphere_exact(C, sr, o, d, dn, r2, hit, in)) continue;
+          if (ext) {
+            if (COUNT) cnt[C_SPHERE_HITS]++;
+            const double dist = vr(vsub(o, hit));    // Ray#distance
+            if (dist < best) {
+              best = dist;
+              besti = run.obj0 + k;
+            }
+          } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
+            total -= penumbra(C, sr, o, d, radius, err);
+          }
         }
       }
     } else if (run.type == OBJ_PLANE) {
@@ -267,24 +333,23 @@ __device__ __forceinline__ void query(const SceneDev& S, const float4* __restric
 }
 
 // ----------------------------------------------------------------- shading
-__device__ __forceinline__ Ray reflection(const Ray& ray, V3 n, V3 hit, V3 delta, uint32_t& err) {
-  // WorldObject#get_reflection_by_ray_and_n (world_object.rb:121-125)
-  const double c = vcos(ray.d, vneg(n), err);
+// WorldObject#get_reflection_by_ray_and_n (world_object.rb:121-125).
+// nn = n.normalize, c = ray.front.cos(-n) (== ray.front.cos(n): |cos| of a
+// negated vector has the same bits), both computed once per hit.
+__device__ __forceinline__ Ray reflection(const Ray& ray, V3 nn, double c, V3 hit, V3 delta, uint32_t& err) {
   Ray r;
-  r.d = vnorm(vadd(vsc(vnorm(n, err), 2.0 * c * vr(ray.d)), ray.d), err);
+  r.d = vnorm(vadd(vsc(nn, 2.0 * c * vr(ray.d)), ray.d), err);
   r.o = vadd(hit, delta);
   return r;
 }
 
-__device__ __forceinline__ bool refraction(const Ray& ray, V3 n, V3 hit, V3 refl, double rate, Ray& out,
-                                           uint32_t& err) {
-  // WorldObject#get_refraction_by_ray_and_n (world_object.rb:127-137)
-  const double c = vcos(ray.d, n, err);
+// WorldObject#get_refraction_by_ray_and_n (world_object.rb:127-137).
+__device__ __forceinline__ bool refraction(const Ray& ray, V3 nn, double c, V3 hit, V3 refl, double rate,
+                                           Ray& out, uint32_t& err) {
   const double sin_i = sqrt(1.0 - c * c);        // 1 - cos**2
   const double sin_r = sin_i / rate;
   if (sin_r >= 1) return false;                  // total internal reflection
   const double r = asin(sin_r);
-  const V3 nn = vnorm(n, err);
   out.d = vadd(vsc(nn, -cos(r)), vsc(vnorm(vadd(refl, ray.d), err), sin_r));
   out.o = vsub(hit, vsc(nn, EPS));
   return true;
@@ -387,27 +452,29 @@ __device__ __forceinline__ void emit(Stack<MAXS>& st, Item& pend, bool& has, uin
 // or the local-lighting leaf.  Returns true with the next ray in `cur`.
 template <int MAXS>
 RTX_SHADE_FN bool shade_finish(const SceneDev& S, const CameraDev& cam, uint64_t seed, int x, int y,
-                                          int sample, int obj, bool in, V3 hit, V3 delta, V3 n, V3 lc, int nl,
+                                          int sample, int obj, bool in, V3 hit, V3 delta, V3 n, V3 nn, V3 lc,
+                                          int nl,
                                           Item& cur, Stack<MAXS>& st, V3& sum, uint32_t& err) {
   const Material& m = S.mat[obj];
   Item pend;
   bool has = false;
   const uint64_t R = (uint64_t)cam.pt + 3;
-  const Ray refl = reflection(cur.ray, n, hit, delta, err);
+  const double c = vcos(cur.ray.d, n, err);
+  const Ray refl = reflection(cur.ray, nn, c, hit, delta, err);
   emit<MAXS>(st, pend, has, err, refl, vmul(cur.att, v3p(m.refl_att)), cur.path * R + 1, cur.depth - 1);
   Ray refr;
   bool has_refr = false;
   if (m.type == OBJ_SPHERE)                                  // sphere.rb:92-94: rate inverted leaving
-    has_refr = refraction(cur.ray, n, hit, refl.d, in ? m.rr : 1.0 / m.rr, refr, err);
+    has_refr = refraction(cur.ray, nn, c, hit, refl.d, in ? m.rr : 1.0 / m.rr, refr, err);
   else if (m.has_rr)                                         // plane.rb:57-61: same rate both ways
-    has_refr = refraction(cur.ray, n, hit, refl.d, m.rr, refr, err);
+    has_refr = refraction(cur.ray, nn, c, hit, refl.d, m.rr, refr, err);
   if (has_refr)
     emit<MAXS>(st, pend, has, err, refr, vmul(cur.att, v3p(m.refr_att)), cur.path * R + 2, cur.depth - 1);
   if (nl == 0) {
     // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
     const int pt = cam.pt;
     const V3 att = vmul(cur.att, vdiv(v3p(m.diffuse), (double)pt));
-    const V3 front = vnorm(n, err);
+    const V3 front = nn;
     const V3 left = vnorm(vertical_vector(n, err), err);
     const V3 up = vcross(front, left);
     Ray r;
@@ -451,20 +518,23 @@ RTX_SHADE_FN bool shade_finish(const SceneDev& S, const CameraDev& cam, uint64_t
   return has;
 }
 
-// Camera#lens_func (camera.rb:129-151) with the per-camera constants hoisted.
-__device__ __forceinline__ Ray lens(const CameraDev& c, int x, int y, int j, uint64_t seed) {
+// Camera#lens_func (camera.rb:129-151).  Everything but the aperture point is
+// independent of the sample: the focal-plane target of pixel (x, y) is
+// computed once per pixel (lens_target), the sample's ray per draw (lens_ray).
+__device__ __forceinline__ V3 lens_target(const CameraDev& c, int x, int y) {
   const V3 rp = vadd(vadd(v3p(c.retina_center), vsc(v3p(c.left), 2.0 * ((double)x / c.width - 0.5) * c.retina_width)),
                      vsc(v3p(c.up_n), 2.0 * ((double)y / c.height - 0.5) * c.retina_height));
+  const V3 rd = vsub(v3p(c.pos), rp);                           // Ray(position - retina, retina)
+  const double t = vdot(vsub(v3p(c.pofp), rp), v3p(c.front)) / vdot(v3p(c.front), rd);
+  return vadd(rp, vsc(rd, t));                                  // intersect_plane (:123-127)
+}
+
+__device__ __forceinline__ Ray lens_ray(const CameraDev& c, V3 target, int x, int y, int j, uint64_t seed) {
   const double theta = rand01(seed, x, y, j, 0, 0);
   const V3 rv = vsc(vadd(vsc(v3p(c.left_n), cos(theta)), vsc(v3p(c.up_n), sin(theta))), c.aperture_radius);
-  const V3 pos = v3p(c.pos);
-  const V3 ap = vadd(pos, rv);
-  const V3 rd = vsub(pos, rp);                                  // Ray(position - retina, retina)
-  const double t = vdot(vsub(v3p(c.pofp), rp), v3p(c.front)) / vdot(v3p(c.front), rd);
-  const V3 target = vadd(rp, vsc(rd, t));
   Ray r;
-  r.o = ap;
-  r.d = vsub(target, ap);
+  r.o = vadd(v3p(c.pos), rv);
+  r.d = vsub(target, r.o);
   return r;
 }
 
@@ -531,16 +601,16 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
                                                      const int32_t* __restrict__ keys, int nrays) {
   const SceneDev& S = p.scene;                // kernel argument: scalar loads
   const CameraDev& cam = *p.cam;
+  // Sphere pre-test records: staged in LDS (LDS = true) or read with scalar
+  // loads from the constant address space (LDS = false).
   extern __shared__ float4 lds_sph[];
-  const float4* sph;
   if (LDS) {
-    for (int i = threadIdx.x; i < S.n_sphere; i += blockDim.x)
+    for (int i = threadIdx.x; i < S.n_sphere + 4; i += blockDim.x)
       lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
     __syncthreads();
-    sph = lds_sph;
-  } else {
-    sph = reinterpret_cast<const float4*>(S.sph32);
   }
+  const float* sph_lds = reinterpret_cast<const float*>(lds_sph);
+  const RTX_CONST float* sph_k = cptr(S.sph32);
 
   int x, y, row, px_ = 0;
   if (SRC == SRC_PIXELS) {
@@ -563,6 +633,7 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
   unsigned long long cnt[C_N];
   if (COUNT)
     for (int k = 0; k < C_N; k++) cnt[k] = 0;
+  const V3 tgt = SRC == SRC_PIXELS ? lens_target(cam, x, y) : v3(0.0, 0.0, 0.0);
 
   Stack<MAXS> st;
   st.n = 0;
@@ -581,11 +652,13 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
   int besti = -1, li = 0, nl = 0;
   bool hin = true;
   double best = 0.0, total = 0.0;
-  V3 hit = avg, delta = avg, n = avg, lc = avg;
+  V3 hit = avg, delta = avg, n = avg, nn = avg, lc = avg;
   V3 qo = avg, qd = avg, qL = avg;
   double qrad = 0.0;
 
+  unsigned long long tA = 0, tB = 0, tC = 0, tD = 0, iters = 0, t0 = 0, t1;
   while (true) {
+    if (RTX_STAMPS) t0 = stamp();
     // ---- A: find this lane's next query (divergent, short)
     while (mode == M_NEED) {
       if (have) {
@@ -629,7 +702,7 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
         }
         sum = v3(0.0, 0.0, 0.0);
         if (SRC == SRC_PIXELS) {
-          cur.ray = lens(cam, x, y, j, p.seed);
+          cur.ray = lens_ray(cam, tgt, x, y, j, p.seed);
           sample = j;
           if (COUNT) cnt[C_PRIMARY]++;
         } else {
@@ -654,10 +727,24 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
       best = S.max_distance;
       besti = -1;
     }
+    if (RTX_STAMPS) {
+      t1 = stamp();
+      tA += t1 - t0;
+      t0 = t1;
+      iters++;
+    }
     if (mode == M_DONE) break;
 
     // ---- B: the object walk, shared by EXTEND and SHADOW lanes
-    query<COUNT>(S, sph, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err, cnt);
+    if (LDS)
+      query<COUNT>(S, sph_lds, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err, cnt);
+    else
+      query<COUNT>(S, sph_k, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err, cnt);
+    if (RTX_STAMPS) {
+      t1 = stamp();
+      tB += t1 - t0;
+      t0 = t1;
+    }
 
     // ---- C: consume the query result
     if (mode == M_EXTEND) {
@@ -667,6 +754,7 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
       }
       if (COUNT) cnt[C_SHADE_HITS]++;
       hit_info(S, besti, cur.ray, hit, delta, n, hin);
+      nn = vnorm(n, err);                    // n.normalize, shared by every use below
       li = 0;
       nl = 0;
       lc = v3(0.0, 0.0, 0.0);
@@ -679,7 +767,6 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
         nl++;
         const double pw = S.sse_is_two ? area * area : pow(area, S.sse);
         const V3 lcol = vsc(v3p(L.color), pw / (double)S.n_light);
-        const V3 nn = vnorm(n, err);
         const V3 ll = vnorm(vsub(v3p(L.pos), hit), err);
         double ldn = vdot(ll, nn);
         if (ldn > 1) ldn = 1.0;
@@ -696,10 +783,29 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
       qd = vsub(qL, qo);                     // Ray(light - target, target)
       qrad = L.radius;
       total = 1.0;
+      if (RTX_STAMPS) {
+        t1 = stamp();
+        tC += t1 - t0;
+      }
       continue;
     }
-    have = shade_finish<MAXS>(S, cam, p.seed, x, y, sample, besti, hin, hit, delta, n, lc, nl, cur, st, sum, err);
+    if (RTX_STAMPS) {
+      t1 = stamp();
+      tC += t1 - t0;
+      t0 = t1;
+    }
+    have = shade_finish<MAXS>(S, cam, p.seed, x, y, sample, besti, hin, hit, delta, n, nn, lc, nl, cur, st, sum,
+                              err);
     mode = M_NEED;
+    if (RTX_STAMPS) tD += stamp() - t0;
+  }
+  if (RTX_STAMPS && (threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
+    atomicAdd(&rtx_stamps[0], tA);
+    atomicAdd(&rtx_stamps[1], tB);
+    atomicAdd(&rtx_stamps[2], tC);
+    atomicAdd(&rtx_stamps[3], tD);
+    atomicAdd(&rtx_stamps[4], iters);
+    atomicAdd(&rtx_stamps[5], 1ull);
   }
 
   if (SRC == SRC_PIXELS) {
@@ -738,6 +844,15 @@ __global__ void k_quantize(const double* __restrict__ rgb, int w, int h, size_t 
 }
 
 // ----------------------------------------------------------------- launchers
+extern "C" int rtxdbg_read_stamps(unsigned long long* out, int reset) {   // diagnostic builds
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtx_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtx_stamps), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+
 int stack_bucket(int need) {
   if (need <= 8) return 8;
   if (need <= 16) return 16;
@@ -746,27 +861,28 @@ int stack_bucket(int need) {
   return -1;
 }
 
-// Spheres staged in LDS when they fit this budget (keeps 4+ workgroups/CU).
+// Sphere pre-test records: LDS staging (sphere_src = 0, if they fit the budget
+// that keeps several workgroups per CU) or scalar loads (sphere_src = 1).
 constexpr int LDS_SPHERE_BYTES = 32 * 1024;
 
 template <bool COUNT, int MAXS, int WPS, int SRC>
-static hipError_t launch_one(const KParams& p, int n_sphere, dim3 grid, const double* rays, const int32_t* keys,
-                             int n, hipStream_t s) {
-  const size_t lds = (size_t)n_sphere * 16;
-  if (lds <= (size_t)LDS_SPHERE_BYTES)
-    hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, WPS, true, SRC>), grid, dim3(256), lds ? lds : 16, s, p, rays,
-                       keys, n);
+static hipError_t launch_one(const KParams& p, int n_sphere, int sphere_src, dim3 grid, const double* rays,
+                             const int32_t* keys, int n, hipStream_t s) {
+  const size_t lds = (size_t)(n_sphere + 4) * 16;
+  if (sphere_src == 0 && lds <= (size_t)LDS_SPHERE_BYTES)
+    hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, WPS, true, SRC>), grid, dim3(256), lds, s, p, rays, keys, n);
   else
     hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, WPS, false, SRC>), grid, dim3(256), 0, s, p, rays, keys, n);
   return hipGetLastError();
 }
 
-hipError_t launch_render(const KParams& p, int n_sphere, bool count, int maxs, int wps, hipStream_t s) {
+hipError_t launch_render(const KParams& p, int n_sphere, int sphere_src, bool count, int maxs, int wps,
+                         hipStream_t s) {
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   const dim3 grid((tiles + 3) / 4);
   if (tiles == 0) return hipSuccess;
 #define RTX_L(C, M, W) \
-  if (count == C && maxs == M && wps == W) return launch_one<C, M, W, SRC_PIXELS>(p, n_sphere, grid, nullptr, nullptr, 0, s);
+  if (count == C && maxs == M && wps == W) return launch_one<C, M, W, SRC_PIXELS>(p, n_sphere, sphere_src, grid, nullptr, nullptr, 0, s);
   RTX_L(false, 8, 2) RTX_L(false, 16, 2) RTX_L(false, 32, 2) RTX_L(false, 64, 2)
   RTX_L(false, 16, 1) RTX_L(false, 16, 3) RTX_L(false, 16, 4)
   RTX_L(true, 8, 2) RTX_L(true, 16, 2) RTX_L(true, 32, 2) RTX_L(true, 64, 2)
@@ -774,15 +890,15 @@ hipError_t launch_render(const KParams& p, int n_sphere, bool count, int maxs, i
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_trace(const KParams& p, int n_sphere, const double* rays, const int32_t* keys, int n, int maxs,
-                        hipStream_t s) {
+hipError_t launch_trace(const KParams& p, int n_sphere, int sphere_src, const double* rays, const int32_t* keys,
+                        int n, int maxs, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const dim3 grid((n + 255) / 256);
   switch (maxs) {
-    case 8: return launch_one<false, 8, 2, SRC_RAYS>(p, n_sphere, grid, rays, keys, n, s);
-    case 16: return launch_one<false, 16, 2, SRC_RAYS>(p, n_sphere, grid, rays, keys, n, s);
-    case 32: return launch_one<false, 32, 2, SRC_RAYS>(p, n_sphere, grid, rays, keys, n, s);
-    case 64: return launch_one<false, 64, 2, SRC_RAYS>(p, n_sphere, grid, rays, keys, n, s);
+    case 8: return launch_one<false, 8, 2, SRC_RAYS>(p, n_sphere, sphere_src, grid, rays, keys, n, s);
+    case 16: return launch_one<false, 16, 2, SRC_RAYS>(p, n_sphere, sphere_src, grid, rays, keys, n, s);
+    case 32: return launch_one<false, 32, 2, SRC_RAYS>(p, n_sphere, sphere_src, grid, rays, keys, n, s);
+    case 64: return launch_one<false, 64, 2, SRC_RAYS>(p, n_sphere, sphere_src, grid, rays, keys, n, s);
   }
   return hipErrorInvalidValue;
 }

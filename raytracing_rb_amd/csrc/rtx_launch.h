@@ -29,9 +29,10 @@ struct KParams {
 };
 
 int stack_bucket(int need);
-hipError_t launch_render(const KParams& p, int n_sphere, bool count, int maxs, int wps, hipStream_t s);
-hipError_t launch_trace(const KParams& p, int n_sphere, const double* rays, const int32_t* keys, int n, int maxs,
-                        hipStream_t s);
+hipError_t launch_render(const KParams& p, int n_sphere, int sphere_src, bool count, int maxs, int wps,
+                         hipStream_t s);
+hipError_t launch_trace(const KParams& p, int n_sphere, int sphere_src, const double* rays, const int32_t* keys,
+                        int n, int maxs, hipStream_t s);
 hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,
                            hipStream_t s);
 

@@ -1,0 +1,24 @@
+#!/usr/bin/env python3
+"""Phase breakdown of k_render from a -DRTX_STAMPS=1 build (diagnostic only)."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch
+from raytracing_rb_amd import config, _abi
+from raytracing_rb_amd.runtime import Renderer
+scene = sys.argv[1] if len(sys.argv) > 1 else "c2"
+sd, cd = config.load_scene(os.path.join(ROOT, "scenes", scene + "_world.yml"), os.path.join(ROOT, "scenes", scene + "_camera.yml"))
+r = Renderer(sd, cd)
+lib = _abi.load_library()
+out = torch.empty((cd.height, cd.width, 3), dtype=torch.float64, device="cuda")
+r.render_device(out.data_ptr()); r.sync()
+st = (ctypes.c_ulonglong * 8)()
+lib.rtxdbg_read_stamps(st, 1)
+r.render_device(out.data_ptr()); r.sync()
+lib.rtxdbg_read_stamps(st, 1)
+tA, tB, tC, tD, iters, waves, wexact, lexact = list(st)[:8]
+tot = tA + tB + tC + tD
+print("waves %d  iterations/wave %.1f" % (waves, iters / waves))
+for n, v in (("A fetch/pop/lens/highlight", tA), ("B query (object walk)", tB), ("C hit_info/lights", tC), ("D shade_finish", tD)):
+    print("%-28s %5.1f%%  %.0f cycles/wave  %.0f cycles/iteration" % (n, 100 * v / tot, v / waves, v / iters))
+print("exact sphere tests: per wave-iteration %.2f (any lane), per lane-query %.3f" % (wexact / iters, lexact / (iters * 64)))
