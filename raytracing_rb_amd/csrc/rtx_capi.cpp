@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -44,6 +45,7 @@ struct rtx_context {
   size_t scratch_bytes = 0;
   int64_t opt_force_stack = 0;
   int64_t opt_wps = 2;
+  int64_t opt_bvh = 1;               // build the bounding-ball hierarchy at scene upload
   int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
 };
 
@@ -70,6 +72,90 @@ static void free_scene(rtx_context* c) {
   c->d_bufs.clear();
   c->have_scene = false;
 }
+
+// ------------------------------------------------------------------ BVH build
+// Median split along the longest centroid axis, leaves of <= BVH_LEAF spheres,
+// pre-order layout with skip links.  Node balls are float32 and contain every
+// member ball exactly (radius rounded outwards); see DESIGN.md §2.1.
+namespace {
+struct BSph {
+  double c[3];
+  double r;
+  int rec;
+};
+
+static float f32_up(double x) {             // smallest float >= x (x >= 0)
+  float f = (float)x;
+  if ((double)f < x) f = nextafterf(f, INFINITY);
+  return f;
+}
+
+struct BvhBuilder {
+  std::vector<BSph>& sp;
+  std::vector<BvhNode> nodes;
+  std::vector<int32_t> slot_rec;
+  std::vector<float> slot32;
+  const std::vector<float>& sph32;
+  float max_scale = 0.0f;
+
+  int build(int lo, int hi) {
+    const int me = (int)nodes.size();
+    nodes.push_back(BvhNode{});
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = lo; i < hi; i++)
+      for (int a = 0; a < 3; a++) {
+        mn[a] = fmin(mn[a], sp[i].c[a] - sp[i].r);
+        mx[a] = fmax(mx[a], sp[i].c[a] + sp[i].r);
+      }
+    float cf[3];
+    for (int a = 0; a < 3; a++) cf[a] = (float)(0.5 * (mn[a] + mx[a]));
+    double rad = 0.0;
+    for (int i = lo; i < hi; i++) {
+      const double dx = sp[i].c[0] - cf[0], dy = sp[i].c[1] - cf[1], dz = sp[i].c[2] - cf[2];
+      rad = fmax(rad, sqrt(dx * dx + dy * dy + dz * dz) + fabs(sp[i].r));
+    }
+    rad = rad * (1.0 + 1e-9) + 1e-30;            // cover double rounding of the bound itself
+    BvhNode& n = nodes[me];
+    n.cx = cf[0];
+    n.cy = cf[1];
+    n.cz = cf[2];
+    n.r = f32_up(rad);
+    n.r2 = f32_up((double)n.r * (double)n.r);
+    const float sc = f32_up((fabs((double)cf[0]) + fabs((double)cf[1]) + fabs((double)cf[2]) + n.r) * (1.0 + 1e-6));
+    if (sc > max_scale) max_scale = sc;
+    if (hi - lo <= BVH_LEAF) {
+      n.first = (int)slot_rec.size();
+      n.count = hi - lo;
+      for (int u = 0; u < BVH_LEAF; u++) {
+        const int rec = lo + u < hi ? sp[lo + u].rec : -1;
+        slot_rec.push_back(rec);
+        for (int k = 0; k < 4; k++) slot32.push_back(rec >= 0 ? sph32[4 * rec + k] : 0.0f);
+      }
+      nodes[me].skip = me + 1;
+      return me;
+    }
+    double cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = lo; i < hi; i++)
+      for (int a = 0; a < 3; a++) {
+        cmn[a] = fmin(cmn[a], sp[i].c[a]);
+        cmx[a] = fmax(cmx[a], sp[i].c[a]);
+      }
+    int axis = 0;
+    for (int a = 1; a < 3; a++)
+      if (cmx[a] - cmn[a] > cmx[axis] - cmn[axis]) axis = a;
+    const int mid = (lo + hi) / 2;
+    std::nth_element(sp.begin() + lo, sp.begin() + mid, sp.begin() + hi, [axis](const BSph& a, const BSph& b) {
+      return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.rec < b.rec);
+    });
+    nodes[me].first = -1;
+    nodes[me].count = 0;
+    build(lo, mid);
+    build(mid, hi);
+    nodes[me].skip = (int)nodes.size();
+    return me;
+  }
+};
+}  // namespace
 
 extern "C" {
 
@@ -131,6 +217,10 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_force_stack = value;
     return RTX_OK;
   }
+  if (!strcmp(key, "bvh")) {               // 0: linear ordered walk; 1: hierarchy (applies at next upload)
+    c->opt_bvh = value != 0;
+    return RTX_OK;
+  }
   if (!strcmp(key, "sphere_src")) {        // sphere pre-test records: 0 = LDS, 1 = scalar loads
     if (value < 0 || value > 1) return fail(c, RTX_EINVAL, "sphere_src must be 0 or 1");
     c->opt_sphere_src = value;
@@ -180,6 +270,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   std::vector<Material> mat(sd->n_objects);
   std::vector<Sphere64> sph64;
   std::vector<float> sph32;
+  std::vector<int32_t> sph_obj;
   std::vector<double> planes, boxes;
   float sph_scale = 0.0f;
   for (int i = 0; i < sd->n_objects; i++) {
@@ -212,6 +303,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
     if (o.type == RTX_SPHERE) {
       if (!o.has_refractive_rate) return fail(c, RTX_EINVAL, "object %d: sphere needs refractive_rate", i);
       m.rec = (int)sph64.size();
+      sph_obj.push_back(i);
       Sphere64 sp;
       set3(sp.c, v3p(o.center));
       sp.r = o.radius;
@@ -251,6 +343,16 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   }
   if (err) return fail(c, RTX_EZERO_VEC, "zero vector detected while building the scene");
   if (!std::isfinite(sph_scale)) return fail(c, RTX_EINVAL, "non-finite sphere coordinates");
+  // bounding-ball hierarchy (before the padding records are appended)
+  std::vector<BSph> bs(sph64.size());
+  for (size_t k = 0; k < sph64.size(); k++) {
+    for (int a = 0; a < 3; a++) bs[k].c[a] = sph64[k].c[a];
+    bs[k].r = sph64[k].r;
+    bs[k].rec = (int)k;
+  }
+  BvhBuilder bb{bs, {}, {}, {}, sph32};
+  if (!bs.empty() && c->opt_bvh) bb.build(0, (int)bs.size());
+  if (bb.max_scale > sph_scale) sph_scale = bb.max_scale;
   for (int k = 0; k < 16; k++) sph32.push_back(0.0f);   // 4 padding records: group loads stay in bounds
   std::vector<LightDev> lights(sd->n_lights);
   for (int i = 0; i < sd->n_lights; i++) {
@@ -303,6 +405,10 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   HIPCHK(c, up(planes.data(), planes.size() * sizeof(double), &ptr));    S.planes = (const double*)ptr;
   HIPCHK(c, up(boxes.data(), boxes.size() * sizeof(double), &ptr));      S.boxes = (const double*)ptr;
   HIPCHK(c, up(mat.data(), mat.size() * sizeof(Material), &ptr));        S.mat = (const Material*)ptr;
+  HIPCHK(c, up(bb.nodes.data(), bb.nodes.size() * sizeof(BvhNode), &ptr)); S.bvh = (const BvhNode*)ptr;
+  HIPCHK(c, up(bb.slot32.data(), bb.slot32.size() * sizeof(float), &ptr)); S.bvh_sph32 = (const float*)ptr;
+  HIPCHK(c, up(bb.slot_rec.data(), bb.slot_rec.size() * sizeof(int32_t), &ptr)); S.bvh_rec = (const int32_t*)ptr;
+  HIPCHK(c, up(sph_obj.data(), sph_obj.size() * sizeof(int32_t), &ptr)); S.sph_obj = (const int32_t*)ptr;
   HIPCHK(c, up(lights.data(), lights.size() * sizeof(LightDev), &ptr));  S.light = (const LightDev*)ptr;
   HIPCHK(c, up(tex.data(), tex.size() * sizeof(TexDev), &ptr));          S.tex = (const TexDev*)ptr;
   HIPCHK(c, up(texels.data(), texels.size(), &ptr));                     S.texels = (const uint8_t*)ptr;
@@ -312,6 +418,8 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   S.n_plane = (int)(planes.size() / PLANE_GEO);
   S.n_box = (int)(boxes.size() / BOX_GEO);
   S.n_runs = (int)runs.size();
+  S.n_nodes = (int)bb.nodes.size();
+  S.n_slots = (int)bb.slot_rec.size();
   S.max_distance = sd->max_distance;
   S.sse = sd->soft_shadow_exponent;
   S.sph_scale = sph_scale;

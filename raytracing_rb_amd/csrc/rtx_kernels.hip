@@ -207,8 +207,15 @@ __device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o
   const double r2 = r * r;                        // front.r2
   // front.normalize is needed only by a sphere that passes the pre-test:
   // computed on first use (same bits wherever it is computed).
+#ifndef RTX_LAZY_DN
+#define RTX_LAZY_DN 0
+#endif
   V3 dn = d;
   bool have_dn = false;
+  if (!RTX_LAZY_DN) {
+    if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r);
+    have_dn = true;
+  }
   // float32 pre-test constants (exact culls)
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
   const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
@@ -263,7 +270,7 @@ __device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o
           keep |= (miss_line || behind) ? 0u : (1u << u);
         }
         if (k0 + 4 > run.count) keep &= (1u << (run.count - k0)) - 1u;
-#if RTX_STAMPS
+#if RTX_STAMPS == 2
         if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
           for (int u = 0; u < 4; u++) atomicAdd(&rtx_stamps[6], __ballot(keep >> u & 1) ? 1ull : 0ull);
         }

@@ -38,6 +38,23 @@ struct Sphere64 {
   double r;
 };
 
+// Bounding-ball hierarchy over the spheres (built on the host, rtx_capi.cpp).
+// Every node's ball contains the balls of all spheres below it (exactly, for
+// its float32 center and radius), so a float32 rejection of the node proves
+// the exact binary64 test of every member returns nil.
+// Nodes are stored in depth-first pre-order with a skip link (the index after
+// the node's subtree): traversal needs no stack.  Leaves hold <= 4 spheres
+// whose pre-test records sit in 4 contiguous slots; slot -> sphere record in
+// `bvh_rec` (-1 = padding).
+constexpr int BVH_LEAF = 4;
+struct BvhNode {
+  float cx, cy, cz, r2;   // ball center and radius^2 (radius^2 rounded up)
+  float r;                // ball radius (rounded up)
+  int32_t skip;           // first node after this subtree
+  int32_t first;          // leaf: first slot; internal: -1
+  int32_t count;          // leaf: number of spheres; internal: 0
+};
+
 struct Material {
   double diffuse[3];
   double ambient[3];
@@ -76,10 +93,15 @@ struct SceneDev {
   const double* planes;   // PLANE_GEO doubles per plane
   const double* boxes;    // BOX_GEO doubles per box
   const Material* mat;
+  const BvhNode* bvh;     // n_nodes nodes, root = 0 (n_nodes == 0: no hierarchy)
+  const float* bvh_sph32; // 4 floats per slot, BVH leaf order
+  const int32_t* bvh_rec; // slot -> sphere record (-1 = padding)
+  const int32_t* sph_obj; // sphere record -> global (YAML) object index
   const LightDev* light;
   const TexDev* tex;
   const uint8_t* texels;
   int32_t n_obj, n_light, n_sphere, n_plane, n_box, n_runs;
+  int32_t n_nodes, n_slots;
   double max_distance;
   double sse;             // soft_shadow_exponent
   float sph_scale;        // max over spheres of |C|_1 + R (pre-test margin scale)
