@@ -26,9 +26,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-WORLD = os.path.join(ROOT, "scenes", "c2_world.yml")
-CAMERA = os.path.join(ROOT, "scenes", "c2_camera.yml")
-WORKLOAD = "C2: 64 spheres + ground plane + area light (soft shadows), 1920x1080, 4x AA, depth 5"
+WORKLOADS = {
+    "c2": ("c2_world.yml", "c2_camera.yml",
+           "C2: 64 spheres + ground plane + area light (soft shadows), 1920x1080, 4x AA, depth 5"),
+    "c4": ("c4_world.yml", "c4_camera.yml",
+           "C4: 4096 random spheres + textured ground + area light, 3840x2160, 8x AA, depth 8"),
+}
+WORLD = os.path.join(ROOT, "scenes", WORKLOADS["c2"][0])
+CAMERA = os.path.join(ROOT, "scenes", WORKLOADS["c2"][1])
+WORKLOAD = WORKLOADS["c2"][2]
 METRIC = "Mpixels/sec at 1920×1080, 4× AA, depth 5; per-channel RMS vs ref"
 TILE_ROWS = 8
 
@@ -37,6 +43,8 @@ def cpu_baseline(col_stride=4, max_procs=16):
     """Time the C restatement (fork per core, camera.rb:54 column bands) on a
     strided column sample, in a child process started before any GPU init."""
     nprocs = max(1, min(max_procs, os.cpu_count() or 1))
+    if WORLD.endswith("c4_world.yml"):
+        col_stride = col_stride * 64           # C4: ~300x the work per pixel; keep the sample ~10-30 s
     code = (
         "import sys, time, json; sys.path.insert(0, %r)\n"
         "from raytracing_rb_amd import config\n"
@@ -60,9 +68,9 @@ def cpu_baseline(col_stride=4, max_procs=16):
     except Exception:
         pass
     return {"value": round(r["px"] / r["dt"] / 1e6, 5), "unit": "Mpixels/s", "cores": nprocs, "kind": "port",
-            "sample": "every %dth column of the C2 1920x1080 4xAA depth-5 frame (%d px), %d forked processes "
-                      "with camera.rb:54 column bands; %.1f s wall; CPU: %s" % (col_stride, r["px"], nprocs,
-                                                                              r["dt"], model)}
+            "sample": "every %dth column of the %s frame (%d px), %d forked processes "
+                      "with camera.rb:54 column bands; %.1f s wall; CPU: %s" % (col_stride, WORKLOAD.split(":")[0],
+                                                                              r["px"], nprocs, r["dt"], model)}
 
 
 def main():
@@ -71,8 +79,20 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--waves-per-simd", type=int, default=0)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
+                    help="c2: the metric's configuration (default); c4: the 4096-sphere stress scene")
+    ap.add_argument("--bvh", type=int, default=1, help="sphere walk: 0 ordered linear, 1 auto, 2 hierarchy")
     args = ap.parse_args()
+    global WORLD, CAMERA, WORKLOAD, METRIC
+    if args.workload != "c2":
+        if args.workload == "c4":
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import make_scenes
+            make_scenes.ensure_c4()
+        WORLD = os.path.join(ROOT, "scenes", WORKLOADS[args.workload][0])
+        CAMERA = os.path.join(ROOT, "scenes", WORKLOADS[args.workload][1])
+        WORKLOAD = WORKLOADS[args.workload][2]
+        METRIC = "Mpixels/sec at 3840×2160, 8× AA, depth 8 (C4, 4096 spheres)"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -101,8 +121,7 @@ def main():
     scene, cam = config.load_scene(WORLD, CAMERA)
     W, H = cam.width, cam.height
     r = Renderer(scene, cam, device=local_rank)
-    if args.waves_per_simd:
-        r.set_option("waves_per_simd", args.waves_per_simd)
+    r.set_option("bvh", args.bvh)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 

@@ -28,8 +28,9 @@ class ConfigError(ValueError):
     pass
 
 
-class _Loader(yaml.SafeLoader):
-    """YAML 1.1 as Psych reads it: ``1e-5`` is a Float (PyYAML needs a '.')."""
+class _Loader(getattr(yaml, "CSafeLoader", yaml.SafeLoader)):
+    """YAML 1.1 as Psych reads it: ``1e-5`` is a Float (PyYAML needs a '.').
+    libyaml's parser when present (same documents, ~6x faster on C4's 2 MB)."""
 
 
 _Loader.add_implicit_resolver(

@@ -44,8 +44,8 @@ struct rtx_context {
   double* d_scratch = nullptr;
   size_t scratch_bytes = 0;
   int64_t opt_force_stack = 0;
-  int64_t opt_wps = 2;
-  int64_t opt_bvh = 1;               // build the bounding-ball hierarchy at scene upload
+  int64_t opt_bvh = 1;               // 0: ordered linear walk; 1: hierarchy from opt_bvh_min spheres; 2: always
+  int64_t opt_bvh_min = 256;
   int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
 };
 
@@ -74,9 +74,11 @@ static void free_scene(rtx_context* c) {
 }
 
 // ------------------------------------------------------------------ BVH build
-// Median split along the longest centroid axis, leaves of <= BVH_LEAF spheres,
-// pre-order layout with skip links.  Node balls are float32 and contain every
-// member ball exactly (radius rounded outwards); see DESIGN.md §2.1.
+// Four-wide hierarchy: each node splits its spheres at the median of the
+// longest centroid axis, then splits each half again (up to four children);
+// groups of <= BVH_LEAF spheres become leaves.  Child balls are float32 and
+// contain every member sphere exactly (radius rounded outwards); see
+// DESIGN.md §2.1 and rtx_scene.h.
 namespace {
 struct BSph {
   double c[3];
@@ -90,50 +92,40 @@ static float f32_up(double x) {             // smallest float >= x (x >= 0)
   return f;
 }
 
-struct BvhBuilder {
+struct Bvh4Builder {
   std::vector<BSph>& sp;
-  std::vector<BvhNode> nodes;
-  std::vector<int32_t> slot_rec;
-  std::vector<float> slot32;
+  const std::vector<Sphere64>& sph64;
   const std::vector<float>& sph32;
+  const std::vector<int32_t>& sph_obj;
+  std::vector<Bvh4Node> nodes;
+  std::vector<float> slot32;
+  std::vector<Sphere64> slot64;
+  std::vector<int32_t> slot_obj;
   float max_scale = 0.0f;
+  int depth = 0;
 
-  int build(int lo, int hi) {
-    const int me = (int)nodes.size();
-    nodes.push_back(BvhNode{});
+  // float32 ball {cx, cy, cz, r} containing every sphere of sp[lo, hi)
+  void ball(int lo, int hi, float out[4]) {
     double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = lo; i < hi; i++)
       for (int a = 0; a < 3; a++) {
-        mn[a] = fmin(mn[a], sp[i].c[a] - sp[i].r);
-        mx[a] = fmax(mx[a], sp[i].c[a] + sp[i].r);
+        mn[a] = fmin(mn[a], sp[i].c[a] - fabs(sp[i].r));
+        mx[a] = fmax(mx[a], sp[i].c[a] + fabs(sp[i].r));
       }
-    float cf[3];
-    for (int a = 0; a < 3; a++) cf[a] = (float)(0.5 * (mn[a] + mx[a]));
+    for (int a = 0; a < 3; a++) out[a] = (float)(0.5 * (mn[a] + mx[a]));
     double rad = 0.0;
     for (int i = lo; i < hi; i++) {
-      const double dx = sp[i].c[0] - cf[0], dy = sp[i].c[1] - cf[1], dz = sp[i].c[2] - cf[2];
+      const double dx = sp[i].c[0] - out[0], dy = sp[i].c[1] - out[1], dz = sp[i].c[2] - out[2];
       rad = fmax(rad, sqrt(dx * dx + dy * dy + dz * dz) + fabs(sp[i].r));
     }
-    rad = rad * (1.0 + 1e-9) + 1e-30;            // cover double rounding of the bound itself
-    BvhNode& n = nodes[me];
-    n.cx = cf[0];
-    n.cy = cf[1];
-    n.cz = cf[2];
-    n.r = f32_up(rad);
-    n.r2 = f32_up((double)n.r * (double)n.r);
-    const float sc = f32_up((fabs((double)cf[0]) + fabs((double)cf[1]) + fabs((double)cf[2]) + n.r) * (1.0 + 1e-6));
+    rad = rad * (1.0 + 1e-9) + 1e-30;            // cover the double rounding of the bound itself
+    out[3] = f32_up(rad);
+    const float sc = f32_up((fabs((double)out[0]) + fabs((double)out[1]) + fabs((double)out[2]) + out[3]) *
+                            (1.0 + 1e-6));
     if (sc > max_scale) max_scale = sc;
-    if (hi - lo <= BVH_LEAF) {
-      n.first = (int)slot_rec.size();
-      n.count = hi - lo;
-      for (int u = 0; u < BVH_LEAF; u++) {
-        const int rec = lo + u < hi ? sp[lo + u].rec : -1;
-        slot_rec.push_back(rec);
-        for (int k = 0; k < 4; k++) slot32.push_back(rec >= 0 ? sph32[4 * rec + k] : 0.0f);
-      }
-      nodes[me].skip = me + 1;
-      return me;
-    }
+  }
+
+  int split(int lo, int hi) {                   // median split on the longest centroid axis
     double cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = lo; i < hi; i++)
       for (int a = 0; a < 3; a++) {
@@ -147,11 +139,44 @@ struct BvhBuilder {
     std::nth_element(sp.begin() + lo, sp.begin() + mid, sp.begin() + hi, [axis](const BSph& a, const BSph& b) {
       return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.rec < b.rec);
     });
-    nodes[me].first = -1;
-    nodes[me].count = 0;
-    build(lo, mid);
-    build(mid, hi);
-    nodes[me].skip = (int)nodes.size();
+    return mid;
+  }
+
+  int32_t leaf(int lo, int hi) {
+    const int id = (int)(slot_obj.size() / BVH_LEAF);
+    for (int u = 0; u < BVH_LEAF; u++) {
+      const int rec = lo + u < hi ? sp[lo + u].rec : -1;
+      slot_obj.push_back(rec >= 0 ? sph_obj[rec] : -1);
+      slot64.push_back(rec >= 0 ? sph64[rec] : Sphere64{{0.0, 0.0, 0.0}, 0.0});
+      for (int k = 0; k < 4; k++) slot32.push_back(rec >= 0 ? sph32[4 * rec + k] : 0.0f);
+    }
+    return ~(int32_t)((id << 3) | (hi - lo));
+  }
+
+  // Reference to the subtree over sp[lo, hi).
+  int32_t build(int lo, int hi, int lvl) {
+    if (lvl > depth) depth = lvl;
+    if (hi - lo <= BVH_LEAF) return leaf(lo, hi);
+    const int me = (int)nodes.size();
+    nodes.push_back(Bvh4Node{});
+    int g[5], ng = 0;
+    const int mid = split(lo, hi);
+    for (int h = 0; h < 2; h++) {
+      const int a = h ? mid : lo, b = h ? hi : mid;
+      g[ng++] = a;
+      if (b - a > BVH_LEAF) g[ng++] = split(a, b);
+    }
+    g[ng] = hi;
+    Bvh4Node n;
+    for (int k = 0; k < 4; k++) {
+      n.child[k] = BVH_NONE;
+      for (int a = 0; a < 4; a++) n.ball[k][a] = 0.0f;
+    }
+    for (int k = 0; k < ng; k++) {
+      ball(g[k], g[k + 1], n.ball[k]);
+      n.child[k] = build(g[k], g[k + 1], lvl + 1);
+    }
+    nodes[me] = n;
     return me;
   }
 };
@@ -217,18 +242,19 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_force_stack = value;
     return RTX_OK;
   }
-  if (!strcmp(key, "bvh")) {               // 0: linear ordered walk; 1: hierarchy (applies at next upload)
-    c->opt_bvh = value != 0;
+  if (!strcmp(key, "bvh")) {               // 0: linear ordered walk; 1: auto (>= bvh_min spheres); 2: always
+    if (value < 0 || value > 2) return fail(c, RTX_EINVAL, "bvh must be 0, 1 or 2");
+    c->opt_bvh = value;
     return RTX_OK;
   }
-  if (!strcmp(key, "sphere_src")) {        // sphere pre-test records: 0 = LDS, 1 = scalar loads
+  if (!strcmp(key, "bvh_min")) {           // sphere count from which bvh=1 uses the hierarchy
+    if (value < 0) return fail(c, RTX_EINVAL, "bvh_min must be >= 0");
+    c->opt_bvh_min = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads
     if (value < 0 || value > 1) return fail(c, RTX_EINVAL, "sphere_src must be 0 or 1");
     c->opt_sphere_src = value;
-    return RTX_OK;
-  }
-  if (!strcmp(key, "waves_per_simd")) {    // k_render occupancy variant (1..4; 16-entry stack only)
-    if (value < 1 || value > 4) return fail(c, RTX_EINVAL, "waves_per_simd must be 1..4");
-    c->opt_wps = value;
     return RTX_OK;
   }
   return fail(c, RTX_EINVAL, "unknown option '%s'", key);
@@ -350,8 +376,9 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
     bs[k].r = sph64[k].r;
     bs[k].rec = (int)k;
   }
-  BvhBuilder bb{bs, {}, {}, {}, sph32};
-  if (!bs.empty() && c->opt_bvh) bb.build(0, (int)bs.size());
+  Bvh4Builder bb{bs, sph64, sph32, sph_obj};
+  const int32_t bvh_root = bs.empty() ? BVH_NONE : bb.build(0, (int)bs.size(), 0);
+  if (3 * bb.depth + 4 > BVH_STACK) return fail(c, RTX_EINVAL, "sphere hierarchy too deep");
   if (bb.max_scale > sph_scale) sph_scale = bb.max_scale;
   for (int k = 0; k < 16; k++) sph32.push_back(0.0f);   // 4 padding records: group loads stay in bounds
   std::vector<LightDev> lights(sd->n_lights);
@@ -405,9 +432,10 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   HIPCHK(c, up(planes.data(), planes.size() * sizeof(double), &ptr));    S.planes = (const double*)ptr;
   HIPCHK(c, up(boxes.data(), boxes.size() * sizeof(double), &ptr));      S.boxes = (const double*)ptr;
   HIPCHK(c, up(mat.data(), mat.size() * sizeof(Material), &ptr));        S.mat = (const Material*)ptr;
-  HIPCHK(c, up(bb.nodes.data(), bb.nodes.size() * sizeof(BvhNode), &ptr)); S.bvh = (const BvhNode*)ptr;
+  HIPCHK(c, up(bb.nodes.data(), bb.nodes.size() * sizeof(Bvh4Node), &ptr)); S.bvh = (const Bvh4Node*)ptr;
   HIPCHK(c, up(bb.slot32.data(), bb.slot32.size() * sizeof(float), &ptr)); S.bvh_sph32 = (const float*)ptr;
-  HIPCHK(c, up(bb.slot_rec.data(), bb.slot_rec.size() * sizeof(int32_t), &ptr)); S.bvh_rec = (const int32_t*)ptr;
+  HIPCHK(c, up(bb.slot64.data(), bb.slot64.size() * sizeof(Sphere64), &ptr)); S.bvh_sph64 = (const Sphere64*)ptr;
+  HIPCHK(c, up(bb.slot_obj.data(), bb.slot_obj.size() * sizeof(int32_t), &ptr)); S.bvh_obj = (const int32_t*)ptr;
   HIPCHK(c, up(sph_obj.data(), sph_obj.size() * sizeof(int32_t), &ptr)); S.sph_obj = (const int32_t*)ptr;
   HIPCHK(c, up(lights.data(), lights.size() * sizeof(LightDev), &ptr));  S.light = (const LightDev*)ptr;
   HIPCHK(c, up(tex.data(), tex.size() * sizeof(TexDev), &ptr));          S.tex = (const TexDev*)ptr;
@@ -419,7 +447,8 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   S.n_box = (int)(boxes.size() / BOX_GEO);
   S.n_runs = (int)runs.size();
   S.n_nodes = (int)bb.nodes.size();
-  S.n_slots = (int)bb.slot_rec.size();
+  S.n_slots = (int)bb.slot_obj.size();
+  S.bvh_root = bvh_root;
   S.max_distance = sd->max_distance;
   S.sse = sd->soft_shadow_exponent;
   S.sph_scale = sph_scale;
@@ -474,6 +503,14 @@ static int required_stack(const rtx_context* c) {
   return need > 64 ? -1 : stack_bucket((int)need);
 }
 
+// Sphere walk of the next launch (SphMode); the launchers fall back to scalar
+// loads when the records exceed the LDS budget.
+static int sph_mode(const rtx_context* c) {
+  const bool bvh = c->opt_bvh == 2 || (c->opt_bvh == 1 && c->scene.n_sphere >= c->opt_bvh_min);
+  if (bvh && c->scene.bvh_root != BVH_NONE) return c->opt_sphere_src ? SPH_BVH_GLOBAL : SPH_BVH_LDS;
+  return c->opt_sphere_src ? SPH_LIN_SCALAR : SPH_LIN_LDS;
+}
+
 static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
   if (!c->have_scene) return fail(c, RTX_EINVAL, "no scene uploaded");
   if (!c->have_cam) return fail(c, RTX_EINVAL, "no camera set");
@@ -505,7 +542,7 @@ rtx_status rtx_render_device(rtx_context* c, int32_t x0, int32_t y0, int32_t x1,
   p.nrows = y1 - y0;
   p.out = d_out;
   p.stride = row_stride;
-  HIPCHK(c, launch_render(p, c->scene.n_sphere, (int)c->opt_sphere_src, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
+  HIPCHK(c, launch_render(p, sph_mode(c), false, maxs, (hipStream_t)stream));
   return RTX_OK;
 }
 
@@ -533,7 +570,7 @@ rtx_status rtx_render_tiles_device(rtx_context* c, int32_t tile_rows, int32_t ra
   p.nranks = nranks;
   p.out = d_packed;
   p.stride = (size_t)c->cam.width * 3;
-  HIPCHK(c, launch_render(p, c->scene.n_sphere, (int)c->opt_sphere_src, false, maxs, maxs == 16 ? (int)c->opt_wps : 2, (hipStream_t)stream));
+  HIPCHK(c, launch_render(p, sph_mode(c), false, maxs, (hipStream_t)stream));
   return RTX_OK;
 }
 
@@ -611,7 +648,7 @@ rtx_status rtx_trace(rtx_context* c, int32_t n, const double* rays, const int32_
   HIPCHK(c, hipMemcpy(d_rays, rays, rb, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(d_keys, keys, kb, hipMemcpyHostToDevice));
   p.out = d_out;
-  HIPCHK(c, launch_trace(p, c->scene.n_sphere, (int)c->opt_sphere_src, d_rays, d_keys, n, maxs, nullptr));
+  HIPCHK(c, launch_trace(p, sph_mode(c), d_rays, d_keys, n, maxs, nullptr));
   HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
   return rtx_sync(c, nullptr);
 }
@@ -632,7 +669,7 @@ rtx_status rtx_count_work(rtx_context* c, uint64_t seed, uint64_t counts[RTX_NCO
   p.nrows = H;
   p.out = c->d_scratch;
   p.stride = (size_t)W * 3;
-  HIPCHK(c, launch_render(p, c->scene.n_sphere, (int)c->opt_sphere_src, true, maxs, 2, nullptr));
+  HIPCHK(c, launch_render(p, sph_mode(c), true, maxs, nullptr));
   HIPCHK(c, hipDeviceSynchronize());
   unsigned long long tmp[RTX_NCOUNT];
   HIPCHK(c, hipMemcpy(tmp, c->d_counts, sizeof tmp, hipMemcpyDeviceToHost));

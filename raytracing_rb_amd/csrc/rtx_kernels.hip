@@ -339,6 +339,216 @@ __device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o
   }
 }
 
+// ----------------------------------------------------------------- the query, hierarchical
+// The same query answered through the four-wide ball hierarchy (rtx_scene.h)
+// with a wave-coherent traversal: the wave visits a node if any of its lanes
+// may need it, so every decision below is wave-uniform and the per-wave
+// stack lives in LDS.  A lane wants a child ball unless a float32 test with
+// the margins of DESIGN.md §2.1 proves that every sphere below it
+//   * misses the ray's line, or lies wholly behind the origin (nil), or
+//   * EXTEND: is farther than the lane's current best hit (loses the strict <
+//     of world.rb:48-50 even on a tie), or
+//   * SHADOW: lies wholly beyond the light (cover factor 0, sphere.rb:30).
+// Order independence makes the result bit-identical to the ordered walk:
+//   * EXTEND keeps the lexicographic minimum of (distance, object index) below
+//     max_distance, which is exactly what the ordered strict-< scan returns;
+//   * SHADOW collects the non-zero covers in a per-lane list sorted by object
+//     index and subtracts them in that order (world.rb:64-67).  A lane whose
+//     list overflows COVER_K repeats the ordered linear walk.
+// Planes and boxes are few: they are walked first (tightening `best`).
+__device__ __forceinline__ bool lex_better(double dist, int obj, double best, int besti) {
+  return dist < best || (dist == best && besti >= 0 && obj < besti);
+}
+
+template <int BS>
+__device__ __forceinline__ void push_cover(int* ci, double* cv, int& n, bool& ovf, int obj, double val) {
+  if (n >= COVER_K) {
+    ovf = true;
+    return;
+  }
+  int k = n;                                        // insertion sort by object index
+  while (k > 0) {
+    const int pi = ci[(k - 1) * BS];
+    if (pi < obj) break;
+    ci[k * BS] = pi;
+    cv[k * BS] = cv[(k - 1) * BS];
+    k--;
+  }
+  ci[k * BS] = obj;
+  cv[k * BS] = val;
+  n++;
+}
+
+template <int BS, typename NP, typename LP>
+__device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32, int* wstack, int* ci, double* cv,
+                                          bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
+                                          double& total, uint32_t& err) {
+  const double r = vr(d);
+  const double r2 = r * r;                        // front.r2
+  V3 dn = d;
+  if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r); // front.normalize (same bits as the walk)
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float dd = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+  const float Sx = fabsf(ox) + fabsf(oy) + fabsf(oz) + S.sph_scale;
+  const float ms2 = CULL_M * Sx * Sx;
+  const float mS = CULL_M * Sx;
+  const float kline = dd * ms2;
+  const float qneg = -CULL_M * Sx * sqrtf(dd);
+  const float sqd = sqrtf(dd);
+  // A non-finite ray makes no cull (every comparison below would be unordered).
+  const bool fin = __builtin_isfinite(dd) && __builtin_isfinite(Sx);
+  float bestf = (float)(best * (1.0 + 1e-6));      // >= best: culls keep a margin over it
+  int ncov = 0;
+  bool ovf = false;
+
+  // planes and boxes first, in run order (their order does not matter either)
+  const RTX_CONST Run* runs = cptr(S.runs);
+  const int n_runs = uni(S.n_runs);
+  for (int ri = 0; ri < n_runs; ri++) {
+    const int type = uni(runs[ri].type);
+    if (type == OBJ_SPHERE) continue;
+    const int obj0 = uni(runs[ri].obj0), count = uni(runs[ri].count), rec0 = uni(runs[ri].rec0);
+    for (int k = 0; k < count; k++) {
+      V3 hit;
+      bool h;
+      if (type == OBJ_PLANE) {
+        h = plane_hit(cptr(S.planes) + (size_t)(rec0 + k) * PLANE_GEO, o, d, hit);
+      } else {
+        int face;
+        h = box_hit(cptr(S.boxes) + (size_t)(rec0 + k) * BOX_GEO, o, d, hit, face);
+      }
+      if (!h) continue;
+      if (ext) {
+        const double dist = vr(vsub(o, hit));
+        if (lex_better(dist, obj0 + k, best, besti)) {
+          best = dist;
+          besti = obj0 + k;
+          bestf = (float)(best * (1.0 + 1e-6));
+        }
+      } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {
+        push_cover<BS>(ci, cv, ncov, ovf, obj0 + k, 1.0);
+      }
+    }
+  }
+
+  const bool leader = __lane_id() == (unsigned)__builtin_ctzll(__ballot(1));
+  const RTX_CONST Sphere64* s64 = cptr(S.bvh_sph64);
+  const RTX_CONST int32_t* sobj = cptr(S.bvh_obj);
+  int ref = uni(S.bvh_root);
+  int sp = 0;
+  while (ref != BVH_NONE) {
+    if (ref >= 0) {
+      // ---- internal node: test the four child balls for every lane
+      int ch[4];
+      float key[4];
+      uint64_t want[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        ch[k] = uni(nodes[ref].child[k]);
+        const float cx = nodes[ref].ball[k][0], cy = nodes[ref].ball[k][1], cz = nodes[ref].ball[k][2];
+        const float br = nodes[ref].ball[k][3];
+        const float ocx = cx - ox, ocy = cy - oy, ocz = cz - oz;
+        const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+        const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
+        const float rr = br + mS;
+        const bool line = __builtin_fmaf(s, dd, -q * q) <= __builtin_fmaf(dd, br * br, kline);
+        const bool front = q >= -rr * sqd;
+        const float fb = bestf + rr;
+        const bool reach = ext ? s <= fb * fb : q <= __builtin_fmaf(rr, sqd, dd);
+        const bool w = !fin || (line && front && reach);
+        want[k] = ch[k] != BVH_NONE ? __ballot(w) : 0ull;
+        key[k] = want[k] ? __builtin_bit_cast(float, uni(__builtin_bit_cast(int, q))) : __builtin_inff();
+        if (!(key[k] == key[k])) key[k] = 0.0f;
+        if (!want[k]) ch[k] = BVH_NONE;
+      }
+      // near-first for the wave's first lane (an ordering heuristic only)
+#define RTX_CS(a, b)                   \
+  if (key[b] < key[a]) {               \
+    const float tk = key[a];           \
+    key[a] = key[b];                   \
+    key[b] = tk;                       \
+    const int tc = ch[a];              \
+    ch[a] = ch[b];                     \
+    ch[b] = tc;                        \
+  }
+      RTX_CS(0, 1) RTX_CS(2, 3) RTX_CS(0, 2) RTX_CS(1, 3) RTX_CS(1, 2)
+#undef RTX_CS
+#pragma unroll
+      for (int k = 3; k >= 1; k--) {
+        if (ch[k] == BVH_NONE) continue;
+        if (leader) wstack[sp] = ch[k];
+        sp++;
+      }
+      if (ch[0] != BVH_NONE) {
+        ref = ch[0];
+        continue;
+      }
+    } else {
+      // ---- leaf: pre-test its spheres, exact test for those not ruled out
+      const int v = ~ref;
+      const int slot0 = (v >> 3) * BVH_LEAF;
+      const int cnt = v & 7;
+      float4 c[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int b = 4 * (slot0 + u);
+        c[u].x = leaf32[b];
+        c[u].y = leaf32[b + 1];
+        c[u].z = leaf32[b + 2];
+        c[u].w = leaf32[b + 3];
+      }
+      uint32_t keep = 0;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const float ocx = c[u].x - ox, ocy = c[u].y - oy, ocz = c[u].z - oz;
+        const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+        const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
+        const bool miss_line = __builtin_fmaf(s, dd, -q * q) > __builtin_fmaf(dd, c[u].w, kline);
+        const bool behind = q < qneg && s > c[u].w + ms2;
+        keep |= (miss_line || behind) ? 0u : (1u << u);
+      }
+      keep &= (1u << cnt) - 1u;
+      if (keep) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (!(keep >> u & 1)) continue;
+          const RTX_CONST Sphere64& sp64 = s64[slot0 + u];
+          const V3 C = v3(sp64.c[0], sp64.c[1], sp64.c[2]);
+          const double sr = sp64.r;
+          V3 hit;
+          bool in;
+          if (!sphere_exact(C, sr, o, d, dn, r2, hit, in)) continue;
+          const int obj = sobj[slot0 + u];
+          if (ext) {
+            const double dist = vr(vsub(o, hit));    // Ray#distance
+            if (lex_better(dist, obj, best, besti)) {
+              best = dist;
+              besti = obj;
+              bestf = (float)(best * (1.0 + 1e-6));
+            }
+          } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
+            const double cov = penumbra(C, sr, o, d, radius, err);
+            if (cov != 0.0) push_cover<BS>(ci, cv, ncov, ovf, obj, cov);
+          }
+        }
+      }
+    }
+    if (sp == 0) break;
+    sp--;
+    ref = uni(wstack[sp]);
+  }
+  if (!ext) {
+    total = 1.0;
+    if (ovf) {
+      // more than COVER_K non-zero covers: the ordered linear walk (rare)
+      query<false>(S, cptr(S.sph32), false, o, d, L, radius, best, besti, total, err, nullptr);
+    } else {
+      for (int k = 0; k < ncov; k++) total -= cv[k * BS];
+    }
+  }
+}
+
 // ----------------------------------------------------------------- shading
 // WorldObject#get_reflection_by_ray_and_n (world_object.rb:121-125).
 // nn = n.normalize, c = ray.front.cos(-n) (== ray.front.cos(n): |cos| of a
@@ -602,27 +812,40 @@ __device__ __forceinline__ int row_to_y(const KParams& p, int row) {
 
 // SRC_PIXELS: one lane per pixel (a wave covers an 8x8 tile) running
 // Camera#render_at.  SRC_RAYS: one lane per explicit ray running
-// RayTracer#trace_sync (rtx_trace).
-template <bool COUNT, int MAXS, int MAXPRE, int WPS, bool LDS, int SRC>
-__global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __restrict__ rays,
-                                                     const int32_t* __restrict__ keys, int nrays) {
+// RayTracer#trace_sync (rtx_trace).  SPH: where the sphere walk reads its
+// records (SphMode, rtx_launch.h).  BS: threads per workgroup.
+template <bool COUNT, int MAXS, int MAXPRE, int WPS, int SPH, int SRC, int BS>
+__global__ __launch_bounds__(BS, WPS) void k_render(KParams p, const double* __restrict__ rays,
+                                                    const int32_t* __restrict__ keys, int nrays) {
+  static_assert(!COUNT || SPH == SPH_LIN_LDS || SPH == SPH_LIN_SCALAR, "counting launches walk linearly");
   const SceneDev& S = p.scene;                // kernel argument: scalar loads
   const CameraDev& cam = *p.cam;
-  // Sphere pre-test records: staged in LDS (LDS = true) or read with scalar
-  // loads from the constant address space (LDS = false).
+  // Dynamic LDS: the sphere records of the walk (SPH_LIN_LDS: float32 pre-test
+  // records; SPH_BVH_LDS: hierarchy nodes at 0, leaf records at lds_leaf),
+  // then (BVH modes) the per-wave traversal stacks and per-lane cover lists.
   extern __shared__ float4 lds_sph[];
-  if (LDS) {
-    for (int i = threadIdx.x; i < S.n_sphere + 4; i += blockDim.x)
+  char* lds = reinterpret_cast<char*>(lds_sph);
+  if (SPH == SPH_LIN_LDS) {
+    for (int i = threadIdx.x; i < S.n_sphere + 4; i += BS)
       lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
+    __syncthreads();
+  } else if (SPH == SPH_BVH_LDS) {
+    const int nn = S.n_nodes * (int)(sizeof(Bvh4Node) / 16);
+    for (int i = threadIdx.x; i < nn; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.bvh)[i];
+    float4* leaf = reinterpret_cast<float4*>(lds + p.lds_leaf);
+    for (int i = threadIdx.x; i < S.n_slots; i += BS) leaf[i] = reinterpret_cast<const float4*>(S.bvh_sph32)[i];
     __syncthreads();
   }
   const float* sph_lds = reinterpret_cast<const float*>(lds_sph);
   const RTX_CONST float* sph_k = cptr(S.sph32);
+  int* wstack = reinterpret_cast<int*>(lds + p.lds_stack) + (threadIdx.x >> 6) * BVH_STACK;
+  int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
+  double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
 
   int x, y, row, px_ = 0;
   if (SRC == SRC_PIXELS) {
     const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int tile = blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
     const int tiles_x = (p.nx + 7) >> 3;
     px_ = (tile % tiles_x) * 8 + (lane & 7);
     row = (tile / tiles_x) * 8 + (lane >> 3);
@@ -743,10 +966,16 @@ __global__ __launch_bounds__(256, WPS) void k_render(KParams p, const double* __
     if (mode == M_DONE) break;
 
     // ---- B: the object walk, shared by EXTEND and SHADOW lanes
-    if (LDS)
+    if (SPH == SPH_LIN_LDS)
       query<COUNT>(S, sph_lds, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err, cnt);
-    else
+    else if (SPH == SPH_LIN_SCALAR)
       query<COUNT>(S, sph_k, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err, cnt);
+    else if (SPH == SPH_BVH_LDS)
+      query_bvh<BS>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float*>(lds + p.lds_leaf),
+                    wstack, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err);
+    else
+      query_bvh<BS>(S, cptr(S.bvh), cptr(S.bvh_sph32), wstack, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad,
+                    best, besti, total, err);
     if (RTX_STAMPS) {
       t1 = stamp();
       tB += t1 - t0;
@@ -868,44 +1097,108 @@ int stack_bucket(int need) {
   return -1;
 }
 
-// Sphere pre-test records: LDS staging (sphere_src = 0, if they fit the budget
-// that keeps several workgroups per CU) or scalar loads (sphere_src = 1).
-constexpr int LDS_SPHERE_BYTES = 32 * 1024;
+// LDS budgets.  Linear walk: 16 B per sphere in 256-thread workgroups, small
+// enough for several workgroups per CU.  Hierarchy: nodes + leaf records in
+// one 512-thread workgroup per CU (2 waves per SIMD, the register-limited
+// occupancy), next to its stacks and cover lists.
+constexpr size_t LDS_SPHERE_BYTES = 32 * 1024;
+constexpr size_t LDS_TOTAL_BYTES = 160 * 1024;
+constexpr int BS_LIN = 256, BS_BVH = 512;
 
-template <bool COUNT, int MAXS, int WPS, int SRC>
-static hipError_t launch_one(const KParams& p, int n_sphere, int sphere_src, dim3 grid, const double* rays,
-                             const int32_t* keys, int n, hipStream_t s) {
-  const size_t lds = (size_t)(n_sphere + 4) * 16;
-  if (sphere_src == 0 && lds <= (size_t)LDS_SPHERE_BYTES)
-    hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, WPS, true, SRC>), grid, dim3(256), lds, s, p, rays, keys, n);
-  else
-    hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, WPS, false, SRC>), grid, dim3(256), 0, s, p, rays, keys, n);
+static size_t bvh_lds_fixed(int bs) {
+  return (size_t)(bs / 64) * BVH_STACK * 4 + (size_t)COVER_K * bs * 12;
+}
+
+int resolve_mode(const SceneDev& S, int mode) {
+  if (mode == SPH_LIN_LDS && (size_t)(S.n_sphere + 4) * 16 > LDS_SPHERE_BYTES) return SPH_LIN_SCALAR;
+  if (mode == SPH_BVH_LDS &&
+      (size_t)S.n_nodes * sizeof(Bvh4Node) + (size_t)S.n_slots * 16 + bvh_lds_fixed(BS_BVH) > LDS_TOTAL_BYTES)
+    return SPH_BVH_GLOBAL;
+  return mode;
+}
+
+// Fills the LDS layout of `p` for `mode` and returns the dynamic LDS bytes.
+static size_t lds_layout(KParams& p, int mode, int bs) {
+  const SceneDev& S = p.scene;
+  size_t off = 0;
+  if (mode == SPH_LIN_LDS) off = (size_t)(S.n_sphere + 4) * 16;
+  if (mode == SPH_BVH_LDS) {
+    off = (size_t)S.n_nodes * sizeof(Bvh4Node);
+    p.lds_leaf = (int32_t)off;
+    off += (size_t)S.n_slots * 16;
+  }
+  off = (off + 15) & ~(size_t)15;
+  p.lds_stack = (int32_t)off;
+  p.lds_cov = (int32_t)off;
+  if (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL) {
+    off += (size_t)(bs / 64) * BVH_STACK * 4;
+    off = (off + 15) & ~(size_t)15;
+    p.lds_cov = (int32_t)off;
+    off += (size_t)COVER_K * bs * 12;
+  }
+  return off;
+}
+
+template <bool COUNT, int MAXS, int SPH, int SRC>
+static hipError_t launch_one(KParams p, dim3 grid_px, const double* rays, const int32_t* keys, int n,
+                             hipStream_t s) {
+  constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
+  const size_t lds = lds_layout(p, SPH, BS);
+  dim3 grid;
+  if (SRC == SRC_PIXELS) {
+    const int tiles = (int)grid_px.x;
+    grid = dim3((tiles + BS / 64 - 1) / (BS / 64));
+  } else {
+    grid = dim3((n + BS - 1) / BS);
+  }
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_render<COUNT, MAXS, 16, 2, SPH, SRC, BS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, 2, SPH, SRC, BS>), grid, dim3(BS), lds, s, p, rays, keys, n);
   return hipGetLastError();
 }
 
-hipError_t launch_render(const KParams& p, int n_sphere, int sphere_src, bool count, int maxs, int wps,
-                         hipStream_t s) {
+template <bool COUNT, int MAXS, int SRC>
+static hipError_t launch_mode(const KParams& p, int mode, dim3 g, const double* rays, const int32_t* keys, int n,
+                              hipStream_t s) {
+  switch (COUNT ? (mode == SPH_LIN_LDS ? SPH_LIN_LDS : SPH_LIN_SCALAR) : mode) {
+    case SPH_LIN_LDS: return launch_one<COUNT, MAXS, SPH_LIN_LDS, SRC>(p, g, rays, keys, n, s);
+    case SPH_LIN_SCALAR: return launch_one<COUNT, MAXS, SPH_LIN_SCALAR, SRC>(p, g, rays, keys, n, s);
+    case SPH_BVH_LDS:
+      if (!COUNT) return launch_one<false, MAXS, SPH_BVH_LDS, SRC>(p, g, rays, keys, n, s);
+      break;
+    case SPH_BVH_GLOBAL:
+      if (!COUNT) return launch_one<false, MAXS, SPH_BVH_GLOBAL, SRC>(p, g, rays, keys, n, s);
+      break;
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s) {
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
-  const dim3 grid((tiles + 3) / 4);
   if (tiles == 0) return hipSuccess;
-#define RTX_L(C, M, W) \
-  if (count == C && maxs == M && wps == W) return launch_one<C, M, W, SRC_PIXELS>(p, n_sphere, sphere_src, grid, nullptr, nullptr, 0, s);
-  RTX_L(false, 8, 2) RTX_L(false, 16, 2) RTX_L(false, 32, 2) RTX_L(false, 64, 2)
-  RTX_L(false, 16, 1) RTX_L(false, 16, 3) RTX_L(false, 16, 4)
-  RTX_L(true, 8, 2) RTX_L(true, 16, 2) RTX_L(true, 32, 2) RTX_L(true, 64, 2)
+  if (count) mode = (mode == SPH_LIN_LDS || mode == SPH_BVH_LDS) ? SPH_LIN_LDS : SPH_LIN_SCALAR;
+  mode = resolve_mode(p.scene, mode);
+  const dim3 g(tiles);
+#define RTX_L(M)                                                                      \
+  if (maxs == M)                                                                      \
+    return count ? launch_mode<true, M, SRC_PIXELS>(p, mode, g, nullptr, nullptr, 0, s) \
+                 : launch_mode<false, M, SRC_PIXELS>(p, mode, g, nullptr, nullptr, 0, s);
+  RTX_L(8) RTX_L(16) RTX_L(32) RTX_L(64)
 #undef RTX_L
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_trace(const KParams& p, int n_sphere, int sphere_src, const double* rays, const int32_t* keys,
-                        int n, int maxs, hipStream_t s) {
+hipError_t launch_trace(KParams p, int mode, const double* rays, const int32_t* keys, int n, int maxs,
+                        hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const dim3 grid((n + 255) / 256);
+  mode = resolve_mode(p.scene, mode);
+  const dim3 g(0);
   switch (maxs) {
-    case 8: return launch_one<false, 8, 2, SRC_RAYS>(p, n_sphere, sphere_src, grid, rays, keys, n, s);
-    case 16: return launch_one<false, 16, 2, SRC_RAYS>(p, n_sphere, sphere_src, grid, rays, keys, n, s);
-    case 32: return launch_one<false, 32, 2, SRC_RAYS>(p, n_sphere, sphere_src, grid, rays, keys, n, s);
-    case 64: return launch_one<false, 64, 2, SRC_RAYS>(p, n_sphere, sphere_src, grid, rays, keys, n, s);
+    case 8: return launch_mode<false, 8, SRC_RAYS>(p, mode, g, rays, keys, n, s);
+    case 16: return launch_mode<false, 16, SRC_RAYS>(p, mode, g, rays, keys, n, s);
+    case 32: return launch_mode<false, 32, SRC_RAYS>(p, mode, g, rays, keys, n, s);
+    case 64: return launch_mode<false, 64, SRC_RAYS>(p, mode, g, rays, keys, n, s);
   }
   return hipErrorInvalidValue;
 }

@@ -26,13 +26,26 @@ struct KParams {
   size_t stride;                   // doubles per output row
   ErrState* err;
   unsigned long long* counts;      // RTX_NCOUNT counters (counting launches only)
+  // dynamic LDS layout (bytes), filled by launch_render/launch_trace
+  int32_t lds_leaf, lds_stack, lds_cov;
+};
+
+// Where the sphere walk reads its records:
+enum SphMode : int {
+  SPH_LIN_LDS = 0,       // ordered linear walk, float32 pre-test records staged in LDS
+  SPH_LIN_SCALAR = 1,    // ordered linear walk, records by scalar loads
+  SPH_BVH_LDS = 2,       // four-wide ball hierarchy, nodes + leaf records staged in LDS
+  SPH_BVH_GLOBAL = 3,    // four-wide ball hierarchy, nodes + leaf records by scalar loads
 };
 
 int stack_bucket(int need);
-hipError_t launch_render(const KParams& p, int n_sphere, int sphere_src, bool count, int maxs, int wps,
-                         hipStream_t s);
-hipError_t launch_trace(const KParams& p, int n_sphere, int sphere_src, const double* rays, const int32_t* keys,
-                        int n, int maxs, hipStream_t s);
+// mode: SphMode; a linear mode whose records exceed the LDS budget falls back to
+// SPH_LIN_SCALAR, a BVH mode to SPH_BVH_GLOBAL.  Counting launches always walk
+// linearly (the counters are the reference's brute-force events).
+hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s);
+hipError_t launch_trace(KParams p, int mode, const double* rays, const int32_t* keys, int n, int maxs,
+                        hipStream_t s);
+int resolve_mode(const SceneDev& S, int mode);
 hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,
                            hipStream_t s);
 

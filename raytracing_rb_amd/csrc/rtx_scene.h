@@ -38,22 +38,30 @@ struct Sphere64 {
   double r;
 };
 
-// Bounding-ball hierarchy over the spheres (built on the host, rtx_capi.cpp).
-// Every node's ball contains the balls of all spheres below it (exactly, for
-// its float32 center and radius), so a float32 rejection of the node proves
-// the exact binary64 test of every member returns nil.
-// Nodes are stored in depth-first pre-order with a skip link (the index after
-// the node's subtree): traversal needs no stack.  Leaves hold <= 4 spheres
-// whose pre-test records sit in 4 contiguous slots; slot -> sphere record in
-// `bvh_rec` (-1 = padding).
+// Four-wide bounding-ball hierarchy over the spheres (built on the host,
+// rtx_capi.cpp).  A node holds the balls of its (up to) four children; every
+// child ball contains every sphere below it exactly (float32 center, radius
+// rounded outwards), so a float32 rejection of a child ball with the margins
+// of DESIGN.md §2.1 proves the exact binary64 test of every sphere below it
+// returns nil (or, for a shadow query, a zero cover).
+//   child[k] >= 0        : internal node index
+//   child[k] == BVH_NONE : empty slot
+//   child[k] <  0        : leaf, ~child = leaf << 3 | count; its `count` (1..4)
+//                          spheres sit in slots 4*leaf .. 4*leaf+count-1 of the
+//                          slot arrays (float32 pre-test record, binary64 record,
+//                          global object index); unused slots are padding.
+// Nodes are in pre-order (root = 0).  The traversal order never matters for
+// the result: nearest hits compare (distance, object index) lexicographically
+// and shadow covers are subtracted in object order (rtx_kernels.hip).
 constexpr int BVH_LEAF = 4;
-struct BvhNode {
-  float cx, cy, cz, r2;   // ball center and radius^2 (radius^2 rounded up)
-  float r;                // ball radius (rounded up)
-  int32_t skip;           // first node after this subtree
-  int32_t first;          // leaf: first slot; internal: -1
-  int32_t count;          // leaf: number of spheres; internal: 0
+constexpr int32_t BVH_NONE = 0x7fffffff;
+constexpr int BVH_STACK = 64;     // per-wave traversal stack entries (LDS)
+constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); more -> ordered re-walk
+struct Bvh4Node {
+  float ball[4][4];       // per child: cx, cy, cz, radius (rounded up)
+  int32_t child[4];
 };
+static_assert(sizeof(Bvh4Node) == 80, "Bvh4Node layout");
 
 struct Material {
   double diffuse[3];
@@ -93,15 +101,17 @@ struct SceneDev {
   const double* planes;   // PLANE_GEO doubles per plane
   const double* boxes;    // BOX_GEO doubles per box
   const Material* mat;
-  const BvhNode* bvh;     // n_nodes nodes, root = 0 (n_nodes == 0: no hierarchy)
-  const float* bvh_sph32; // 4 floats per slot, BVH leaf order
-  const int32_t* bvh_rec; // slot -> sphere record (-1 = padding)
+  const Bvh4Node* bvh;    // n_nodes nodes, root = 0
+  const float* bvh_sph32; // 4 floats per slot {cx, cy, cz, R^2}, leaf order
+  const Sphere64* bvh_sph64; // binary64 record per slot
+  const int32_t* bvh_obj; // slot -> global (YAML) object index (-1 = padding)
   const int32_t* sph_obj; // sphere record -> global (YAML) object index
   const LightDev* light;
   const TexDev* tex;
   const uint8_t* texels;
   int32_t n_obj, n_light, n_sphere, n_plane, n_box, n_runs;
   int32_t n_nodes, n_slots;
+  int32_t bvh_root;       // root reference (BVH_NONE: no spheres)
   double max_distance;
   double sse;             // soft_shadow_exponent
   float sph_scale;        // max over spheres of |C|_1 + R (pre-test margin scale)

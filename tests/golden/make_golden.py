@@ -8,6 +8,10 @@ Fixtures (numpy .npz, data only):
                     committed scene at a reduced size (scene YAML sha256 kept to
                     detect drift)
   vectors.npz       counter-RNG values, Camera#lens_func rays, trace_sync colours
+  frame_c4_48x27.npz the 4096-sphere C4 scene: rendered by the C restatement
+                    (oracle/rt_oracle.c, bit-checked against rt_ref.py on the other
+                    frames and on sampled C4 pixels in tests/test_oracle.py), since
+                    the pure-Python walk over 4097 objects would take hours
 
     python tests/golden/make_golden.py
 """
@@ -74,7 +78,31 @@ def vectors():
                 scene_sha=sha(os.path.join(SC, "c2_world.yml")))
 
 
+C_FRAMES = {
+    "c4_48x27": ("c4_world.yml", "c4_camera.yml", {"width": 48, "height": 27}),
+}
+
+
+def render_c(world, camera, ov, seed=1):
+    from oracle.c_oracle import Oracle
+    from raytracing_rb_amd import config
+    sd, cd = config.load_scene(os.path.join(SC, world), os.path.join(SC, camera), camera_overrides=ov)
+    fb, st, rc = Oracle(sd, cd).render(seed=seed)
+    return fb, st.astype(np.int32)
+
+
 def main(only=None):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_scenes
+    make_scenes.ensure_c4()
+    for name, (world, camera, ov) in C_FRAMES.items():
+        if only and name not in only:
+            continue
+        fb, st = render_c(world, camera, ov)
+        np.savez_compressed(os.path.join(HERE, "frame_%s.npz" % name), frame=fb, status=st,
+                            world=world, camera=camera, overrides=repr(ov),
+                            scene_sha=sha(os.path.join(SC, world)), seed=1, source="rt_oracle.c")
+        print(name, fb.shape, "errors", int((st != 0).sum()), "mean", fb.mean(axis=(0, 1)))
     for name, (world, camera, ov) in FRAMES.items():
         if only and name not in only:
             continue

@@ -119,3 +119,28 @@ def test_color_gt1_raise_site(oracle_lib, tmp_path):
             except Exception as e:
                 pys[y, x] = {"color_gt1": 2, "zero_vec": 1, "domain": 3}[e.kind]
     assert np.array_equal(pys, st)
+
+
+@pytest.fixture(scope="module")
+def c4_scene():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(SCENES), "tools"))
+    import make_scenes
+    return make_scenes.ensure_c4()
+
+
+def test_c4_golden_and_python_restatement_on_sampled_pixels(oracle_lib, c4_scene):
+    """C4 (4096 spheres): the committed golden (made by the C restatement) is
+    reproduced bit for bit, and the pure-Python restatement agrees with the C
+    one on sampled pixels (all 8 samples, depth 8)."""
+    z = _load("c4_48x27")
+    assert _sha(c4_scene) == str(z["scene_sha"]), "scene file drifted from fixture"
+    ov = eval(str(z["overrides"]), {})
+    sd, cd = config.load_scene(c4_scene, os.path.join(SCENES, "c4_camera.yml"), camera_overrides=ov)
+    xy = np.array([[5, 3], [24, 13], [40, 20]], np.int32)
+    ref, st, rc = Oracle(sd, cd).render_pixels(xy, seed=1)
+    assert rc == 0
+    assert np.array_equal(ref.view(np.uint64), z["frame"][xy[:, 1], xy[:, 0]].view(np.uint64))
+    _, cam = rt_ref.load_scene(c4_scene, os.path.join(SCENES, "c4_camera.yml"), seed=1, overrides=ov)
+    py = np.array([cam.render_at(int(x), int(y)).to_a() for x, y in xy], dtype=np.float64)
+    assert np.array_equal(py.view(np.uint64), ref.view(np.uint64))

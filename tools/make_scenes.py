@@ -242,6 +242,17 @@ def c4():
     return s
 
 
+def ensure_c4():
+    """scenes/c4_world.yml is generated (2 MB, not committed): write it if missing."""
+    path = os.path.join(SC, "c4_world.yml")
+    if not os.path.exists(path):
+        tmp = path + ".%d.tmp" % os.getpid()
+        with open(tmp, "w") as fh:
+            fh.write(c4())
+        os.replace(tmp, path)
+    return path
+
+
 def main():
     os.makedirs(SC, exist_ok=True)
     textures()

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Time k_render on one scene under several runtime options (GPU box).
+
+    python tools/timing.py --scene c2 [--size 1920x1080] [--reps 5] '{"bvh": 0}' '{"bvh": 2}'
+
+Prints per-option min/median kernel ms (HIP events on the launch stream) and a
+hash of the frame (every option must render the same bits).
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="c2")
+    ap.add_argument("--size", default="")
+    ap.add_argument("--spp", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("opts", nargs="*")
+    a = ap.parse_args()
+    import torch
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import Renderer
+    if a.scene == "c4":
+        import make_scenes
+        make_scenes.ensure_c4()
+    ov = {}
+    if a.size:
+        w, h = a.size.split("x")
+        ov.update(width=int(w), height=int(h))
+    if a.spp:
+        ov.update(pre_sample_times=a.spp, max_sample_times=a.spp)
+    sd, cd = config.load_scene(os.path.join(ROOT, "scenes", a.scene + "_world.yml"),
+                               os.path.join(ROOT, "scenes", a.scene + "_camera.yml"), camera_overrides=ov)
+    r = Renderer(sd, cd)
+    out = torch.empty((cd.height, cd.width, 3), dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    for o in (a.opts or ["{}"]):
+        opts = json.loads(o)
+        for k, v in opts.items():
+            r.set_option(k, v)
+        r.render_device(out.data_ptr(), stream=s.cuda_stream)
+        r.sync(s.cuda_stream)
+        ts = []
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r.render_device(out.data_ptr(), stream=s.cuda_stream)
+            e1.record(s)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        r.sync(s.cuda_stream)
+        ts.sort()
+        sha = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
+        print("%-8s %-40s min %9.3f ms  median %9.3f ms  %8.2f Mpix/s  sha %s" % (
+            a.scene, o, ts[0], ts[len(ts) // 2], cd.width * cd.height / ts[len(ts) // 2] / 1e3, sha), flush=True)
+
+
+if __name__ == "__main__":
+    main()
