@@ -76,8 +76,8 @@ static void free_scene(rtx_context* c) {
 // ------------------------------------------------------------------ BVH build
 // Four-wide hierarchy: each node splits its spheres at the median of the
 // longest centroid axis, then splits each half again (up to four children);
-// groups of <= BVH_LEAF spheres become leaves.  Child balls are float32 and
-// contain every member sphere exactly (radius rounded outwards); see
+// groups of <= BVH_LEAF spheres become leaves.  Child boxes are float32 and
+// contain every member sphere exactly (bounds rounded outwards); see
 // DESIGN.md §2.1 and rtx_scene.h.
 namespace {
 struct BSph {
@@ -86,7 +86,12 @@ struct BSph {
   int rec;
 };
 
-static float f32_up(double x) {             // smallest float >= x (x >= 0)
+static float f32_down(double x) {           // largest float <= x
+  float f = (float)x;
+  if ((double)f > x) f = nextafterf(f, -INFINITY);
+  return f;
+}
+static float f32_up(double x) {             // smallest float >= x
   float f = (float)x;
   if ((double)f < x) f = nextafterf(f, INFINITY);
   return f;
@@ -101,28 +106,21 @@ struct Bvh4Builder {
   std::vector<float> slot32;
   std::vector<Sphere64> slot64;
   std::vector<int32_t> slot_obj;
-  float max_scale = 0.0f;
-  int depth = 0;
+  int stack = 0;                              // worst-case traversal stack (3 pushes per internal level)
 
-  // float32 ball {cx, cy, cz, r} containing every sphere of sp[lo, hi)
-  void ball(int lo, int hi, float out[4]) {
-    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = lo; i < hi; i++)
-      for (int a = 0; a < 3; a++) {
-        mn[a] = fmin(mn[a], sp[i].c[a] - fabs(sp[i].r));
-        mx[a] = fmax(mx[a], sp[i].c[a] + fabs(sp[i].r));
+  // float32 box containing every sphere of sp[lo, hi); the double bounds are
+  // widened by a relative 1e-12 to cover their own rounding.
+  void box(int lo, int hi, float blo[3], float bhi[3]) {
+    for (int a = 0; a < 3; a++) {
+      double mn = INFINITY, mx = -INFINITY;
+      for (int i = lo; i < hi; i++) {
+        const double r = fabs(sp[i].r);
+        mn = fmin(mn, sp[i].c[a] - r);
+        mx = fmax(mx, sp[i].c[a] + r);
       }
-    for (int a = 0; a < 3; a++) out[a] = (float)(0.5 * (mn[a] + mx[a]));
-    double rad = 0.0;
-    for (int i = lo; i < hi; i++) {
-      const double dx = sp[i].c[0] - out[0], dy = sp[i].c[1] - out[1], dz = sp[i].c[2] - out[2];
-      rad = fmax(rad, sqrt(dx * dx + dy * dy + dz * dz) + fabs(sp[i].r));
+      blo[a] = f32_down(mn - 1e-12 * fabs(mn) - 1e-300);
+      bhi[a] = f32_up(mx + 1e-12 * fabs(mx) + 1e-300);
     }
-    rad = rad * (1.0 + 1e-9) + 1e-30;            // cover the double rounding of the bound itself
-    out[3] = f32_up(rad);
-    const float sc = f32_up((fabs((double)out[0]) + fabs((double)out[1]) + fabs((double)out[2]) + out[3]) *
-                            (1.0 + 1e-6));
-    if (sc > max_scale) max_scale = sc;
   }
 
   int split(int lo, int hi) {                   // median split on the longest centroid axis
@@ -147,15 +145,14 @@ struct Bvh4Builder {
     for (int u = 0; u < BVH_LEAF; u++) {
       const int rec = lo + u < hi ? sp[lo + u].rec : -1;
       slot_obj.push_back(rec >= 0 ? sph_obj[rec] : -1);
-      slot64.push_back(rec >= 0 ? sph64[rec] : Sphere64{{0.0, 0.0, 0.0}, 0.0});
+      slot64.push_back(rec >= 0 ? sph64[rec] : Sphere64{{0.0, 0.0, 0.0}, -1.0});
       for (int k = 0; k < 4; k++) slot32.push_back(rec >= 0 ? sph32[4 * rec + k] : 0.0f);
     }
-    return ~(int32_t)((id << 3) | (hi - lo));
+    return ~(int32_t)((id << 2) | (hi - lo - 1));
   }
 
-  // Reference to the subtree over sp[lo, hi).
-  int32_t build(int lo, int hi, int lvl) {
-    if (lvl > depth) depth = lvl;
+  // Reference to the subtree over sp[lo, hi); `pushes` = stack entries above it.
+  int32_t build(int lo, int hi, int pushes) {
     if (hi - lo <= BVH_LEAF) return leaf(lo, hi);
     const int me = (int)nodes.size();
     nodes.push_back(Bvh4Node{});
@@ -170,11 +167,21 @@ struct Bvh4Builder {
     Bvh4Node n;
     for (int k = 0; k < 4; k++) {
       n.child[k] = BVH_NONE;
-      for (int a = 0; a < 4; a++) n.ball[k][a] = 0.0f;
+      for (int a = 0; a < 3; a++) {
+        n.lo[a][k] = 0.0f;
+        n.hi[a][k] = 0.0f;
+      }
     }
+    const int below = pushes + ng - 1;          // visiting one child leaves <= ng-1 siblings pushed
+    if (below > stack) stack = below;
     for (int k = 0; k < ng; k++) {
-      ball(g[k], g[k + 1], n.ball[k]);
-      n.child[k] = build(g[k], g[k + 1], lvl + 1);
+      float blo[3], bhi[3];
+      box(g[k], g[k + 1], blo, bhi);
+      for (int a = 0; a < 3; a++) {
+        n.lo[a][k] = blo[a];
+        n.hi[a][k] = bhi[a];
+      }
+      n.child[k] = build(g[k], g[k + 1], below);
     }
     nodes[me] = n;
     return me;
@@ -378,8 +385,6 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   }
   Bvh4Builder bb{bs, sph64, sph32, sph_obj};
   const int32_t bvh_root = bs.empty() ? BVH_NONE : bb.build(0, (int)bs.size(), 0);
-  if (3 * bb.depth + 4 > BVH_STACK) return fail(c, RTX_EINVAL, "sphere hierarchy too deep");
-  if (bb.max_scale > sph_scale) sph_scale = bb.max_scale;
   for (int k = 0; k < 16; k++) sph32.push_back(0.0f);   // 4 padding records: group loads stay in bounds
   std::vector<LightDev> lights(sd->n_lights);
   for (int i = 0; i < sd->n_lights; i++) {
@@ -449,6 +454,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   S.n_nodes = (int)bb.nodes.size();
   S.n_slots = (int)bb.slot_obj.size();
   S.bvh_root = bvh_root;
+  S.bvh_stack = bb.stack + 1;
   S.max_distance = sd->max_distance;
   S.sse = sd->soft_shadow_exponent;
   S.sph_scale = sph_scale;

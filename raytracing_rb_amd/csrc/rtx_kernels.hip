@@ -340,11 +340,12 @@ __device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o
 }
 
 // ----------------------------------------------------------------- the query, hierarchical
-// The same query answered through the four-wide ball hierarchy (rtx_scene.h)
-// with a wave-coherent traversal: the wave visits a node if any of its lanes
-// may need it, so every decision below is wave-uniform and the per-wave
-// stack lives in LDS.  A lane wants a child ball unless a float32 test with
-// the margins of DESIGN.md §2.1 proves that every sphere below it
+// The same query answered through the four-wide box hierarchy (rtx_scene.h).
+// Every lane traverses on its own (per-lane stack in LDS, nearest child first,
+// "while-while": lanes descend through inner nodes together, then process
+// their leaves together).  A lane skips a child box when a float32 slab test
+// of the box dilated by m*S (the margin of DESIGN.md §2.1) proves that every
+// sphere below it
 //   * misses the ray's line, or lies wholly behind the origin (nil), or
 //   * EXTEND: is farther than the lane's current best hit (loses the strict <
 //     of world.rb:48-50 even on a tie), or
@@ -356,6 +357,13 @@ __device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o
 //     index and subtracts them in that order (world.rb:64-67).  A lane whose
 //     list overflows COVER_K repeats the ordered linear walk.
 // Planes and boxes are few: they are walked first (tightening `best`).
+//
+// Slab-test rounding: each computed slab bound errs by a few float32 ulps of
+// (|box coordinate| + |o| + m*S) / |d_axis| <= 1e-6 * S / |d_axis|, far inside
+// the dilation m*S / |d_axis| (m = 2e-5), so the computed interval contains
+// the exact interval of the undilated box; direction components below
+// 1e-20 |d|_1 are replaced by that value (a deviation of < 1e-15 over any
+// distance the scene spans) so every reciprocal is finite.
 __device__ __forceinline__ bool lex_better(double dist, int obj, double best, int besti) {
   return dist < best || (dist == best && besti >= 0 && obj < besti);
 }
@@ -380,7 +388,7 @@ __device__ __forceinline__ void push_cover(int* ci, double* cv, int& n, bool& ov
 }
 
 template <int BS, typename NP, typename LP>
-__device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32, int* wstack, int* ci, double* cv,
+__device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32, int* stk, int* ci, double* cv,
                                           bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
                                           double& total, uint32_t& err) {
   const double r = vr(d);
@@ -395,10 +403,21 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32
   const float mS = CULL_M * Sx;
   const float kline = dd * ms2;
   const float qneg = -CULL_M * Sx * sqrtf(dd);
-  const float sqd = sqrtf(dd);
-  // A non-finite ray makes no cull (every comparison below would be unordered).
-  const bool fin = __builtin_isfinite(dd) && __builtin_isfinite(Sx);
-  float bestf = (float)(best * (1.0 + 1e-6));      // >= best: culls keep a margin over it
+  // slab set-up: reciprocal direction and the dilated origin terms
+  const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
+  const float tiny = 1e-20f * l1;
+  const float ex = fabsf(dx) < tiny ? copysignf(tiny, dx) : dx;
+  const float ey = fabsf(dy) < tiny ? copysignf(tiny, dy) : dy;
+  const float ez = fabsf(dz) < tiny ? copysignf(tiny, dz) : dz;
+  const float ix = 1.0f / ex, iy = 1.0f / ey, iz = 1.0f / ez;
+  const float ax = (ox + mS) * ix, ay = (oy + mS) * iy, az = (oz + mS) * iz;   // lo - mS side
+  const float bx = (ox - mS) * ix, by = (oy - mS) * iy, bz = (oz - mS) * iz;   // hi + mS side
+  // A non-finite or zero ray makes no cull (comparisons would be unordered).
+  const bool fin = __builtin_isfinite(dd) && __builtin_isfinite(Sx) && l1 > 0.0f && __builtin_isfinite(ix) &&
+                   __builtin_isfinite(iy) && __builtin_isfinite(iz);
+  const float rf = (float)r;
+  // far bound on the ray parameter: EXTEND the current best hit, SHADOW the light
+  float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + mS / rf;
   int ncov = 0;
   bool ovf = false;
 
@@ -424,7 +443,7 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32
         if (lex_better(dist, obj0 + k, best, besti)) {
           best = dist;
           besti = obj0 + k;
-          bestf = (float)(best * (1.0 + 1e-6));
+          thi = (float)(best / r * (1.0 + 1e-6));
         }
       } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {
         push_cover<BS>(ci, cv, ncov, ovf, obj0 + k, 1.0);
@@ -432,63 +451,50 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32
     }
   }
 
-  const bool leader = __lane_id() == (unsigned)__builtin_ctzll(__ballot(1));
-  const RTX_CONST Sphere64* s64 = cptr(S.bvh_sph64);
-  const RTX_CONST int32_t* sobj = cptr(S.bvh_obj);
-  int ref = uni(S.bvh_root);
+  int ref = S.bvh_root;
   int sp = 0;
   while (ref != BVH_NONE) {
-    if (ref >= 0) {
-      // ---- internal node: test the four child balls for every lane
-      int ch[4];
+    // ---- inner nodes: slab-test the four child boxes, descend into the nearest
+    while (ref >= 0 && ref != BVH_NONE) {
       float key[4];
-      uint64_t want[4];
+      int ch[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        ch[k] = uni(nodes[ref].child[k]);
-        const float cx = nodes[ref].ball[k][0], cy = nodes[ref].ball[k][1], cz = nodes[ref].ball[k][2];
-        const float br = nodes[ref].ball[k][3];
-        const float ocx = cx - ox, ocy = cy - oy, ocz = cz - oz;
-        const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
-        const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
-        const float rr = br + mS;
-        const bool line = __builtin_fmaf(s, dd, -q * q) <= __builtin_fmaf(dd, br * br, kline);
-        const bool front = q >= -rr * sqd;
-        const float fb = bestf + rr;
-        const bool reach = ext ? s <= fb * fb : q <= __builtin_fmaf(rr, sqd, dd);
-        const bool w = !fin || (line && front && reach);
-        want[k] = ch[k] != BVH_NONE ? __ballot(w) : 0ull;
-        key[k] = want[k] ? __builtin_bit_cast(float, uni(__builtin_bit_cast(int, q))) : __builtin_inff();
-        if (!(key[k] == key[k])) key[k] = 0.0f;
-        if (!want[k]) ch[k] = BVH_NONE;
+        ch[k] = nodes[ref].child[k];
+        const float t0x = __builtin_fmaf(nodes[ref].lo[0][k], ix, -ax);
+        const float t1x = __builtin_fmaf(nodes[ref].hi[0][k], ix, -bx);
+        const float t0y = __builtin_fmaf(nodes[ref].lo[1][k], iy, -ay);
+        const float t1y = __builtin_fmaf(nodes[ref].hi[1][k], iy, -by);
+        const float t0z = __builtin_fmaf(nodes[ref].lo[2][k], iz, -az);
+        const float t1z = __builtin_fmaf(nodes[ref].hi[2][k], iz, -bz);
+        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+        const bool w = ch[k] != BVH_NONE && (!fin || (tn <= tf && tf >= 0.0f && tn <= thi));
+        key[k] = w ? (fin ? tn : 0.0f) : __builtin_inff();
       }
-      // near-first for the wave's first lane (an ordering heuristic only)
-#define RTX_CS(a, b)                   \
-  if (key[b] < key[a]) {               \
-    const float tk = key[a];           \
-    key[a] = key[b];                   \
-    key[b] = tk;                       \
-    const int tc = ch[a];              \
-    ch[a] = ch[b];                     \
-    ch[b] = tc;                        \
+#define RTX_CS(a, b)         \
+  if (key[b] < key[a]) {     \
+    const float tk = key[a]; \
+    key[a] = key[b];         \
+    key[b] = tk;             \
+    const int tc = ch[a];    \
+    ch[a] = ch[b];           \
+    ch[b] = tc;              \
   }
       RTX_CS(0, 1) RTX_CS(2, 3) RTX_CS(0, 2) RTX_CS(1, 3) RTX_CS(1, 2)
 #undef RTX_CS
 #pragma unroll
-      for (int k = 3; k >= 1; k--) {
-        if (ch[k] == BVH_NONE) continue;
-        if (leader) wstack[sp] = ch[k];
-        sp++;
-      }
-      if (ch[0] != BVH_NONE) {
-        ref = ch[0];
-        continue;
-      }
-    } else {
-      // ---- leaf: pre-test its spheres, exact test for those not ruled out
+      for (int k = 3; k >= 1; k--)
+        if (key[k] < __builtin_inff()) stk[(sp++) * BS] = ch[k];
+      if (key[0] < __builtin_inff()) ref = ch[0];
+      else ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
+    }
+    if (ref == BVH_NONE) break;
+    // ---- leaf: pre-test its spheres, exact test for those not ruled out
+    {
       const int v = ~ref;
-      const int slot0 = (v >> 3) * BVH_LEAF;
-      const int cnt = v & 7;
+      const int slot0 = (v >> 2) * BVH_LEAF;
+      const int cnt = (v & 3) + 1;
       float4 c[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
@@ -509,34 +515,29 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32
         keep |= (miss_line || behind) ? 0u : (1u << u);
       }
       keep &= (1u << cnt) - 1u;
-      if (keep) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          if (!(keep >> u & 1)) continue;
-          const RTX_CONST Sphere64& sp64 = s64[slot0 + u];
-          const V3 C = v3(sp64.c[0], sp64.c[1], sp64.c[2]);
-          const double sr = sp64.r;
-          V3 hit;
-          bool in;
-          if (!sphere_exact(C, sr, o, d, dn, r2, hit, in)) continue;
-          const int obj = sobj[slot0 + u];
-          if (ext) {
-            const double dist = vr(vsub(o, hit));    // Ray#distance
-            if (lex_better(dist, obj, best, besti)) {
-              best = dist;
-              besti = obj;
-              bestf = (float)(best * (1.0 + 1e-6));
-            }
-          } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
-            const double cov = penumbra(C, sr, o, d, radius, err);
-            if (cov != 0.0) push_cover<BS>(ci, cv, ncov, ovf, obj, cov);
+      while (keep) {
+        const int u = __builtin_ctz(keep);
+        keep &= keep - 1;
+        const Sphere64 sp64 = S.bvh_sph64[slot0 + u];
+        const V3 C = v3(sp64.c[0], sp64.c[1], sp64.c[2]);
+        V3 hit;
+        bool in;
+        if (!sphere_exact(C, sp64.r, o, d, dn, r2, hit, in)) continue;
+        const int obj = S.bvh_obj[slot0 + u];
+        if (ext) {
+          const double dist = vr(vsub(o, hit));      // Ray#distance
+          if (lex_better(dist, obj, best, besti)) {
+            best = dist;
+            besti = obj;
+            thi = (float)(best / r * (1.0 + 1e-6));
           }
+        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
+          const double cov = penumbra(C, sp64.r, o, d, radius, err);
+          if (cov != 0.0) push_cover<BS>(ci, cv, ncov, ovf, obj, cov);
         }
       }
     }
-    if (sp == 0) break;
-    sp--;
-    ref = uni(wstack[sp]);
+    ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
   }
   if (!ext) {
     total = 1.0;
@@ -838,7 +839,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p, const double* __r
   }
   const float* sph_lds = reinterpret_cast<const float*>(lds_sph);
   const RTX_CONST float* sph_k = cptr(S.sph32);
-  int* wstack = reinterpret_cast<int*>(lds + p.lds_stack) + (threadIdx.x >> 6) * BVH_STACK;
+  int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
   int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
   double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
 
@@ -972,10 +973,10 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p, const double* __r
       query<COUNT>(S, sph_k, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err, cnt);
     else if (SPH == SPH_BVH_LDS)
       query_bvh<BS>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float*>(lds + p.lds_leaf),
-                    wstack, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err);
+                    stk, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, total, err);
     else
-      query_bvh<BS>(S, cptr(S.bvh), cptr(S.bvh_sph32), wstack, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad,
-                    best, besti, total, err);
+      query_bvh<BS>(S, S.bvh, S.bvh_sph32, stk, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti,
+                    total, err);
     if (RTX_STAMPS) {
       t1 = stamp();
       tB += t1 - t0;
@@ -1105,14 +1106,14 @@ constexpr size_t LDS_SPHERE_BYTES = 32 * 1024;
 constexpr size_t LDS_TOTAL_BYTES = 160 * 1024;
 constexpr int BS_LIN = 256, BS_BVH = 512;
 
-static size_t bvh_lds_fixed(int bs) {
-  return (size_t)(bs / 64) * BVH_STACK * 4 + (size_t)COVER_K * bs * 12;
+static size_t bvh_lds_fixed(const SceneDev& S, int bs) {
+  return (size_t)S.bvh_stack * bs * 4 + (size_t)COVER_K * bs * 12 + 64;
 }
 
 int resolve_mode(const SceneDev& S, int mode) {
   if (mode == SPH_LIN_LDS && (size_t)(S.n_sphere + 4) * 16 > LDS_SPHERE_BYTES) return SPH_LIN_SCALAR;
   if (mode == SPH_BVH_LDS &&
-      (size_t)S.n_nodes * sizeof(Bvh4Node) + (size_t)S.n_slots * 16 + bvh_lds_fixed(BS_BVH) > LDS_TOTAL_BYTES)
+      (size_t)S.n_nodes * sizeof(Bvh4Node) + (size_t)S.n_slots * 16 + bvh_lds_fixed(S, BS_BVH) > LDS_TOTAL_BYTES)
     return SPH_BVH_GLOBAL;
   return mode;
 }
@@ -1131,7 +1132,7 @@ static size_t lds_layout(KParams& p, int mode, int bs) {
   p.lds_stack = (int32_t)off;
   p.lds_cov = (int32_t)off;
   if (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL) {
-    off += (size_t)(bs / 64) * BVH_STACK * 4;
+    off += (size_t)S.bvh_stack * bs * 4;
     off = (off + 15) & ~(size_t)15;
     p.lds_cov = (int32_t)off;
     off += (size_t)COVER_K * bs * 12;

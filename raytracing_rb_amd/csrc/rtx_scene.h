@@ -38,30 +38,31 @@ struct Sphere64 {
   double r;
 };
 
-// Four-wide bounding-ball hierarchy over the spheres (built on the host,
-// rtx_capi.cpp).  A node holds the balls of its (up to) four children; every
-// child ball contains every sphere below it exactly (float32 center, radius
-// rounded outwards), so a float32 rejection of a child ball with the margins
-// of DESIGN.md §2.1 proves the exact binary64 test of every sphere below it
-// returns nil (or, for a shadow query, a zero cover).
+// Four-wide bounding-box hierarchy over the spheres (built on the host,
+// rtx_capi.cpp).  A node holds the float32 axis-aligned boxes of its (up to)
+// four children; every child box contains every sphere below it exactly
+// (bounds rounded outwards), so a float32 slab test of the box dilated by the
+// margin of DESIGN.md §2.1 that misses proves the exact binary64 test of every
+// sphere below it returns nil (or, for a shadow query, a zero cover).
 //   child[k] >= 0        : internal node index
 //   child[k] == BVH_NONE : empty slot
-//   child[k] <  0        : leaf, ~child = leaf << 3 | count; its `count` (1..4)
-//                          spheres sit in slots 4*leaf .. 4*leaf+count-1 of the
-//                          slot arrays (float32 pre-test record, binary64 record,
-//                          global object index); unused slots are padding.
-// Nodes are in pre-order (root = 0).  The traversal order never matters for
-// the result: nearest hits compare (distance, object index) lexicographically
-// and shadow covers are subtracted in object order (rtx_kernels.hip).
+//   child[k] <  0        : leaf, ~child = leaf << 2 | (count - 1); its `count`
+//                          (1..4) spheres sit in slots 4*leaf .. 4*leaf+count-1
+//                          of the slot arrays (float32 pre-test record, binary64
+//                          record, global object index); unused slots are padding.
+// Nodes are in pre-order (root = 0).  Each lane traverses on its own, nearest
+// child first; the traversal order never matters for the result: nearest hits
+// compare (distance, object index) lexicographically and shadow covers are
+// subtracted in object order (rtx_kernels.hip).
 constexpr int BVH_LEAF = 4;
 constexpr int32_t BVH_NONE = 0x7fffffff;
-constexpr int BVH_STACK = 64;     // per-wave traversal stack entries (LDS)
 constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); more -> ordered re-walk
 struct Bvh4Node {
-  float ball[4][4];       // per child: cx, cy, cz, radius (rounded up)
+  float lo[3][4];         // lo[axis][child]
+  float hi[3][4];
   int32_t child[4];
 };
-static_assert(sizeof(Bvh4Node) == 80, "Bvh4Node layout");
+static_assert(sizeof(Bvh4Node) == 112, "Bvh4Node layout");
 
 struct Material {
   double diffuse[3];
@@ -112,6 +113,7 @@ struct SceneDev {
   int32_t n_obj, n_light, n_sphere, n_plane, n_box, n_runs;
   int32_t n_nodes, n_slots;
   int32_t bvh_root;       // root reference (BVH_NONE: no spheres)
+  int32_t bvh_stack;      // per-lane traversal stack entries the hierarchy can need
   double max_distance;
   double sse;             // soft_shadow_exponent
   float sph_scale;        // max over spheres of |C|_1 + R (pre-test margin scale)
