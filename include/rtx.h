@@ -214,8 +214,8 @@ rtx_status rtx_count_work(rtx_context* ctx, uint64_t seed, uint64_t counts[RTX_N
 
 /* Kernel-variant control for experiments; 0 = default. */
 rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
-/* keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres [default 256],
-         2 always; every choice renders the same bits), "bvh_min", "sphere_src" (0 LDS
+/* keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
+         2 always; every choice renders the same bits), "bvh_min" [32], "sphere_src" (0 LDS
          staging, 1 scalar loads), "force_stack" (per-lane ray-stack bucket). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */

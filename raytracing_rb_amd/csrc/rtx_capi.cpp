@@ -26,6 +26,8 @@
 
 using namespace rtx;
 
+constexpr unsigned RTX_WORK_RING = 256;
+
 struct rtx_context {
   int device = 0;
   std::string err;
@@ -43,9 +45,11 @@ struct rtx_context {
   unsigned long long* d_counts = nullptr;
   double* d_scratch = nullptr;
   size_t scratch_bytes = 0;
+  int* d_work = nullptr;             // ring of per-launch work counters (launches on different streams)
+  unsigned work_seq = 0;
   int64_t opt_force_stack = 0;
   int64_t opt_bvh = 1;               // 0: ordered linear walk; 1: hierarchy from opt_bvh_min spheres; 2: always
-  int64_t opt_bvh_min = 256;
+  int64_t opt_bvh_min = 32;          // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
   int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
 };
 
@@ -219,6 +223,7 @@ rtx_status rtx_context_create(int32_t device, rtx_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(unsigned long long) * RTX_NCOUNT);
   if (e == hipSuccess) e = hipMalloc(&c->d_scene, sizeof(SceneDev));
   if (e == hipSuccess) e = hipMalloc(&c->d_cam, sizeof(CameraDev));
+  if (e == hipSuccess) e = hipMalloc(&c->d_work, sizeof(int) * RTX_WORK_RING);
   if (e == hipSuccess) e = hipMemset(c->d_err, 0, sizeof(unsigned int) * 2);
   if (e == hipSuccess) e = hipMemset(((char*)c->d_err) + 8, 0xFF, sizeof(unsigned long long) * 4);
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -240,6 +245,7 @@ void rtx_context_destroy(rtx_context* c) {
   hipFree(c->d_scene);
   hipFree(c->d_cam);
   hipFree(c->d_scratch);
+  hipFree(c->d_work);
   delete c;
 }
 
@@ -526,6 +532,7 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
   p.seed = seed;
   p.err = c->d_err;
   p.counts = c->d_counts;
+  p.work = c->d_work + (c->work_seq++ % RTX_WORK_RING);
   return RTX_OK;
 }
 
@@ -654,7 +661,10 @@ rtx_status rtx_trace(rtx_context* c, int32_t n, const double* rays, const int32_
   HIPCHK(c, hipMemcpy(d_rays, rays, rb, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(d_keys, keys, kb, hipMemcpyHostToDevice));
   p.out = d_out;
-  HIPCHK(c, launch_trace(p, sph_mode(c), d_rays, d_keys, n, maxs, nullptr));
+  p.rays = d_rays;
+  p.keys = d_keys;
+  p.nrays = n;
+  HIPCHK(c, launch_trace(p, sph_mode(c), maxs, nullptr));
   HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
   return rtx_sync(c, nullptr);
 }

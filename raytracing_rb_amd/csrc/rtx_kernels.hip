@@ -30,6 +30,8 @@
 // so it changes no bit of any result.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rtx_launch.h"
 #include "rtx_scene.h"
 #include "rtx_vec3.h"
@@ -55,7 +57,7 @@ struct Item {                       // one queue entry of RayTracer (ray_tracer.
 enum { C_RAYS = 0, C_SPHERE_TESTS, C_SPHERE_HITS, C_PLANE_TESTS, C_BOX_TESTS, C_SHADE_HITS,
        C_COVER_SPHERE, C_COVER_PLANE, C_COVER_BOX, C_HIGHLIGHT_TESTS, C_PRIMARY, C_N };
 
-enum { M_NEED = 0, M_EXTEND = 1, M_SHADOW = 2, M_DONE = 3 };
+enum { M_NEED = 0, M_EXTEND = 1, M_SHADOW = 2, M_DONE = 3, M_FETCH = 4 };
 
 // Out-of-line the rarely-executed shading blocks (1) or inline everything (0).
 #ifndef RTX_OUTLINE_SHADING
@@ -816,8 +818,10 @@ __device__ __forceinline__ int row_to_y(const KParams& p, int row) {
 // RayTracer#trace_sync (rtx_trace).  SPH: where the sphere walk reads its
 // records (SphMode, rtx_launch.h).  BS: threads per workgroup.
 template <bool COUNT, int MAXS, int MAXPRE, int WPS, int SPH, int SRC, int BS>
-__global__ __launch_bounds__(BS, WPS) void k_render(KParams p, const double* __restrict__ rays,
-                                                    const int32_t* __restrict__ keys, int nrays) {
+__global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
+  const double* __restrict__ rays = p.rays;
+  const int32_t* __restrict__ keys = p.keys;
+  const int nrays = p.nrays;
   static_assert(!COUNT || SPH == SPH_LIN_LDS || SPH == SPH_LIN_SCALAR, "counting launches walk linearly");
   const SceneDev& S = p.scene;                // kernel argument: scalar loads
   const CameraDev& cam = *p.cam;
@@ -843,42 +847,33 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p, const double* __r
   int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
   double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
 
-  int x, y, row, px_ = 0;
-  if (SRC == SRC_PIXELS) {
-    const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
-    const int tiles_x = (p.nx + 7) >> 3;
-    px_ = (tile % tiles_x) * 8 + (lane & 7);
-    row = (tile / tiles_x) * 8 + (lane >> 3);
-    if (px_ >= p.nx || row >= p.nrows) return;
-    y = row_to_y(p, row);
-    if (y >= cam.height) return;
-    x = p.x0 + px_;
-  } else {
-    row = blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= nrays) return;
-    x = keys[3 * row];
-    y = keys[3 * row + 1];
-  }
+  // Persistent lanes: every lane takes work items (SRC_PIXELS: pixels in
+  // 8x8-tile order; SRC_RAYS: rays) from one counter per launch and takes the
+  // next one as soon as its current item is finished, so no lane idles until
+  // the pool is empty.  A wave's lanes that need work are served by one atomic
+  // (ballot + prefix count); a fresh wave's first fetch is one whole tile.
+  const int tiles_x = (p.nx + 7) >> 3;
+  const int nwork = SRC == SRC_PIXELS ? tiles_x * ((p.nrows + 7) >> 3) * 64 : nrays;
+  int x = 0, y = 0, row = 0, px_ = 0;
+  V3 tgt = v3(0.0, 0.0, 0.0);
 
   unsigned long long cnt[C_N];
   if (COUNT)
     for (int k = 0; k < C_N; k++) cnt[k] = 0;
-  const V3 tgt = SRC == SRC_PIXELS ? lens_target(cam, x, y) : v3(0.0, 0.0, 0.0);
 
   Stack<MAXS> st;
   st.n = 0;
   V3 smp[MAXPRE];
   uint32_t err = 0;
   const int pre = cam.pre;
-  int ntot = SRC == SRC_PIXELS ? pre : 1;
+  int ntot = 1;
   bool extra = false;
   V3 avg = v3(0.0, 0.0, 0.0), cv = avg, sum = avg;
   int j = -1;                        // current camera sample
   int sample = 0;                    // RNG key of the current tree
   Item cur;
   bool have = false;                 // `cur` holds a ray not yet processed
-  int mode = M_NEED;
+  int mode = M_FETCH;
   // shading state of the ray being shaded
   int besti = -1, li = 0, nl = 0;
   bool hin = true;
@@ -891,72 +886,124 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p, const double* __r
   while (true) {
     if (RTX_STAMPS) t0 = stamp();
     // ---- A: find this lane's next query (divergent, short)
-    while (mode == M_NEED) {
-      if (have) {
-        have = false;
-      } else if (st.n > 0) {
-        cur = st.a[--st.n];
-      } else {
-        // the current tree (camera sample) is complete
-        if (j >= 0) {
-          if (SRC == SRC_RAYS) {
-            mode = M_DONE;
+    while (true) {
+      while (mode == M_NEED) {
+        if (have) {
+          have = false;
+        } else if (st.n > 0) {
+          cur = st.a[--st.n];
+        } else {
+          // the current tree (camera sample) is complete
+          if (j >= 0) {
+            if (SRC == SRC_RAYS) {
+              p.out[3 * row] = sum.x;
+              p.out[3 * row + 1] = sum.y;
+              p.out[3 * row + 2] = sum.z;
+              if (err) record_error(p.err, err, row, 0, 0x7fffffff);
+              mode = M_FETCH;
+              break;
+            }
+            if (j < pre) {
+              smp[j] = sum;
+              avg = vadd(avg, sum);
+            } else {
+              cv = vadd(cv, sum);
+            }
+            if (j + 1 == pre) {                 // camera.rb:80-85: mean and variance
+              avg = vdiv(avg, (double)pre);
+              double variance = 0.0;
+              for (int k = 0; k < pre; k++) {
+                const V3 dd = vsub(smp[k], avg);
+                double mx = dd.x;
+                if (dd.y > mx) mx = dd.y;
+                if (dd.z > mx) mx = dd.z;
+                variance += mx * mx;              // .max ** 2
+              }
+              variance /= (double)pre;
+              if (variance >= cam.variant_threshold) {
+                extra = true;
+                ntot = cam.max_samples;
+              }
+            }
+          }
+          j++;
+          if (j >= ntot) {                      // pixel done: Camera#render_at's result
+            if (extra) avg = vdiv(vadd(vsc(avg, (double)pre), cv), (double)cam.max_samples);
+            double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
+            o[0] = avg.x;
+            o[1] = avg.y;
+            o[2] = avg.z;
+            if (err) record_error(p.err, err, x, y, cam.width);
+            mode = M_FETCH;
             break;
           }
-          if (j < pre) {
-            smp[j] = sum;
-            avg = vadd(avg, sum);
+          sum = v3(0.0, 0.0, 0.0);
+          if (SRC == SRC_PIXELS) {
+            cur.ray = lens_ray(cam, tgt, x, y, j, p.seed);
+            sample = j;
+            if (COUNT) cnt[C_PRIMARY]++;
           } else {
-            cv = vadd(cv, sum);
+            cur.ray.d = v3p(rays + 6 * row);
+            cur.ray.o = v3p(rays + 6 * row + 3);
+            sample = keys[3 * row + 2];
           }
-          if (j + 1 == pre) {                 // camera.rb:80-85: mean and variance
-            avg = vdiv(avg, (double)pre);
-            double variance = 0.0;
-            for (int k = 0; k < pre; k++) {
-              const V3 dd = vsub(smp[k], avg);
-              double mx = dd.x;
-              if (dd.y > mx) mx = dd.y;
-              if (dd.z > mx) mx = dd.z;
-              variance += mx * mx;              // .max ** 2
-            }
-            variance /= (double)pre;
-            if (variance >= cam.variant_threshold) {
-              extra = true;
-              ntot = cam.max_samples;
-            }
-          }
+          cur.att = v3(1.0, 1.0, 1.0);
+          cur.path = 1;
+          cur.depth = cam.depth;
         }
-        j++;
-        if (j >= ntot) {
+        // rt_map prologue (ray_tracer.rb:52-75)
+        if (cur.depth <= 0 || vr(cur.att) < 0.0001) continue;
+        if (COUNT) {
+          cnt[C_RAYS]++;
+          cnt[C_HIGHLIGHT_TESTS] += S.n_light;
+        }
+        if (highlights(S, cur, sum, err)) continue;
+        mode = M_EXTEND;
+        qo = cur.ray.o;
+        qd = cur.ray.d;
+        best = S.max_distance;
+        besti = -1;
+      }
+      // ---- refill: lanes whose item is finished take the next ones
+      const uint64_t f = __ballot(mode == M_FETCH);
+      if (!f) break;
+      const int src = __builtin_ctzll(f);
+      int base = 0;
+      if ((int)__lane_id() == src) base = atomicAdd(p.work, __popcll(f));
+      base = __builtin_amdgcn_readlane(base, src);
+      if (mode == M_FETCH) {
+        const int k = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(f >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)f, 0u));
+        if (k >= nwork) {
           mode = M_DONE;
-          break;
-        }
-        sum = v3(0.0, 0.0, 0.0);
-        if (SRC == SRC_PIXELS) {
-          cur.ray = lens_ray(cam, tgt, x, y, j, p.seed);
-          sample = j;
-          if (COUNT) cnt[C_PRIMARY]++;
+        } else if (SRC == SRC_PIXELS) {
+          const int tile = k >> 6, l = k & 63;
+          px_ = (tile % tiles_x) * 8 + (l & 7);
+          row = (tile / tiles_x) * 8 + (l >> 3);
+          if (px_ < p.nx && row < p.nrows) {
+            y = row_to_y(p, row);
+            if (y < cam.height) {
+              x = p.x0 + px_;
+              tgt = lens_target(cam, x, y);
+              ntot = pre;
+              extra = false;
+              avg = v3(0.0, 0.0, 0.0);
+              cv = avg;
+              j = -1;
+              err = 0;
+              mode = M_NEED;
+            }
+          }
         } else {
-          cur.ray.d = v3p(rays + 6 * row);
-          cur.ray.o = v3p(rays + 6 * row + 3);
-          sample = keys[3 * row + 2];
+          row = k;
+          x = keys[3 * row];
+          y = keys[3 * row + 1];
+          ntot = 1;
+          j = -1;
+          err = 0;
+          mode = M_NEED;
         }
-        cur.att = v3(1.0, 1.0, 1.0);
-        cur.path = 1;
-        cur.depth = cam.depth;
       }
-      // rt_map prologue (ray_tracer.rb:52-75)
-      if (cur.depth <= 0 || vr(cur.att) < 0.0001) continue;
-      if (COUNT) {
-        cnt[C_RAYS]++;
-        cnt[C_HIGHLIGHT_TESTS] += S.n_light;
-      }
-      if (highlights(S, cur, sum, err)) continue;
-      mode = M_EXTEND;
-      qo = cur.ray.o;
-      qd = cur.ray.d;
-      best = S.max_distance;
-      besti = -1;
     }
     if (RTX_STAMPS) {
       t1 = stamp();
@@ -1045,19 +1092,6 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p, const double* __r
     atomicAdd(&rtx_stamps[5], 1ull);
   }
 
-  if (SRC == SRC_PIXELS) {
-    if (extra) avg = vdiv(vadd(vsc(avg, (double)pre), cv), (double)cam.max_samples);
-    double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
-    o[0] = avg.x;
-    o[1] = avg.y;
-    o[2] = avg.z;
-    if (err) record_error(p.err, err, x, y, cam.width);
-  } else {
-    p.out[3 * row] = sum.x;
-    p.out[3 * row + 1] = sum.y;
-    p.out[3 * row + 2] = sum.z;
-    if (err) record_error(p.err, err, row, 0, 0x7fffffff);
-  }
   if (COUNT)
     for (int k = 0; k < C_N; k++) atomicAdd(&p.counts[k], cnt[k]);
 }
@@ -1140,36 +1174,42 @@ static size_t lds_layout(KParams& p, int mode, int bs) {
   return off;
 }
 
+// Persistent launch: as many workgroups as can be resident at once (the
+// occupancy API; an over-estimate only leaves blocks that start after the
+// pool is empty and exit at once), never more than the work needs.
 template <bool COUNT, int MAXS, int SPH, int SRC>
-static hipError_t launch_one(KParams p, dim3 grid_px, const double* rays, const int32_t* keys, int n,
-                             hipStream_t s) {
+static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
   const size_t lds = lds_layout(p, SPH, BS);
-  dim3 grid;
-  if (SRC == SRC_PIXELS) {
-    const int tiles = (int)grid_px.x;
-    grid = dim3((tiles + BS / 64 - 1) / (BS / 64));
-  } else {
-    grid = dim3((n + BS - 1) / BS);
-  }
+  auto kern = k_render<COUNT, MAXS, 16, 2, SPH, SRC, BS>;
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_render<COUNT, MAXS, 16, 2, SPH, SRC, BS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((k_render<COUNT, MAXS, 16, 2, SPH, SRC, BS>), grid, dim3(BS), lds, s, p, rays, keys, n);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  int dev = 0, cus = 0, per_cu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BS, lds);
+  if (e != hipSuccess) return e;
+  if (per_cu < 1) per_cu = 1;
+  const long need = ((long)nwork + BS - 1) / BS;
+  const long blocks = std::min<long>(need, (long)cus * per_cu);
+  if (blocks <= 0) return hipSuccess;
+  e = hipMemsetAsync(p.work, 0, sizeof(int), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BS), lds, s, p);
   return hipGetLastError();
 }
 
 template <bool COUNT, int MAXS, int SRC>
-static hipError_t launch_mode(const KParams& p, int mode, dim3 g, const double* rays, const int32_t* keys, int n,
-                              hipStream_t s) {
-  switch (COUNT ? (mode == SPH_LIN_LDS ? SPH_LIN_LDS : SPH_LIN_SCALAR) : mode) {
-    case SPH_LIN_LDS: return launch_one<COUNT, MAXS, SPH_LIN_LDS, SRC>(p, g, rays, keys, n, s);
-    case SPH_LIN_SCALAR: return launch_one<COUNT, MAXS, SPH_LIN_SCALAR, SRC>(p, g, rays, keys, n, s);
+static hipError_t launch_mode(const KParams& p, int mode, int nwork, hipStream_t s) {
+  switch (mode) {
+    case SPH_LIN_LDS: return launch_one<COUNT, MAXS, SPH_LIN_LDS, SRC>(p, nwork, s);
+    case SPH_LIN_SCALAR: return launch_one<COUNT, MAXS, SPH_LIN_SCALAR, SRC>(p, nwork, s);
     case SPH_BVH_LDS:
-      if (!COUNT) return launch_one<false, MAXS, SPH_BVH_LDS, SRC>(p, g, rays, keys, n, s);
+      if (!COUNT) return launch_one<false, MAXS, SPH_BVH_LDS, SRC>(p, nwork, s);
       break;
     case SPH_BVH_GLOBAL:
-      if (!COUNT) return launch_one<false, MAXS, SPH_BVH_GLOBAL, SRC>(p, g, rays, keys, n, s);
+      if (!COUNT) return launch_one<false, MAXS, SPH_BVH_GLOBAL, SRC>(p, nwork, s);
       break;
   }
   return hipErrorInvalidValue;
@@ -1180,26 +1220,23 @@ hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t 
   if (tiles == 0) return hipSuccess;
   if (count) mode = (mode == SPH_LIN_LDS || mode == SPH_BVH_LDS) ? SPH_LIN_LDS : SPH_LIN_SCALAR;
   mode = resolve_mode(p.scene, mode);
-  const dim3 g(tiles);
-#define RTX_L(M)                                                                      \
-  if (maxs == M)                                                                      \
-    return count ? launch_mode<true, M, SRC_PIXELS>(p, mode, g, nullptr, nullptr, 0, s) \
-                 : launch_mode<false, M, SRC_PIXELS>(p, mode, g, nullptr, nullptr, 0, s);
+  const int nwork = tiles * 64;
+#define RTX_L(M)                                                                                      \
+  if (maxs == M)                                                                                      \
+    return count ? launch_mode<true, M, SRC_PIXELS>(p, mode, nwork, s) : launch_mode<false, M, SRC_PIXELS>(p, mode, nwork, s);
   RTX_L(8) RTX_L(16) RTX_L(32) RTX_L(64)
 #undef RTX_L
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_trace(KParams p, int mode, const double* rays, const int32_t* keys, int n, int maxs,
-                        hipStream_t s) {
-  if (n == 0) return hipSuccess;
+hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s) {
+  if (p.nrays == 0) return hipSuccess;
   mode = resolve_mode(p.scene, mode);
-  const dim3 g(0);
   switch (maxs) {
-    case 8: return launch_mode<false, 8, SRC_RAYS>(p, mode, g, rays, keys, n, s);
-    case 16: return launch_mode<false, 16, SRC_RAYS>(p, mode, g, rays, keys, n, s);
-    case 32: return launch_mode<false, 32, SRC_RAYS>(p, mode, g, rays, keys, n, s);
-    case 64: return launch_mode<false, 64, SRC_RAYS>(p, mode, g, rays, keys, n, s);
+    case 8: return launch_mode<false, 8, SRC_RAYS>(p, mode, p.nrays, s);
+    case 16: return launch_mode<false, 16, SRC_RAYS>(p, mode, p.nrays, s);
+    case 32: return launch_mode<false, 32, SRC_RAYS>(p, mode, p.nrays, s);
+    case 64: return launch_mode<false, 64, SRC_RAYS>(p, mode, p.nrays, s);
   }
   return hipErrorInvalidValue;
 }

@@ -26,6 +26,10 @@ struct KParams {
   size_t stride;                   // doubles per output row
   ErrState* err;
   unsigned long long* counts;      // RTX_NCOUNT counters (counting launches only)
+  int* work;                       // work-item counter of this launch (zeroed by the launcher)
+  const double* rays;              // SRC_RAYS (rtx_trace): 6 doubles per ray, keys (x, y, sample)
+  const int32_t* keys;
+  int32_t nrays;
   // dynamic LDS layout (bytes), filled by launch_render/launch_trace
   int32_t lds_leaf, lds_stack, lds_cov;
 };
@@ -43,8 +47,7 @@ int stack_bucket(int need);
 // SPH_LIN_SCALAR, a BVH mode to SPH_BVH_GLOBAL.  Counting launches always walk
 // linearly (the counters are the reference's brute-force events).
 hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s);
-hipError_t launch_trace(KParams p, int mode, const double* rays, const int32_t* keys, int n, int maxs,
-                        hipStream_t s);
+hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s);
 int resolve_mode(const SceneDev& S, int mode);
 hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,
                            hipStream_t s);
