@@ -51,6 +51,7 @@ struct rtx_context {
   int64_t opt_bvh = 1;               // 0: ordered linear walk; 1: hierarchy from opt_bvh_min spheres; 2: always
   int64_t opt_bvh_min = 32;          // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
   int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
+  int64_t opt_lds_stack = -1;        // ray-stack entries per lane in LDS (-1: as many as fit)
 };
 
 static rtx_status fail(rtx_context* c, rtx_status s, const char* fmt, ...) {
@@ -263,6 +264,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "bvh_min")) {           // sphere count from which bvh=1 uses the hierarchy
     if (value < 0) return fail(c, RTX_EINVAL, "bvh_min must be >= 0");
     c->opt_bvh_min = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lds_stack")) {         // ray-stack entries per lane kept in LDS (-1: as many as fit)
+    if (value < -1 || value > 64) return fail(c, RTX_EINVAL, "lds_stack must be in [-1, 64]");
+    c->opt_lds_stack = value;
     return RTX_OK;
   }
   if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads
@@ -533,6 +539,7 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
   p.err = c->d_err;
   p.counts = c->d_counts;
   p.work = c->d_work + (c->work_seq++ % RTX_WORK_RING);
+  p.stk_slots_max = c->opt_lds_stack < 0 ? 64 : (int32_t)c->opt_lds_stack;
   return RTX_OK;
 }
 

@@ -31,7 +31,9 @@ struct KParams {
   const int32_t* keys;
   int32_t nrays;
   // dynamic LDS layout (bytes), filled by launch_render/launch_trace
-  int32_t lds_leaf, lds_stack, lds_cov;
+  int32_t lds_leaf, lds_stack, lds_cov, lds_items;
+  int32_t stk_slots;               // ray-stack entries per lane kept in LDS (set by the launcher)
+  int32_t stk_slots_max;           // cap (option "lds_stack"; the stack bucket by default)
 };
 
 // Where the sphere walk reads its records:

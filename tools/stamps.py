@@ -7,8 +7,12 @@ import torch
 from raytracing_rb_amd import config, _abi
 from raytracing_rb_amd.runtime import Renderer
 scene = sys.argv[1] if len(sys.argv) > 1 else "c2"
-sd, cd = config.load_scene(os.path.join(ROOT, "scenes", scene + "_world.yml"), os.path.join(ROOT, "scenes", scene + "_camera.yml"))
+ov = dict(width=960, height=540) if scene == "c4" else {}
+sd, cd = config.load_scene(os.path.join(ROOT, "scenes", scene + "_world.yml"), os.path.join(ROOT, "scenes", scene + "_camera.yml"), camera_overrides=ov)
 r = Renderer(sd, cd)
+for kv in sys.argv[2:]:
+    k, v = kv.split("=")
+    r.set_option(k, int(v))
 lib = _abi.load_library()
 out = torch.empty((cd.height, cd.width, 3), dtype=torch.float64, device="cuda")
 r.render_device(out.data_ptr()); r.sync()
