@@ -180,6 +180,17 @@ def main():
     kern_avg_ms = float(np.mean(kern_ms))
 
     if rank == 0:
+        # HBM traffic of one k_render launch: the committed rocprofv3 PMC passes of
+        # this workload (tools/gpu_session.sh -> profiles/pmc_k_render.json)
+        traffic, traffic_src = None, None
+        pj = os.path.join(ROOT, "profiles", "pmc_k_render.json")
+        if world == 1 and os.path.exists(pj):
+            with open(pj) as f:
+                pm = json.load(f)
+            if pm.get("workload") == args.workload and pm.get("traffic_bytes"):
+                traffic = int(pm["traffic_bytes"])
+                traffic_src = {"read_bytes": int(pm["read_bytes"]), "write_bytes": int(pm["write_bytes"]),
+                               "correction": pm["correction"], "source": pm["source"]}
         counts = r.count_work(seed=1)           # one counting launch, outside the timed region
         ops_frame = roofline.algorithmic_ops(counts)
         ops_launch = ops_frame if world == 1 else ops_frame / world
@@ -210,13 +221,14 @@ def main():
                 "achieved": round(achieved_tf, 4),
                 "peak": roofline.FP64_PEAK_TFLOPS,
                 "frac": round(achieved_tf / roofline.FP64_PEAK_TFLOPS, 5),
-                "traffic": None,
+                "traffic": traffic,
                 "kernel": "k_render",
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "algorithmic_fp64_ops_per_launch": int(ops_launch),
                 "note": "FP64 VALU-bound path (no dense contraction): peak = MI355X dense FP64 78.6 TF "
                         "(vector == matrix rate); ops = device-counted reference events x frozen cost table "
                         "(raytracing_rb_amd/roofline.py)",
+                "traffic_detail": traffic_src,
                 "hbm_write": {"achieved": round(wr_gbs, 3), "peak": roofline.HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(wr_gbs / roofline.HBM_PEAK_GBS, 7),
                               "bytes_per_px": roofline.FRAMEBUFFER_BYTES_PER_PX},
