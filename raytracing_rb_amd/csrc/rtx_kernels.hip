@@ -107,10 +107,29 @@ __device__ __forceinline__ unsigned long long stamp() {
 #ifndef RTX_SEPARATE_SINCOS
 #define RTX_SEPARATE_SINCOS 1
 #endif
-#if RTX_SEPARATE_SINCOS
-#define RTX_SINCOS(x, s, c) (*(s) = sin(x), *(c) = cos(x))
+// Transcendentals are real calls by default: inlined into the state machine,
+// their 64-bit polynomial coefficients are hoisted to the kernel entry and
+// spilled, and every sin/cos/acos then waits on a chain of serialized scratch
+// reloads (seen in the gfx950 ISA).  -DRTX_INLINE_MATH=1 inlines them again.
+#ifndef RTX_INLINE_MATH
+#define RTX_INLINE_MATH 0
+#endif
+#if RTX_INLINE_MATH
+#define RTX_MATH_FN __device__ __forceinline__
 #else
-#define RTX_SINCOS(x, s, c) sincos((x), (s), (c))
+#define RTX_MATH_FN __device__ __noinline__
+#endif
+RTX_MATH_FN double rx_sin(double x) { return sin(x); }
+RTX_MATH_FN double rx_cos(double x) { return cos(x); }
+RTX_MATH_FN double rx_asin(double x) { return asin(x); }
+RTX_MATH_FN double rx_acos(double x) { return acos(x); }
+RTX_MATH_FN double rx_pow(double x, double y) { return pow(x, y); }
+RTX_MATH_FN void rx_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+
+#if RTX_SEPARATE_SINCOS
+#define RTX_SINCOS(x, s, c) (*(s) = rx_sin(x), *(c) = rx_cos(x))
+#else
+#define RTX_SINCOS(x, s, c) rx_sincos((x), (s), (c))
 #endif
 
 __device__ __forceinline__ void seterr(uint32_t& err, uint32_t code) {
@@ -199,8 +218,8 @@ RTX_SHADE_FN double penumbra(V3 C, double R, V3 T, V3 lt, double radius, uint32_
     if (c1 > 1.0) c1 = 1.0;
     if (c2 > 1.0) c2 = 1.0;
     if (c1 < -1.0 || c2 < -1.0) seterr(err, ERR_DOMAIN);     // Math::DomainError
-    const double th1 = acos(c1), th2 = acos(c2);
-    const double ds = ((th1 - sin(th1)) * r1 * r1 + (th2 - sin(th2)) * R * R) / 2.0;
+    const double th1 = rx_acos(c1), th2 = rx_acos(c2);
+    const double ds = ((th1 - rx_sin(th1)) * r1 * r1 + (th2 - rx_sin(th2)) * R * R) / 2.0;
     return 1.0 * ds / s1;
   }
   if (r1 > R) return 1.0 * PI * R * R / s1;
@@ -588,8 +607,8 @@ __device__ __forceinline__ bool refraction(const Ray& ray, V3 nn, double c, V3 h
   const double sin_i = sqrt(1.0 - c * c);        // 1 - cos**2
   const double sin_r = sin_i / rate;
   if (sin_r >= 1) return false;                  // total internal reflection
-  const double r = asin(sin_r);
-  out.d = vadd(vsc(nn, -cos(r)), vsc(vnorm(vadd(refl, ray.d), err), sin_r));
+  const double r = rx_asin(sin_r);
+  out.d = vadd(vsc(nn, -rx_cos(r)), vsc(vnorm(vadd(refl, ray.d), err), sin_r));
   out.o = vsub(hit, vsc(nn, EPS));
   return true;
 }
@@ -851,7 +870,7 @@ __device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3
       double c = sqrt(g / r1 / r2);                 // Vec3#cos exactly
       if (c > 1) c = 1;
       if (c < -1) c = -1;
-      fire = acos(c) < L.hl_angle_rad;
+      fire = rx_acos(c) < L.hl_angle_rad;
     }
     if (fire) {
       fired |= 1u << l;
@@ -1117,7 +1136,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
       if (area > 0) {
         const LightDev& L = S.light[li];
         nl++;
-        const double pw = S.sse_is_two ? area * area : pow(area, S.sse);
+        const double pw = S.sse_is_two ? area * area : rx_pow(area, S.sse);
         const V3 lcol = vsc(v3p(L.color), pw / (double)S.n_light);
         const V3 ll = vnorm(vsub(v3p(L.pos), hit), err);
         double ldn = vdot(ll, nn);
