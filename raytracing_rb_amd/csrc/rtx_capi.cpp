@@ -170,11 +170,11 @@ struct Bvh4Builder {
     }
     g[ng] = hi;
     Bvh4Node n;
-    for (int k = 0; k < 4; k++) {
-      n.child[k] = BVH_NONE;
+    for (int k = 0; k < 4; k++) {               // empty slot: a point far outside every scene,
+      n.child[k] = BVH_NONE;                     // which no finite ray's slab test accepts
       for (int a = 0; a < 3; a++) {
-        n.lo[a][k] = 0.0f;
-        n.hi[a][k] = 0.0f;
+        n.lo[a][k] = 3e38f;
+        n.hi[a][k] = 3e38f;
       }
     }
     const int below = pushes + ng - 1;          // visiting one child leaves <= ng-1 siblings pushed

@@ -424,7 +424,7 @@ __device__ __forceinline__ void push_cover(int* ci, double* cv, int& n, bool& ov
 }
 
 template <int BS, typename NP, typename LP>
-__device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32, int* stk, int* ci, double* cv,
+__device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf4, int* stk, int* ci, double* cv,
                                           bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
                                           V3& bhit, bool& bin, double& total, uint32_t& err) {
   const double r = vr(d);
@@ -451,6 +451,12 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32
   // A non-finite or zero ray makes no cull (comparisons would be unordered).
   const bool fin = __builtin_isfinite(dd) && __builtin_isfinite(Sx) && l1 > 0.0f && __builtin_isfinite(ix) &&
                    __builtin_isfinite(iy) && __builtin_isfinite(iz);
+  if (!fin) {
+    // no float32 cull is valid for this ray: the ordered linear walk (same result)
+    if (!ext) total = 1.0;
+    query<false>(S, cptr(S.sph32), ext, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
+    return;
+  }
   const float rf = (float)r;
   // far bound on the ray parameter: EXTEND the current best hit, SHADOW the light
   float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + mS / rf;
@@ -507,8 +513,8 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32
         const float t1z = __builtin_fmaf(nodes[ref].hi[2][k], iz, -bz);
         const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
         const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-        const bool w = ch[k] != BVH_NONE && (!fin || (tn <= tf && tf >= 0.0f && tn <= thi));
-        key[k] = w ? (fin ? tn : 0.0f) : __builtin_inff();
+        // empty slots hold a box at (3e38, 3e38, 3e38): never wanted by a finite ray
+        key[k] = (tn <= tf && tf >= 0.0f && tn <= thi) ? tn : __builtin_inff();
       }
 #define RTX_CS(a, b)         \
   if (key[b] < key[a]) {     \
@@ -535,13 +541,7 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf32
       const int cnt = (v & 3) + 1;
       float4 c[4];
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int b = 4 * (slot0 + u);
-        c[u].x = leaf32[b];
-        c[u].y = leaf32[b + 1];
-        c[u].z = leaf32[b + 2];
-        c[u].w = leaf32[b + 3];
-      }
+      for (int u = 0; u < 4; u++) c[u] = leaf4[slot0 + u];
       uint32_t keep = 0;
 #pragma unroll
       for (int u = 0; u < 4; u++) {
@@ -1106,10 +1106,10 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
     else if (SPH == SPH_LIN_SCALAR)
       query<COUNT>(S, sph_k, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, cnt);
     else if (SPH == SPH_BVH_LDS)
-      query_bvh<BS>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float*>(lds + p.lds_leaf),
+      query_bvh<BS>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
                     stk, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err);
     else
-      query_bvh<BS>(S, S.bvh, S.bvh_sph32, stk, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti,
+      query_bvh<BS>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), stk, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti,
                     hit, hin, total, err);
     if (RTX_STAMPS) {
       t1 = stamp();
