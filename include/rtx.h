@@ -172,6 +172,15 @@ int32_t    rtx_tiles_rows_per_rank(int32_t height, int32_t tile_rows, int32_t nr
 rtx_status rtx_render_tiles_device(rtx_context* ctx, int32_t tile_rows, int32_t rank, int32_t nranks,
                                    uint64_t seed, double* d_packed, void* hip_stream);
 
+/* Host-buffer variant of rtx_render_tiles_device (synchronous): packed holds
+ * rtx_tiles_rows_per_rank() * width * 3 doubles.  One call per worker of
+ * Camera#render_fork (camera.rb:41-68) in a single-process, multi-GPU host. */
+rtx_status rtx_render_tiles(rtx_context* ctx, int32_t tile_rows, int32_t rank, int32_t nranks, uint64_t seed,
+                            double* packed);
+
+/* Number of HIP devices visible to this process (the node's GPUs). */
+int32_t    rtx_device_count(void);
+
 /* Wait for `hip_stream` and report the first reference raise recorded by the
  * device since the last rtx_sync (RTX_OK if none); details in rtx_last_error. */
 rtx_status rtx_sync(rtx_context* ctx, void* hip_stream);
@@ -216,7 +225,8 @@ rtx_status rtx_count_work(rtx_context* ctx, uint64_t seed, uint64_t counts[RTX_N
 rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
 /* keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
          2 always; every choice renders the same bits), "bvh_min" [32], "sphere_src" (0 LDS
-         staging, 1 scalar loads), "force_stack" (per-lane ray-stack bucket). */
+         staging, 1 scalar loads), "lds_stack" (ray-stack entries per lane kept in LDS,
+         -1 = as many as fit), "force_stack" (per-lane ray-stack bucket). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

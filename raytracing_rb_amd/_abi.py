@@ -83,6 +83,8 @@ SIGNATURES = [
     ("rtx_render_device", _I, [_P, _I, _I, _I, _I, _U64, _P, _SZ, _P]),
     ("rtx_tiles_rows_per_rank", _I, [_I, _I, _I]),
     ("rtx_render_tiles_device", _I, [_P, _I, _I, _I, _U64, _P, _P]),
+    ("rtx_render_tiles", _I, [_P, _I, _I, _I, _U64, _DP]),
+    ("rtx_device_count", _I, []),
     ("rtx_sync", _I, [_P, _P]),
     ("rtx_render_at", _I, [_P, _I, _I, _U64, _DP]),
     ("rtx_trace", _I, [_P, _I, _DP, C.POINTER(C.c_int32), _U64, _DP]),

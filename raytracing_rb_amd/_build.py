@@ -22,6 +22,26 @@ FLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fno-fast-math",
          "-shared", "-Wall", "-Wno-unused-result", "-Wno-unused-value"]
 
 
+CLI_SRC = os.path.join(HERE, "cli", "rtx_main.cpp")
+CLI_DEPS = [CLI_SRC] + [os.path.join(HERE, "cli", f) for f in ("yaml_lite.hpp", "png_io.hpp", "scene_load.hpp")] + [
+    os.path.join(ROOT, "include", "rtx.h")]
+CLI_OUT = os.path.join(HERE, "rtx")
+
+
+def build_cli(force=False, verbose=False):
+    """The native CLI (counterpart of src/main.rb): g++ over librtx.so + zlib."""
+    if not force and os.path.exists(CLI_OUT) and all(
+            os.path.getmtime(p) <= os.path.getmtime(CLI_OUT) for p in CLI_DEPS + [OUT]):
+        return CLI_OUT
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", CLI_OUT + ".tmp", CLI_SRC, "-L" + HERE, "-l:librtx.so",
+           "-lz", "-lpthread", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(CLI_OUT + ".tmp", CLI_OUT)
+    return CLI_OUT
+
+
 def stale():
     if not os.path.exists(OUT):
         return True
@@ -43,3 +63,4 @@ def build(force=False, verbose=False, out=None, defines=()):
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
+    build_cli(force="--force" in sys.argv, verbose=True)

@@ -644,6 +644,29 @@ rtx_status rtx_render(rtx_context* c, int32_t x0, int32_t y0, int32_t x1, int32_
   return rtx_sync(c, nullptr);
 }
 
+rtx_status rtx_render_tiles(rtx_context* c, int32_t tile_rows, int32_t rank, int32_t nranks, uint64_t seed,
+                            double* packed) {
+  if (!c || !packed) return fail(c, RTX_EINVAL, "null argument");
+  if (!c->have_cam) return fail(c, RTX_EINVAL, "no camera set");
+  if (tile_rows <= 0 || nranks <= 0 || rank < 0 || rank >= nranks) return fail(c, RTX_EINVAL, "bad tiling");
+  rtx_status s = rtx_sync(c, nullptr);               // clear stale device errors
+  (void)s;
+  hipSetDevice(c->device);
+  const size_t rows = (size_t)rtx_tiles_rows_per_rank(c->cam.height, tile_rows, nranks);
+  const size_t bytes = sizeof(double) * 3 * rows * (size_t)c->cam.width;
+  if (bytes == 0) return RTX_OK;
+  if ((s = ensure_scratch(c, bytes))) return s;
+  HIPCHK(c, hipMemset(c->d_scratch, 0, bytes));
+  if ((s = rtx_render_tiles_device(c, tile_rows, rank, nranks, seed, c->d_scratch, nullptr))) return s;
+  HIPCHK(c, hipMemcpy(packed, c->d_scratch, bytes, hipMemcpyDeviceToHost));
+  return rtx_sync(c, nullptr);
+}
+
+int32_t rtx_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 rtx_status rtx_render_at(rtx_context* c, int32_t x, int32_t y, uint64_t seed, double rgb[3]) {
   return rtx_render(c, x, y, x + 1, y + 1, seed, rgb, 3);
 }
