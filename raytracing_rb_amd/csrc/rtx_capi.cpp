@@ -45,6 +45,8 @@ struct rtx_context {
   unsigned long long* d_counts = nullptr;
   double* d_scratch = nullptr;
   size_t scratch_bytes = 0;
+  double* d_stk = nullptr;           // per-lane global ray-stack regions
+  size_t stk_bytes = 0;
   int* d_work = nullptr;             // ring of per-launch work counters (launches on different streams)
   unsigned work_seq = 0;
   int64_t opt_force_stack = 0;
@@ -246,6 +248,7 @@ void rtx_context_destroy(rtx_context* c) {
   hipFree(c->d_scene);
   hipFree(c->d_cam);
   hipFree(c->d_scratch);
+  hipFree(c->d_stk);
   hipFree(c->d_work);
   delete c;
 }
@@ -529,6 +532,27 @@ static int sph_mode(const rtx_context* c) {
   return c->opt_sphere_src ? SPH_LIN_SCALAR : SPH_LIN_LDS;
 }
 
+// Global per-lane regions (ray-stack entries beyond LDS + render_at's sample
+// colours) for every lane a persistent launch can keep resident (512 per CU:
+// the 256-VGPR kernels run 8 waves per CU).
+static rtx_status ensure_stack(rtx_context* c, KParams& p, int maxs) {
+  int cus = 0;
+  HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  const size_t lanes = (size_t)(cus > 0 ? cus : 1) * 512;
+  const size_t per_lane = ((size_t)maxs * 12 + 3 * 16) * sizeof(double);   // + MAXPRE (16) sample colours
+  const size_t bytes = lanes * per_lane;
+  if (bytes > c->stk_bytes) {
+    hipFree(c->d_stk);
+    c->d_stk = nullptr;
+    c->stk_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->d_stk, bytes));
+    c->stk_bytes = bytes;
+  }
+  p.stk_glb = c->d_stk;
+  p.stk_glb_lanes = (int32_t)(c->stk_bytes / per_lane);
+  return RTX_OK;
+}
+
 static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
   if (!c->have_scene) return fail(c, RTX_EINVAL, "no scene uploaded");
   if (!c->have_cam) return fail(c, RTX_EINVAL, "no camera set");
@@ -555,6 +579,7 @@ rtx_status rtx_render_device(rtx_context* c, int32_t x0, int32_t y0, int32_t x1,
   if (row_stride < (size_t)(x1 - x0) * 3) return fail(c, RTX_EINVAL, "row_stride too small");
   const int maxs = required_stack(c);
   if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  if ((s = ensure_stack(c, p, maxs))) return s;
   hipSetDevice(c->device);
   p.x0 = x0;
   p.nx = x1 - x0;
@@ -581,6 +606,7 @@ rtx_status rtx_render_tiles_device(rtx_context* c, int32_t tile_rows, int32_t ra
   if (tile_rows <= 0 || nranks <= 0 || rank < 0 || rank >= nranks) return fail(c, RTX_EINVAL, "bad tiling");
   const int maxs = required_stack(c);
   if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  if ((s = ensure_stack(c, p, maxs))) return s;
   hipSetDevice(c->device);
   p.x0 = 0;
   p.nx = c->cam.width;
@@ -680,6 +706,7 @@ rtx_status rtx_trace(rtx_context* c, int32_t n, const double* rays, const int32_
   if (s) return s;
   const int maxs = required_stack(c);
   if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  if ((s = ensure_stack(c, p, maxs))) return s;
   rtx_sync(c, nullptr);
   hipSetDevice(c->device);
   const size_t rb = sizeof(double) * 6 * n, kb = sizeof(int32_t) * 3 * n, ob = sizeof(double) * 3 * n;
@@ -706,6 +733,7 @@ rtx_status rtx_count_work(rtx_context* c, uint64_t seed, uint64_t counts[RTX_NCO
   if (s) return s;
   const int maxs = required_stack(c);
   if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  if ((s = ensure_stack(c, p, maxs))) return s;
   hipSetDevice(c->device);
   const int W = c->cam.width, H = c->cam.height;
   if ((s = ensure_scratch(c, sizeof(double) * 3 * (size_t)W * H))) return s;

@@ -678,13 +678,16 @@ RTX_SHADE_FN void hit_info(const SceneDev& S, int obj, const Ray& ray, V3& hit, 
 // Per-lane LIFO of pending rays (RayTracer#trace_sync's Array, ray_tracer.rb:21-30).
 // The bottom `slots` entries live in LDS (11 eight-byte words per entry, laid
 // out word-major across the workgroup's lanes so a wave's accesses are
-// conflict-free); deeper entries go to the lane's private (scratch) array.
+// conflict-free); deeper entries go to the lane's own contiguous region of a
+// global buffer (12 doubles per entry: one push or pop touches two 64-B lines,
+// where a private-array entry, swizzled across the wave, touched 21).
 constexpr int ITEM_WORDS = 11;
+constexpr int GITEM_DOUBLES = 12;
 template <int MAXS>
 struct Stack {
-  Item a[MAXS];
   int n;
   double* lds;     // this lane's word 0 of entry 0; word w of entry e at lds[(e * ITEM_WORDS + w) * bs]
+  double* g;       // this lane's global region: entry e at g[e * GITEM_DOUBLES]
   int bs;
   int slots;
 
@@ -703,7 +706,13 @@ struct Stack {
       q[9 * bs] = __builtin_bit_cast(double, it.path);
       q[10 * bs] = __builtin_bit_cast(double, (int64_t)it.depth);
     } else {
-      a[n - slots] = it;
+      double2* q = reinterpret_cast<double2*>(g + (size_t)(n - slots) * GITEM_DOUBLES);
+      q[0] = make_double2(it.ray.o.x, it.ray.o.y);
+      q[1] = make_double2(it.ray.o.z, it.ray.d.x);
+      q[2] = make_double2(it.ray.d.y, it.ray.d.z);
+      q[3] = make_double2(it.att.x, it.att.y);
+      q[4] = make_double2(it.att.z, __builtin_bit_cast(double, it.path));
+      q[5] = make_double2(__builtin_bit_cast(double, (int64_t)it.depth), 0.0);
     }
     n++;
   }
@@ -717,7 +726,13 @@ struct Stack {
       it.path = __builtin_bit_cast(uint64_t, q[9 * bs]);
       it.depth = (int32_t)__builtin_bit_cast(int64_t, q[10 * bs]);
     } else {
-      it = a[n - slots];
+      const double2* q = reinterpret_cast<const double2*>(g + (size_t)(n - slots) * GITEM_DOUBLES);
+      const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
+      it.ray.o = v3(a.x, a.y, b.x);
+      it.ray.d = v3(b.y, c.x, c.y);
+      it.att = v3(d.x, d.y, e.x);
+      it.path = __builtin_bit_cast(uint64_t, e.y);
+      it.depth = (int32_t)__builtin_bit_cast(int64_t, f.x);
     }
   }
 };
@@ -950,7 +965,9 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   st.bs = BS;
   st.slots = p.stk_slots;
   st.lds = reinterpret_cast<double*>(lds + p.lds_items) + threadIdx.x;
-  V3 smp[MAXPRE];
+  st.g = p.stk_glb + ((size_t)blockIdx.x * BS + threadIdx.x) * (MAXS * GITEM_DOUBLES + 3 * MAXPRE);
+  // the pre_sample_times colours of render_at's variance test, after the stack entries
+  double* smp = st.g + (size_t)MAXS * GITEM_DOUBLES;
   uint32_t err = 0;
   const int pre = cam.pre;
   int ntot = 1;
@@ -991,7 +1008,9 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
               break;
             }
             if (j < pre) {
-              smp[j] = sum;
+              smp[3 * j] = sum.x;
+              smp[3 * j + 1] = sum.y;
+              smp[3 * j + 2] = sum.z;
               avg = vadd(avg, sum);
             } else {
               cv = vadd(cv, sum);
@@ -1000,7 +1019,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
               avg = vdiv(avg, (double)pre);
               double variance = 0.0;
               for (int k = 0; k < pre; k++) {
-                const V3 dd = vsub(smp[k], avg);
+                const V3 dd = vsub(v3(smp[3 * k], smp[3 * k + 1], smp[3 * k + 2]), avg);
                 double mx = dd.x;
                 if (dd.y > mx) mx = dd.y;
                 if (dd.z > mx) mx = dd.z;
@@ -1289,7 +1308,8 @@ static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   if (e != hipSuccess) return e;
   if (per_cu < 1) per_cu = 1;
   const long need = ((long)nwork + BS - 1) / BS;
-  const long blocks = std::min<long>(need, (long)cus * per_cu);
+  long blocks = std::min<long>(need, (long)cus * per_cu);
+  blocks = std::min<long>(blocks, (long)p.stk_glb_lanes / BS);   // lanes with a global ray-stack region
   if (blocks <= 0) return hipSuccess;
   e = hipMemsetAsync(p.work, 0, sizeof(int), s);
   if (e != hipSuccess) return e;

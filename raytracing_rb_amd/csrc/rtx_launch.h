@@ -34,6 +34,8 @@ struct KParams {
   int32_t lds_leaf, lds_stack, lds_cov, lds_items;
   int32_t stk_slots;               // ray-stack entries per lane kept in LDS (set by the launcher)
   int32_t stk_slots_max;           // cap (option "lds_stack"; the stack bucket by default)
+  double* stk_glb;                 // per-lane regions: MAXS * 12 doubles of ray stack + 3 * 16 sample colours
+  int32_t stk_glb_lanes;           // lanes the buffer holds (the launcher caps the grid to it)
 };
 
 // Where the sphere walk reads its records:
