@@ -53,7 +53,7 @@ struct rtx_context {
   int64_t opt_bvh = 1;               // 0: ordered linear walk; 1: hierarchy from opt_bvh_min spheres; 2: always
   int64_t opt_bvh_min = 32;          // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
   int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
-  int64_t opt_lds_stack = -1;        // ray-stack entries per lane in LDS (-1: as many as fit)
+  int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
 };
 
 static rtx_status fail(rtx_context* c, rtx_status s, const char* fmt, ...) {
@@ -533,12 +533,12 @@ static int sph_mode(const rtx_context* c) {
 }
 
 // Global per-lane regions (ray-stack entries beyond LDS + render_at's sample
-// colours) for every lane a persistent launch can keep resident (512 per CU:
-// the 256-VGPR kernels run 8 waves per CU).
+// colours) for every lane a persistent launch can keep resident (512 per CU at
+// 256 VGPRs; room for 1024).
 static rtx_status ensure_stack(rtx_context* c, KParams& p, int maxs) {
   int cus = 0;
   HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-  const size_t lanes = (size_t)(cus > 0 ? cus : 1) * 512;
+  const size_t lanes = (size_t)(cus > 0 ? cus : 1) * 1024;
   const size_t per_lane = ((size_t)maxs * 12 + 3 * 16) * sizeof(double);   // + MAXPRE (16) sample colours
   const size_t bytes = lanes * per_lane;
   if (bytes > c->stk_bytes) {

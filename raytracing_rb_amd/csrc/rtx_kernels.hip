@@ -1245,7 +1245,13 @@ int stack_bucket(int need) {
 constexpr size_t LDS_SPHERE_BYTES = 32 * 1024;
 constexpr size_t LDS_TOTAL_BYTES = 160 * 1024;
 constexpr size_t LDS_LIN_BLOCK_BYTES = 76 * 1024;   // two 256-thread workgroups per CU
-constexpr int BS_LIN = 256, BS_BVH = 512;
+#ifndef RTX_BS_BVH
+#define RTX_BS_BVH 512
+#endif
+constexpr int BS_LIN = 256, BS_BVH = RTX_BS_BVH;
+#ifndef RTX_WPS
+#define RTX_WPS 2            // waves per SIMD the kernels are compiled for (256 VGPRs)
+#endif
 
 static size_t bvh_lds_fixed(const SceneDev& S, int bs) {
   return (size_t)S.bvh_stack * bs * 4 + (size_t)COVER_K * bs * 12 + 64;
@@ -1297,7 +1303,7 @@ template <bool COUNT, int MAXS, int SPH, int SRC>
 static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
   const size_t lds = lds_layout(p, SPH, BS);
-  auto kern = k_render<COUNT, MAXS, 16, 2, SPH, SRC, BS>;
+  auto kern = k_render<COUNT, MAXS, 16, RTX_WPS, SPH, SRC, BS>;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
