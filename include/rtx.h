@@ -20,6 +20,7 @@
  *                          fork_jobs                      src/camera.rb:53-65, src/fork_jobs.rb:5-22
  *   rtx_render_at         Camera#render_at(x, y)         src/camera.rb:70-99
  *   rtx_trace             RayTracer#trace_sync(x, y, ray) src/ray_tracer.rb:16-46
+ *   rtx_path_trace        RayTracer#path_trace_sync(x, y, ray) src/ray_tracer.rb:181-289 (dead code there)
  *   rtx_quantize          Camera#array_to_color + canvas.point  src/camera.rb:105,153-156
  *   rtx_vec3_*            Fast4DMatrix::Vec3 methods     ext/fast_4d_matrix/fast_4d_matrix.c:29-55
  *   rtx_status codes      the reference's raise sites    fast_4d_matrix.c:124,220,291;
@@ -45,7 +46,9 @@ typedef enum rtx_status {
   RTX_EHIP = 4,        /* HIP runtime failure                                                    */
   RTX_ERCCL = 5,       /* collective failure (reported by the host layer)                        */
   RTX_EINVAL = 6,      /* bad descriptor: the reference's NoMethodError/TypeError on missing keys */
-  RTX_ENOMEM = 7
+  RTX_ENOMEM = 7,
+  RTX_ETYPE = 8        /* TypeError "nil can't be coerced into Integer": path_trace's roulette_random
+                          over unassigned probabilities, ray_tracer.rb:167 (world_object.rb:12)       */
 } rtx_status;
 
 enum rtx_object_type { RTX_SPHERE = 0, RTX_PLANE = 1, RTX_BOX = 2 };
@@ -194,6 +197,13 @@ rtx_status rtx_render_at(rtx_context* ctx, int32_t x, int32_t y, uint64_t seed, 
 rtx_status rtx_trace(rtx_context* ctx, int32_t n, const double* rays, const int32_t* keys,
                      uint64_t seed, double* out_rgb);
 
+/* RayTracer#path_trace_sync(x, y, ray) for n rays (host buffers, rays as in
+ * rtx_trace).  Never called by the reference, reproduced with its behaviour:
+ * black below trace_depth 1 or on a miss, the highlight sum when a light's
+ * cone holds the ray, and RTX_ETYPE on any object hit (roulette_random over
+ * nil probabilities raises before any Monte-Carlo child exists). */
+rtx_status rtx_path_trace(rtx_context* ctx, int32_t n, const double* rays, double* out_rgb);
+
 /* Camera#array_to_color (camera.rb:153-156) + PNG::Canvas#point: RGBA8,
  * byte = trunc(min(256*c, 255)); png_gem_blend != 0 additionally applies the
  * png gem's alpha blend over the black canvas ((v*255) >> 8).  Host buffers. */
@@ -224,7 +234,8 @@ rtx_status rtx_count_work(rtx_context* ctx, uint64_t seed, uint64_t counts[RTX_N
 /* Kernel-variant control for experiments; 0 = default. */
 rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
 /* keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
-         2 always; every choice renders the same bits), "bvh_min" [32], "sphere_src" (0 LDS
+         2 always; every choice renders the same bits), "bvh_min" [32], "bvh_sah" (1 [default] binned-SAH hierarchy
+         unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
          staging, 1 scalar loads), "lds_stack" (ray-stack entries per lane kept in LDS,
          -1 = as many as fit), "force_stack" (per-lane ray-stack bucket). */
 

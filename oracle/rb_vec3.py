@@ -21,7 +21,7 @@ import math
 
 
 class RtxError(Exception):
-    """A reference raise site; ``kind`` in {'zero_vec', 'color_gt1', 'domain'}."""
+    """A reference raise site; ``kind`` in {'zero_vec', 'color_gt1', 'domain', 'type'}."""
 
     def __init__(self, kind, msg):
         super().__init__(msg)

@@ -483,6 +483,27 @@ class RayTracer:                   # src/ray_tracer.rb
             leaves.append(att * obj.local_lighting(intersection, lights, n, ray))
         return children, leaves
 
+    def path_trace_sync(self, x, y, ray):             # :181-195 -> path_trace :196-289
+        """Dead code in the reference (never called).  Followed to the first
+        raise: on any hit, roulette_random (:166-179) sums the
+        [action, probability] pairs whose probabilities are never-assigned
+        attr_accessors (world_object.rb:12), and `0 + nil` raises TypeError."""
+        att = Vec3(1.0, 1.0, 1.0)
+        if self.trace_depth <= 0 or att.r < 0.0001:  # :197-201
+            return Vec3(0.0, 0.0, 0.0)
+        ret = Vec3(0.0, 0.0, 0.0)
+        fired = self.world.high_lights(ray)          # :206-214
+        for light, color in fired:
+            ret = ret + att * color / float(len(fired))
+        if fired:
+            return ret
+        obj, intersection, direction, delta, data = self.world.intersect(ray)   # :217
+        if obj is None:                              # :284-288
+            return Vec3(0.0, 0.0, 0.0)
+        obj.intersect_parameters(ray, intersection, direction, delta, data)    # :219 (may raise first)
+        obj.reflect_refract_vector()                 # :224
+        raise RtxError("type", "TypeError: nil can't be coerced into Integer")   # :226-229 -> :167
+
     @staticmethod
     def rt_reduce(c1, c2):                            # :292-298
         ret = c1 + c2

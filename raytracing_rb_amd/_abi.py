@@ -88,6 +88,7 @@ SIGNATURES = [
     ("rtx_sync", _I, [_P, _P]),
     ("rtx_render_at", _I, [_P, _I, _I, _U64, _DP]),
     ("rtx_trace", _I, [_P, _I, _DP, C.POINTER(C.c_int32), _U64, _DP]),
+    ("rtx_path_trace", _I, [_P, _I, _DP, _DP]),
     ("rtx_quantize", _I, [_DP, _I, _I, _SZ, _I, C.POINTER(C.c_uint8)]),
     ("rtx_quantize_device", _I, [_P, _I, _I, _SZ, _I, _P, _P]),
     ("rtx_count_work", _I, [_P, _U64, C.POINTER(C.c_uint64)]),

@@ -65,6 +65,12 @@ class RayTracer:
         out = self._r.trace(rays, np.array([[x, y, sample]], np.int32), seed=self.seed)
         return Vec3(*out[0])
 
+    def path_trace_sync(self, x, y, ray):
+        """RayTracer#path_trace_sync (ray_tracer.rb:181-289), dead code in the
+        reference: black, a highlight sum, or RtxError(kind "type") on a hit."""
+        rays = np.array([ray.front.to_a() + ray.position.to_a()], np.float64)
+        return Vec3(*self._r.path_trace(rays)[0])
+
     def trace_many(self, fronts, positions, keys):
         """Batched trace_sync: fronts/positions [n, 3], keys [n, 3] = (x, y, sample)."""
         rays = np.concatenate([np.asarray(fronts, np.float64), np.asarray(positions, np.float64)], axis=1)

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -25,6 +26,13 @@
 #include "rtx_vec3.h"
 
 using namespace rtx;
+
+#ifndef RTX_BVH_SAH
+#define RTX_BVH_SAH 1                         // default hierarchy splits: 1 binned SAH, 0 median
+#endif
+#ifndef RTX_SAH_PUSHES
+#define RTX_SAH_PUSHES 12                     // SAH only while <= this many traversal-stack entries sit above
+#endif
 
 constexpr unsigned RTX_WORK_RING = 256;
 
@@ -51,7 +59,8 @@ struct rtx_context {
   unsigned work_seq = 0;
   int64_t opt_force_stack = 0;
   int64_t opt_bvh = 1;               // 0: ordered linear walk; 1: hierarchy from opt_bvh_min spheres; 2: always
-  int64_t opt_bvh_min = 32;          // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
+  int64_t opt_bvh_sah = RTX_BVH_SAH;  // hierarchy splits: 1 binned SAH, 0 median (applies at the next upload)
+  int64_t opt_bvh_min = 32;         // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
   int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
 };
@@ -81,8 +90,9 @@ static void free_scene(rtx_context* c) {
 }
 
 // ------------------------------------------------------------------ BVH build
-// Four-wide hierarchy: each node splits its spheres at the median of the
-// longest centroid axis, then splits each half again (up to four children);
+// Four-wide hierarchy: each node splits its spheres in two (binned SAH near
+// the root, median of the longest centroid axis below), then splits each half
+// again (up to four children);
 // groups of <= BVH_LEAF spheres become leaves.  Child boxes are float32 and
 // contain every member sphere exactly (bounds rounded outwards); see
 // DESIGN.md §2.1 and rtx_scene.h.
@@ -130,13 +140,85 @@ struct Bvh4Builder {
     }
   }
 
-  int split(int lo, int hi) {                   // median split on the longest centroid axis
+  // Split sp[lo, hi) in two.  Binned surface-area heuristic (16 centroid bins
+  // per axis, cost = area(left) * n_left + area(right) * n_right over the
+  // spheres' boxes) while the traversal stack above stays shallow; otherwise,
+  // or when no bin boundary separates the centroids, the median of the longest
+  // centroid axis.  Deterministic: stable partitions, first-best bin wins.
+  bool sah = true;
+  int split(int lo, int hi, int pushes = 0) {
     double cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = lo; i < hi; i++)
       for (int a = 0; a < 3; a++) {
         cmn[a] = fmin(cmn[a], sp[i].c[a]);
         cmx[a] = fmax(cmx[a], sp[i].c[a]);
       }
+    if (sah && pushes <= RTX_SAH_PUSHES) {
+      constexpr int NB = 16;
+      auto bin_of = [&](double x, int a) {
+        int b = (int)((x - cmn[a]) / (cmx[a] - cmn[a]) * NB);
+        return b < 0 ? 0 : (b >= NB ? NB - 1 : b);
+      };
+      auto area = [](const double* mn, const double* mx) {
+        const double dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+        return dx * dy + dy * dz + dz * dx;
+      };
+      double best = INFINITY;
+      int best_axis = -1, best_bin = -1;
+      for (int a = 0; a < 3; a++) {
+        if (!(cmx[a] - cmn[a] > 0)) continue;
+        double bmn[NB][3], bmx[NB][3];
+        int cnt[NB] = {0};
+        for (int b = 0; b < NB; b++)
+          for (int k = 0; k < 3; k++) {
+            bmn[b][k] = INFINITY;
+            bmx[b][k] = -INFINITY;
+          }
+        for (int i = lo; i < hi; i++) {
+          const int b = bin_of(sp[i].c[a], a);
+          const double r = fabs(sp[i].r);
+          cnt[b]++;
+          for (int k = 0; k < 3; k++) {
+            bmn[b][k] = fmin(bmn[b][k], sp[i].c[k] - r);
+            bmx[b][k] = fmax(bmx[b][k], sp[i].c[k] + r);
+          }
+        }
+        double rmn[NB][3], rmx[NB][3];                  // suffix boxes over bins b..NB-1
+        int rcnt[NB];
+        double amn[3] = {INFINITY, INFINITY, INFINITY}, amx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int acc = 0;
+        for (int b = NB - 1; b >= 0; b--) {
+          for (int k = 0; k < 3; k++) {
+            rmn[b][k] = amn[k] = fmin(amn[k], bmn[b][k]);
+            rmx[b][k] = amx[k] = fmax(amx[k], bmx[b][k]);
+          }
+          rcnt[b] = acc += cnt[b];
+        }
+        double lmn[3] = {INFINITY, INFINITY, INFINITY}, lmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int lc = 0;
+        for (int b = 0; b + 1 < NB; b++) {              // left = bins 0..b, right = bins b+1..
+          for (int k = 0; k < 3; k++) {
+            lmn[k] = fmin(lmn[k], bmn[b][k]);
+            lmx[k] = fmax(lmx[k], bmx[b][k]);
+          }
+          lc += cnt[b];
+          if (lc == 0 || rcnt[b + 1] == 0) continue;
+          const double cost = area(lmn, lmx) * lc + area(rmn[b + 1], rmx[b + 1]) * rcnt[b + 1];
+          if (cost < best) {
+            best = cost;
+            best_axis = a;
+            best_bin = b;
+          }
+        }
+      }
+      if (best_axis >= 0) {
+        const int a = best_axis;
+        auto it = std::stable_partition(sp.begin() + lo, sp.begin() + hi,
+                                        [&](const BSph& q) { return bin_of(q.c[a], a) <= best_bin; });
+        const int mid = (int)(it - sp.begin());
+        if (mid > lo && mid < hi) return mid;
+      }
+    }
     int axis = 0;
     for (int a = 1; a < 3; a++)
       if (cmx[a] - cmn[a] > cmx[axis] - cmn[axis]) axis = a;
@@ -164,11 +246,11 @@ struct Bvh4Builder {
     const int me = (int)nodes.size();
     nodes.push_back(Bvh4Node{});
     int g[5], ng = 0;
-    const int mid = split(lo, hi);
+    const int mid = split(lo, hi, pushes);
     for (int h = 0; h < 2; h++) {
       const int a = h ? mid : lo, b = h ? hi : mid;
       g[ng++] = a;
-      if (b - a > BVH_LEAF) g[ng++] = split(a, b);
+      if (b - a > BVH_LEAF) g[ng++] = split(a, b, pushes);
     }
     g[ng] = hi;
     Bvh4Node n;
@@ -210,6 +292,7 @@ const char* rtx_status_string(rtx_status s) {
     case RTX_ERCCL: return "RCCL error";
     case RTX_EINVAL: return "invalid argument";
     case RTX_ENOMEM: return "out of memory";
+    case RTX_ETYPE: return "TypeError: nil can't be coerced into Integer";
   }
   return "unknown";
 }
@@ -228,7 +311,7 @@ rtx_status rtx_context_create(int32_t device, rtx_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_cam, sizeof(CameraDev));
   if (e == hipSuccess) e = hipMalloc(&c->d_work, sizeof(int) * RTX_WORK_RING);
   if (e == hipSuccess) e = hipMemset(c->d_err, 0, sizeof(unsigned int) * 2);
-  if (e == hipSuccess) e = hipMemset(((char*)c->d_err) + 8, 0xFF, sizeof(unsigned long long) * 4);
+  if (e == hipSuccess) e = hipMemset(((char*)c->d_err) + 8, 0xFF, sizeof(ErrState) - 8);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     fprintf(stderr, "rtx_context_create: %s\n", hipGetErrorString(e));
@@ -262,6 +345,10 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "bvh")) {               // 0: linear ordered walk; 1: auto (>= bvh_min spheres); 2: always
     if (value < 0 || value > 2) return fail(c, RTX_EINVAL, "bvh must be 0, 1 or 2");
     c->opt_bvh = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "bvh_sah")) {           // hierarchy splits: 1 binned SAH, 0 median (at the next upload)
+    c->opt_bvh_sah = value != 0;
     return RTX_OK;
   }
   if (!strcmp(key, "bvh_min")) {           // sphere count from which bvh=1 uses the hierarchy
@@ -398,8 +485,25 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
     bs[k].r = sph64[k].r;
     bs[k].rec = (int)k;
   }
-  Bvh4Builder bb{bs, sph64, sph32, sph_obj};
-  const int32_t bvh_root = bs.empty() ? BVH_NONE : bb.build(0, (int)bs.size(), 0);
+  // SAH splits unless their tree would not fit the LDS of a hierarchy
+  // workgroup while the median tree does (C4: the SAH tree spills to global
+  // memory and renders 10 % slower; C2: SAH 1.3 % faster).
+  const std::vector<BSph> bs_in = bs;
+  auto bbp = std::make_unique<Bvh4Builder>(Bvh4Builder{bs, sph64, sph32, sph_obj});
+  bbp->sah = c->opt_bvh_sah != 0;
+  int32_t bvh_root = bs.empty() ? BVH_NONE : bbp->build(0, (int)bs.size(), 0);
+  if (bbp->sah && !bs.empty() &&
+      bvh_lds_bytes((int)bbp->nodes.size(), (int)bbp->slot_obj.size(), bbp->stack + 1) > bvh_lds_budget()) {
+    bs = bs_in;
+    auto med = std::make_unique<Bvh4Builder>(Bvh4Builder{bs, sph64, sph32, sph_obj});
+    med->sah = false;
+    const int32_t r = med->build(0, (int)bs.size(), 0);
+    if (bvh_lds_bytes((int)med->nodes.size(), (int)med->slot_obj.size(), med->stack + 1) <= bvh_lds_budget()) {
+      bbp = std::move(med);
+      bvh_root = r;
+    }
+  }
+  const Bvh4Builder& bb = *bbp;
   for (int k = 0; k < 16; k++) sph32.push_back(0.0f);   // 4 padding records: group loads stay in bounds
   std::vector<LightDev> lights(sd->n_lights);
   for (int i = 0; i < sd->n_lights; i++) {
@@ -627,16 +731,17 @@ rtx_status rtx_sync(rtx_context* c, void* stream) {
   HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
   HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof e, hipMemcpyDeviceToHost));
   HIPCHK(c, hipMemset(c->d_err, 0, 8));
-  HIPCHK(c, hipMemset(((char*)c->d_err) + 8, 0xFF, 32));
+  HIPCHK(c, hipMemset(((char*)c->d_err) + 8, 0xFF, sizeof(ErrState) - 8));
   HIPCHK(c, hipDeviceSynchronize());
   if (!e.flags) return RTX_OK;
-  static const rtx_status order[3] = {RTX_EZERO_VEC, RTX_ECOLOR_GT1, RTX_EDOMAIN};
+  // device ERR_ code -> rtx_status (index = ERR_ code, rtx_vec3.h)
+  static const rtx_status status_of[5] = {RTX_OK, RTX_EZERO_VEC, RTX_ECOLOR_GT1, RTX_EDOMAIN, RTX_ETYPE};
   rtx_status first = RTX_OK;
   unsigned long long pix = ~0ull;
-  for (rtx_status code : order)
+  for (int code = 1; code < 5; code++)
     if ((e.flags >> code & 1) && e.first[code] < pix) {
       pix = e.first[code];
-      first = code;
+      first = status_of[code];
     }
   const long long W = c->have_cam ? c->cam.width : 1;
   return fail(c, first, "%s at pixel (%lld,%lld)%s", rtx_status_string(first), (long long)(pix % W),
@@ -722,6 +827,27 @@ rtx_status rtx_trace(rtx_context* c, int32_t n, const double* rays, const int32_
   p.keys = d_keys;
   p.nrays = n;
   HIPCHK(c, launch_trace(p, sph_mode(c), maxs, nullptr));
+  HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
+  return rtx_sync(c, nullptr);
+}
+
+rtx_status rtx_path_trace(rtx_context* c, int32_t n, const double* rays, double* out) {
+  if (!c || n < 0 || (n && (!rays || !out))) return fail(c, RTX_EINVAL, "bad arguments");
+  if (n == 0) return RTX_OK;
+  KParams p;
+  rtx_status s = prep(c, p, 1);
+  if (s) return s;
+  rtx_sync(c, nullptr);
+  hipSetDevice(c->device);
+  const size_t rb = sizeof(double) * 6 * n, ob = sizeof(double) * 3 * n;
+  if ((s = ensure_scratch(c, rb + ob))) return s;
+  double* d_rays = c->d_scratch;
+  double* d_out = c->d_scratch + 6 * (size_t)n;
+  HIPCHK(c, hipMemcpy(d_rays, rays, rb, hipMemcpyHostToDevice));
+  p.out = d_out;
+  p.rays = d_rays;
+  p.nrays = n;
+  HIPCHK(c, launch_path_trace(p, nullptr));
   HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
   return rtx_sync(c, nullptr);
 }

@@ -860,6 +860,9 @@ __device__ __forceinline__ Ray lens_ray(const CameraDev& c, V3 target, int x, in
 // World#high_lights (world.rb:83-98) for `ray`; fired leaves go into `sum`.
 // Returns true if any light fired (the ray then stops, ray_tracer.rb:77).
 // The `&& lit_area(...)` is always truthy in Ruby and is not evaluated.
+// REDUCE: leaves go through rt_reduce (trace_sync); path_trace adds them
+// with a plain `ret +=` (ray_tracer.rb:210), no "color greater than 1" check.
+template <bool REDUCE = true>
 __device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3& sum, uint32_t& err) {
   uint32_t fired = 0;
   int nfired = 0;
@@ -896,7 +899,9 @@ __device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3
   for (int l = 0; l < S.n_light; l++) {
     if (!(fired >> l & 1)) continue;
     const RTX_CONST LightDev& L = lights[l];
-    add_leaf(sum, vdiv(vmul(it.att, vsc(v3(L.color[0], L.color[1], L.color[2]), L.hl_rate)), (double)nfired), err);
+    const V3 leaf = vdiv(vmul(it.att, vsc(v3(L.color[0], L.color[1], L.color[2]), L.hl_rate)), (double)nfired);
+    if (REDUCE) add_leaf(sum, leaf, err);
+    else sum = vadd(sum, leaf);
   }
   return true;
 }
@@ -1202,6 +1207,54 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
     for (int k = 0; k < C_N; k++) atomicAdd(&p.counts[k], cnt[k]);
 }
 
+// RayTracer#path_trace_sync / #path_trace (ray_tracer.rb:181-289) for explicit
+// rays, one lane per ray.  Dead code in the reference (never called), kept for
+// API fidelity with its exact behaviour:
+//   * trace_depth <= 0 (attenuation starts at 1): black (:197-201);
+//   * a light in the highlight cone: the sum of att * color / n (:206-214);
+//   * no object hit: black (:284-288);
+//   * a hit: intersect_parameters runs (its normalize / asin raises come
+//     first), then roulette_random sums the never-assigned *_probability
+//     accessors (world_object.rb:12): `0 + nil` raises TypeError (:167).
+// The Monte-Carlo children are therefore unreachable.  The walk is the
+// ordered linear one (same first-index nearest hit as every other walk).
+__global__ __launch_bounds__(256) void k_path_trace(KParams p) {
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  if (i >= p.nrays) return;
+  const SceneDev& S = p.scene;
+  Item it;
+  it.ray.d = v3p(p.rays + 6 * (size_t)i);
+  it.ray.o = v3p(p.rays + 6 * (size_t)i + 3);
+  it.att = v3(1.0, 1.0, 1.0);
+  it.path = 1;
+  it.depth = p.cam->depth;
+  uint32_t err = 0;
+  V3 sum = v3(0.0, 0.0, 0.0);
+  if (it.depth > 0 && !(vr(it.att) < 0.0001) && !highlights<false>(S, it, sum, err)) {
+    double best = S.max_distance, total = 0.0;
+    int besti = -1;
+    V3 hit = sum;
+    bool hin = true;
+    query<false>(S, cptr(S.sph32), true, it.ray.o, it.ray.d, hit, 0.0, best, besti, hit, hin, total, err, nullptr);
+    if (besti >= 0) {
+      V3 delta, n;
+      hit_info(S, besti, it.ray, hit, delta, n, hin);
+      const V3 nn = vnorm(n, err);
+      const double c = vcos(it.ray.d, n, err);
+      const Ray refl = reflection(it.ray, nn, c, hit, delta, err);
+      const Material& m = S.mat[besti];
+      Ray refr;
+      if (m.type == OBJ_SPHERE) refraction(it.ray, nn, c, hit, refl.d, hin ? m.rr : 1.0 / m.rr, refr, err);
+      else if (m.has_rr) refraction(it.ray, nn, c, hit, refl.d, m.rr, refr, err);
+      seterr(err, ERR_TYPE);
+    }
+  }
+  p.out[3 * (size_t)i] = sum.x;
+  p.out[3 * (size_t)i + 1] = sum.y;
+  p.out[3 * (size_t)i + 2] = sum.z;
+  if (err) record_error(p.err, err, i, 0, 0x7fffffff);
+}
+
 // Camera#array_to_color (camera.rb:153-156) + PNG::Canvas#point over black.
 __global__ void k_quantize(const double* __restrict__ rgb, int w, int h, size_t stride, int blend,
                            uint8_t* __restrict__ out) {
@@ -1253,14 +1306,15 @@ constexpr int BS_LIN = 256, BS_BVH = RTX_BS_BVH;
 #define RTX_WPS 2            // waves per SIMD the kernels are compiled for (256 VGPRs)
 #endif
 
-static size_t bvh_lds_fixed(const SceneDev& S, int bs) {
-  return (size_t)S.bvh_stack * bs * 4 + (size_t)COVER_K * bs * 12 + 64;
+size_t bvh_lds_bytes(int n_nodes, int n_slots, int bvh_stack) {
+  return (size_t)n_nodes * sizeof(Bvh4Node) + (size_t)n_slots * 16 + (size_t)bvh_stack * BS_BVH * 4 +
+         (size_t)COVER_K * BS_BVH * 12 + 64;
 }
+size_t bvh_lds_budget() { return LDS_TOTAL_BYTES; }
 
 int resolve_mode(const SceneDev& S, int mode) {
   if (mode == SPH_LIN_LDS && (size_t)(S.n_sphere + 4) * 16 > LDS_SPHERE_BYTES) return SPH_LIN_SCALAR;
-  if (mode == SPH_BVH_LDS &&
-      (size_t)S.n_nodes * sizeof(Bvh4Node) + (size_t)S.n_slots * 16 + bvh_lds_fixed(S, BS_BVH) > LDS_TOTAL_BYTES)
+  if (mode == SPH_BVH_LDS && bvh_lds_bytes(S.n_nodes, S.n_slots, S.bvh_stack) > LDS_TOTAL_BYTES)
     return SPH_BVH_GLOBAL;
   return mode;
 }
@@ -1362,6 +1416,12 @@ hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s) {
     case 64: return launch_mode<false, 64, SRC_RAYS>(p, mode, p.nrays, s);
   }
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_path_trace(KParams p, hipStream_t s) {
+  if (p.nrays <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_path_trace, dim3((unsigned)((p.nrays + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
 }
 
 hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,

@@ -13,7 +13,7 @@ namespace rtx {
 struct ErrState {
   unsigned int flags;              // bit (1 << code) for every code raised
   unsigned int pad;
-  unsigned long long first[4];     // per code: min linear pixel index (y*W + x)
+  unsigned long long first[5];     // per ERR_ code (rtx_vec3.h): min linear pixel index (y*W + x)
 };
 
 struct KParams {
@@ -52,7 +52,12 @@ int stack_bucket(int need);
 // linearly (the counters are the reference's brute-force events).
 hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s);
 hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s);
+hipError_t launch_path_trace(KParams p, hipStream_t s);
 int resolve_mode(const SceneDev& S, int mode);
+// LDS bytes a hierarchy workgroup needs (nodes + leaf records + traversal
+// stacks + cover lists) and the budget SPH_BVH_LDS has.
+size_t bvh_lds_bytes(int n_nodes, int n_slots, int bvh_stack);
+size_t bvh_lds_budget();
 hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,
                            hipStream_t s);
 

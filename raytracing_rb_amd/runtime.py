@@ -17,7 +17,8 @@ from ._abi import RTX_NCOUNT, COUNTER_NAMES, load_library
 
 
 class RtxError(RuntimeError):
-    KINDS = {1: "zero_vec", 2: "color_gt1", 3: "domain", 4: "hip", 5: "rccl", 6: "invalid", 7: "nomem"}
+    KINDS = {1: "zero_vec", 2: "color_gt1", 3: "domain", 4: "hip", 5: "rccl", 6: "invalid", 7: "nomem",
+             8: "type"}
 
     def __init__(self, status, msg):
         super().__init__("%s (rtx_status %d)" % (msg, status))
@@ -94,6 +95,13 @@ class Renderer:
         out = np.empty((len(rays), 3), np.float64)
         self._check(self.lib.rtx_trace(self.h, len(rays), _dp(rays),
                                        keys.ctypes.data_as(C.POINTER(C.c_int32)), seed, _dp(out)))
+        return out
+
+    def path_trace(self, rays):
+        """RayTracer#path_trace_sync for rays [n, 6] = (front, position) -> [n, 3]."""
+        rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)
+        out = np.empty((len(rays), 3), np.float64)
+        self._check(self.lib.rtx_path_trace(self.h, len(rays), _dp(rays), _dp(out)))
         return out
 
     def count_work(self, seed=1):

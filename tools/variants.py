@@ -71,6 +71,10 @@ if __name__ == "__main__":
         import argparse
         ap = argparse.ArgumentParser()
         ap.add_argument("cmd"); ap.add_argument("--scene", default="c2"); ap.add_argument("--rounds", type=int, default=3)
-        ap.add_argument("--opts", default="{}")
+        ap.add_argument("--opts", default="{}"); ap.add_argument("--reps", type=int, default=5)
         a = ap.parse_args()
-        time_all(a.scene, a.rounds, opts=a.opts)
+        if a.scene == "c4":
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import make_scenes
+            make_scenes.ensure_c4()
+        time_all(a.scene, a.rounds, reps=a.reps, opts=a.opts)
