@@ -53,7 +53,8 @@ def build(force=False, verbose=False, out=None, defines=()):
     out = out or OUT
     if not force and out == OUT and not stale():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-o", out + ".tmp"] + SOURCES
+    # `defines`: NAME[=VALUE] macros; entries starting with "-" are raw compiler flags
+    cmd = [HIPCC] + FLAGS + [d if d.startswith("-") else "-D" + d for d in defines] + ["-o", out + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -312,6 +312,13 @@ rtx_status rtx_context_create(int32_t device, rtx_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_work, sizeof(int) * RTX_WORK_RING);
   if (e == hipSuccess) e = hipMemset(c->d_err, 0, sizeof(unsigned int) * 2);
   if (e == hipSuccess) e = hipMemset(((char*)c->d_err) + 8, 0xFF, sizeof(ErrState) - 8);
+  if (e == hipSuccess) {           // keep render_region's stream-ordered buffers pooled between frames
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     fprintf(stderr, "rtx_context_create: %s\n", hipGetErrorString(e));
@@ -636,14 +643,13 @@ static int sph_mode(const rtx_context* c) {
   return c->opt_sphere_src ? SPH_LIN_SCALAR : SPH_LIN_LDS;
 }
 
-// Global per-lane regions (ray-stack entries beyond LDS + render_at's sample
-// colours) for every lane a persistent launch can keep resident (512 per CU at
+// Global per-lane regions (ray-stack entries beyond LDS) for every lane a persistent launch can keep resident (512 per CU at
 // 256 VGPRs; room for 1024).
 static rtx_status ensure_stack(rtx_context* c, KParams& p, int maxs) {
   int cus = 0;
   HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
   const size_t lanes = (size_t)(cus > 0 ? cus : 1) * 1024;
-  const size_t per_lane = ((size_t)maxs * 12 + 3 * 16) * sizeof(double);   // + MAXPRE (16) sample colours
+  const size_t per_lane = (size_t)maxs * 12 * sizeof(double);
   const size_t bytes = lanes * per_lane;
   if (bytes > c->stk_bytes) {
     hipFree(c->d_stk);
@@ -668,6 +674,29 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
   p.counts = c->d_counts;
   p.work = c->d_work + (c->work_seq++ % RTX_WORK_RING);
   p.stk_slots_max = c->opt_lds_stack < 0 ? 64 : (int32_t)c->opt_lds_stack;
+  p.pre = c->cam.pre;
+  p.max_samples = c->cam.max_samples;
+  return RTX_OK;
+}
+
+// launch_render with its per-launch sample records and extra-sample list,
+// allocated stream-ordered (the device's default pool keeps the memory, so
+// after the first frame this costs no hipMalloc) and freed after the launch,
+// so launches of one context on different streams never share them.
+static rtx_status render_region(rtx_context* c, KParams& p, bool count, int maxs, hipStream_t stream) {
+  const size_t npx = (size_t)p.nx * p.nrows;
+  if (npx == 0) return RTX_OK;
+  const size_t ms = (size_t)std::max(p.pre, p.max_samples);
+  const size_t smp_bytes = npx * ms * 4 * sizeof(double);
+  void* buf = nullptr;
+  HIPCHK(c, hipMallocAsync(&buf, smp_bytes + (npx + 64) * sizeof(int32_t), stream));
+  p.samples = (double*)buf;
+  p.extra_count = (int32_t*)((char*)buf + smp_bytes);
+  p.extra_list = p.extra_count + 64;
+  const hipError_t e = launch_render(p, sph_mode(c), count, maxs, stream);
+  const hipError_t f = hipFreeAsync(buf, stream);
+  HIPCHK(c, e);
+  HIPCHK(c, f);
   return RTX_OK;
 }
 
@@ -691,8 +720,7 @@ rtx_status rtx_render_device(rtx_context* c, int32_t x0, int32_t y0, int32_t x1,
   p.nrows = y1 - y0;
   p.out = d_out;
   p.stride = row_stride;
-  HIPCHK(c, launch_render(p, sph_mode(c), false, maxs, (hipStream_t)stream));
-  return RTX_OK;
+  return render_region(c, p, false, maxs, (hipStream_t)stream);
 }
 
 int32_t rtx_tiles_rows_per_rank(int32_t height, int32_t tile_rows, int32_t nranks) {
@@ -720,8 +748,7 @@ rtx_status rtx_render_tiles_device(rtx_context* c, int32_t tile_rows, int32_t ra
   p.nranks = nranks;
   p.out = d_packed;
   p.stride = (size_t)c->cam.width * 3;
-  HIPCHK(c, launch_render(p, sph_mode(c), false, maxs, (hipStream_t)stream));
-  return RTX_OK;
+  return render_region(c, p, false, maxs, (hipStream_t)stream);
 }
 
 rtx_status rtx_sync(rtx_context* c, void* stream) {
@@ -869,7 +896,7 @@ rtx_status rtx_count_work(rtx_context* c, uint64_t seed, uint64_t counts[RTX_NCO
   p.nrows = H;
   p.out = c->d_scratch;
   p.stride = (size_t)W * 3;
-  HIPCHK(c, launch_render(p, sph_mode(c), true, maxs, nullptr));
+  if ((s = render_region(c, p, true, maxs, nullptr))) return s;
   HIPCHK(c, hipDeviceSynchronize());
   unsigned long long tmp[RTX_NCOUNT];
   HIPCHK(c, hipMemcpy(tmp, c->d_counts, sizeof tmp, hipMemcpyDeviceToHost));

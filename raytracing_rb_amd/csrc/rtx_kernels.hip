@@ -78,7 +78,7 @@ __device__ __forceinline__ const RTX_CONST T* cptr(const T* p) {
   return (const RTX_CONST T*)(p);
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-enum { SRC_PIXELS = 0, SRC_RAYS = 1 };
+enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2 };
 
 // Diagnostic build only (-DRTX_STAMPS=1): per-wave shader-clock time spent in
 // each phase of the lane state machine, summed into rtx_stamps[] (read with
@@ -89,7 +89,14 @@ enum { SRC_PIXELS = 0, SRC_RAYS = 1 };
 #ifndef RTX_STAMPS
 #define RTX_STAMPS 0
 #endif
-__device__ unsigned long long rtx_stamps[8];
+__device__ unsigned long long rtx_stamps[16];
+__device__ __forceinline__ unsigned long long wall() {   // 100 MHz constant clock, same on every XCD
+#if RTX_STAMPS
+  return __builtin_amdgcn_s_memrealtime();
+#else
+  return 0;
+#endif
+}
 __device__ __forceinline__ unsigned long long stamp() {
 #if RTX_STAMPS
   unsigned long long t;
@@ -917,11 +924,14 @@ __device__ __forceinline__ int row_to_y(const KParams& p, int row) {
   return (k * p.nranks + p.rank) * p.tile_rows + (row - k * p.tile_rows);
 }
 
-// SRC_PIXELS: one lane per pixel (a wave covers an 8x8 tile) running
-// Camera#render_at.  SRC_RAYS: one lane per explicit ray running
+// SRC_PIXELS: work item = one of Camera#render_at's pre_sample_times samples
+// of one pixel (a wave's first fetch covers an 8x8 tile for one sample index);
+// the sample's colour and first raise go to p.samples, and k_finalize does the
+// mean / variance / extra-sample decision.  SRC_EXTRA: the extra samples of the
+// pixels k_finalize listed.  SRC_RAYS: one lane per explicit ray running
 // RayTracer#trace_sync (rtx_trace).  SPH: where the sphere walk reads its
 // records (SphMode, rtx_launch.h).  BS: threads per workgroup.
-template <bool COUNT, int MAXS, int MAXPRE, int WPS, int SPH, int SRC, int BS>
+template <bool COUNT, int MAXS, int WPS, int SPH, int SRC, int BS>
 __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   const double* __restrict__ rays = p.rays;
   const int32_t* __restrict__ keys = p.keys;
@@ -951,13 +961,18 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
   double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
 
-  // Persistent lanes: every lane takes work items (SRC_PIXELS: pixels in
-  // 8x8-tile order; SRC_RAYS: rays) from one counter per launch and takes the
-  // next one as soon as its current item is finished, so no lane idles until
-  // the pool is empty.  A wave's lanes that need work are served by one atomic
-  // (ballot + prefix count); a fresh wave's first fetch is one whole tile.
+  // Persistent lanes: every lane takes work items (SRC_PIXELS: (pixel, sample)
+  // in 8x8-tile order; SRC_EXTRA: (listed pixel, extra sample); SRC_RAYS: rays)
+  // from one counter per launch and takes the next one as soon as its current
+  // item is finished, so no lane idles until the pool is empty.  Items are one
+  // ray tree each: the longest item, which bounds the launch's tail, is one
+  // sample, not a whole pixel.  A wave's lanes that need work are served by one
+  // atomic (ballot + prefix count).
   const int tiles_x = (p.nx + 7) >> 3;
-  const int nwork = SRC == SRC_PIXELS ? tiles_x * ((p.nrows + 7) >> 3) * 64 : nrays;
+  const int pre = p.pre, n_extra = p.max_samples - p.pre;
+  const int ms = p.max_samples > p.pre ? p.max_samples : p.pre;   // sample records per pixel
+  const int nwork = SRC == SRC_PIXELS ? tiles_x * ((p.nrows + 7) >> 3) * 64 * pre
+                    : SRC == SRC_EXTRA ? *p.extra_count * n_extra : nrays;
   int x = 0, y = 0, row = 0, px_ = 0;
   V3 tgt = v3(0.0, 0.0, 0.0);
 
@@ -970,16 +985,11 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   st.bs = BS;
   st.slots = p.stk_slots;
   st.lds = reinterpret_cast<double*>(lds + p.lds_items) + threadIdx.x;
-  st.g = p.stk_glb + ((size_t)blockIdx.x * BS + threadIdx.x) * (MAXS * GITEM_DOUBLES + 3 * MAXPRE);
-  // the pre_sample_times colours of render_at's variance test, after the stack entries
-  double* smp = st.g + (size_t)MAXS * GITEM_DOUBLES;
+  st.g = p.stk_glb + ((size_t)blockIdx.x * BS + threadIdx.x) * (MAXS * GITEM_DOUBLES);
   uint32_t err = 0;
-  const int pre = cam.pre;
-  int ntot = 1;
-  bool extra = false;
-  V3 avg = v3(0.0, 0.0, 0.0), cv = avg, sum = avg;
-  int j = -1;                        // current camera sample
-  int sample = 0;                    // RNG key of the current tree
+  V3 sum = v3(0.0, 0.0, 0.0), avg = sum;
+  bool started = false;              // the current item's tree has begun
+  int sample = 0;                    // camera sample of the item = RNG key of its tree
   Item cur;
   bool have = false;                 // `cur` holds a ray not yet processed
   int mode = M_FETCH;
@@ -992,6 +1002,9 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   double qrad = 0.0;
 
   unsigned long long tA = 0, tB = 0, tC = 0, tD = 0, iters = 0, t0 = 0, t1;
+  const unsigned long long w_start = wall();
+  unsigned long long w_dry = 0;                // when this lane found the work pool empty
+  unsigned long long w_item = 0, w_maxitem = 0; // start of the current item, longest item
   while (true) {
     if (RTX_STAMPS) t0 = stamp();
     // ---- A: find this lane's next query (divergent, short)
@@ -1002,56 +1015,26 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
         } else if (st.n > 0) {
           st.pop(cur);
         } else {
-          // the current tree (camera sample) is complete
-          if (j >= 0) {
+          // the current tree is complete: the item's result
+          if (started) {
             if (SRC == SRC_RAYS) {
               p.out[3 * row] = sum.x;
               p.out[3 * row + 1] = sum.y;
               p.out[3 * row + 2] = sum.z;
               if (err) record_error(p.err, err, row, 0, 0x7fffffff);
-              mode = M_FETCH;
-              break;
+            } else {                            // one camera sample: colour + first raise
+              double2* q = reinterpret_cast<double2*>(p.samples + ((size_t)row * p.nx + px_) * ms * 4 +
+                                                      (size_t)sample * 4);
+              q[0] = make_double2(sum.x, sum.y);
+              q[1] = make_double2(sum.z, __builtin_bit_cast(double, (uint64_t)err));
             }
-            if (j < pre) {
-              smp[3 * j] = sum.x;
-              smp[3 * j + 1] = sum.y;
-              smp[3 * j + 2] = sum.z;
-              avg = vadd(avg, sum);
-            } else {
-              cv = vadd(cv, sum);
-            }
-            if (j + 1 == pre) {                 // camera.rb:80-85: mean and variance
-              avg = vdiv(avg, (double)pre);
-              double variance = 0.0;
-              for (int k = 0; k < pre; k++) {
-                const V3 dd = vsub(v3(smp[3 * k], smp[3 * k + 1], smp[3 * k + 2]), avg);
-                double mx = dd.x;
-                if (dd.y > mx) mx = dd.y;
-                if (dd.z > mx) mx = dd.z;
-                variance += mx * mx;              // .max ** 2
-              }
-              variance /= (double)pre;
-              if (variance >= cam.variant_threshold) {
-                extra = true;
-                ntot = cam.max_samples;
-              }
-            }
-          }
-          j++;
-          if (j >= ntot) {                      // pixel done: Camera#render_at's result
-            if (extra) avg = vdiv(vadd(vsc(avg, (double)pre), cv), (double)cam.max_samples);
-            double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
-            o[0] = avg.x;
-            o[1] = avg.y;
-            o[2] = avg.z;
-            if (err) record_error(p.err, err, x, y, cam.width);
             mode = M_FETCH;
             break;
           }
+          started = true;
           sum = v3(0.0, 0.0, 0.0);
-          if (SRC == SRC_PIXELS) {
-            cur.ray = lens_ray(cam, tgt, x, y, j, p.seed);
-            sample = j;
+          if (SRC != SRC_RAYS) {
+            cur.ray = lens_ray(cam, tgt, x, y, sample, p.seed);
             if (COUNT) cnt[C_PRIMARY]++;
           } else {
             cur.ray.d = v3p(rays + 6 * row);
@@ -1087,20 +1070,32 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)f, 0u));
         if (k >= nwork) {
           mode = M_DONE;
-        } else if (SRC == SRC_PIXELS) {
-          const int tile = k >> 6, l = k & 63;
-          px_ = (tile % tiles_x) * 8 + (l & 7);
-          row = (tile / tiles_x) * 8 + (l >> 3);
+          if (RTX_STAMPS) w_dry = wall();
+        } else if (SRC != SRC_RAYS) {
+          if (RTX_STAMPS) {
+            const unsigned long long w = wall();
+            if (w_item && w - w_item > w_maxitem) w_maxitem = w - w_item;
+            w_item = w;
+          }
+          if (SRC == SRC_PIXELS) {
+            const int tile = k / (64 * pre), r = k - tile * (64 * pre);
+            const int l = r & 63;
+            sample = r >> 6;
+            px_ = (tile % tiles_x) * 8 + (l & 7);
+            row = (tile / tiles_x) * 8 + (l >> 3);
+          } else {
+            const int e = k / n_extra;
+            const int idx = p.extra_list[e];
+            sample = pre + (k - e * n_extra);
+            px_ = idx % p.nx;
+            row = idx / p.nx;
+          }
           if (px_ < p.nx && row < p.nrows) {
             y = row_to_y(p, row);
             if (y < cam.height) {
               x = p.x0 + px_;
               tgt = lens_target(cam, x, y);
-              ntot = pre;
-              extra = false;
-              avg = v3(0.0, 0.0, 0.0);
-              cv = avg;
-              j = -1;
+              started = false;
               err = 0;
               mode = M_NEED;
             }
@@ -1109,8 +1104,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
           row = k;
           x = keys[3 * row];
           y = keys[3 * row + 1];
-          ntot = 1;
-          j = -1;
+          started = false;
           err = 0;
           mode = M_NEED;
         }
@@ -1194,6 +1188,18 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
     mode = M_NEED;
     if (RTX_STAMPS) tD += stamp() - t0;
   }
+  if (RTX_STAMPS) {                            // lane utilisation: busy wall time vs the kernel's span
+    const unsigned long long w_end = wall();
+    atomicMin(&rtx_stamps[8], w_start);
+    atomicMax(&rtx_stamps[9], w_end);
+    atomicAdd(&rtx_stamps[10], w_dry - w_start);
+    atomicAdd(&rtx_stamps[11], 1ull);
+    atomicAdd(&rtx_stamps[12], w_end - w_start);
+    atomicMin(&rtx_stamps[13], w_dry);
+    atomicMax(&rtx_stamps[14], w_dry);
+    if (w_item && w_dry - w_item > w_maxitem) w_maxitem = w_dry - w_item;
+    atomicMax(&rtx_stamps[15], w_maxitem);
+  }
   if (RTX_STAMPS && (threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
     atomicAdd(&rtx_stamps[0], tA);
     atomicAdd(&rtx_stamps[1], tB);
@@ -1255,6 +1261,70 @@ __global__ __launch_bounds__(256) void k_path_trace(KParams p) {
   if (err) record_error(p.err, err, i, 0, 0x7fffffff);
 }
 
+// Camera#render_at's reduction (camera.rb:70-99) over the sample records of
+// k_render.  phase 0, every pixel of the region: mean of the pre_sample_times
+// colours (in sample order), the variance test, then either the pixel's result
+// or (variance >= threshold and max_sample_times > pre_sample_times) an entry in
+// p.extra_list for the SRC_EXTRA launch.  phase 1, every listed pixel: the
+// extra samples' sum in order and (avg * pre + cv) / max.  The first raise of a
+// pixel is the one of its lowest erring sample, as in the sequential loop.
+__global__ __launch_bounds__(256) void k_finalize(KParams p, int phase) {
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  int idx;
+  if (phase == 0) {
+    if (i >= p.nx * p.nrows) return;
+    idx = i;
+  } else {
+    if (i >= *p.extra_count) return;
+    idx = p.extra_list[i];
+  }
+  const int px_ = idx % p.nx, row = idx / p.nx;
+  const int y = row_to_y(p, row);
+  const CameraDev& cam = *p.cam;
+  if (y >= cam.height) return;                       // packed rows past the image bottom
+  const int x = p.x0 + px_;
+  const int pre = p.pre, ms = p.max_samples > p.pre ? p.max_samples : p.pre;
+  const double* q = p.samples + (size_t)idx * ms * 4;
+  uint32_t err = 0;
+  V3 avg = v3(0.0, 0.0, 0.0);
+  for (int j = 0; j < pre; j++) {
+    avg = vadd(avg, v3(q[4 * j], q[4 * j + 1], q[4 * j + 2]));
+    if (!err) err = (uint32_t)__builtin_bit_cast(uint64_t, q[4 * j + 3]);
+  }
+  avg = vdiv(avg, (double)pre);
+  if (phase == 0) {
+    double variance = 0.0;                           // camera.rb:80-85
+    for (int j = 0; j < pre; j++) {
+      const V3 dd = vsub(v3(q[4 * j], q[4 * j + 1], q[4 * j + 2]), avg);
+      double mx = dd.x;
+      if (dd.y > mx) mx = dd.y;
+      if (dd.z > mx) mx = dd.z;
+      variance += mx * mx;                           // .max ** 2
+    }
+    variance /= (double)pre;
+    if (variance >= cam.variant_threshold) {
+      if (p.max_samples > pre) {                     // more samples: the SRC_EXTRA launch
+        p.extra_list[atomicAdd(p.extra_count, 1)] = idx;
+        if (err) record_error(p.err, err, x, y, cam.width);
+        return;
+      }
+      avg = vdiv(vadd(vsc(avg, (double)pre), v3(0.0, 0.0, 0.0)), (double)p.max_samples);
+    }
+  } else {
+    V3 cv = v3(0.0, 0.0, 0.0);
+    for (int j = pre; j < p.max_samples; j++) {
+      cv = vadd(cv, v3(q[4 * j], q[4 * j + 1], q[4 * j + 2]));
+      if (!err) err = (uint32_t)__builtin_bit_cast(uint64_t, q[4 * j + 3]);
+    }
+    avg = vdiv(vadd(vsc(avg, (double)pre), cv), (double)p.max_samples);
+  }
+  double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
+  o[0] = avg.x;
+  o[1] = avg.y;
+  o[2] = avg.z;
+  if (err) record_error(p.err, err, x, y, cam.width);
+}
+
 // Camera#array_to_color (camera.rb:153-156) + PNG::Canvas#point over black.
 __global__ void k_quantize(const double* __restrict__ rgb, int w, int h, size_t stride, int blend,
                            uint8_t* __restrict__ out) {
@@ -1275,9 +1345,9 @@ __global__ void k_quantize(const double* __restrict__ rgb, int w, int h, size_t 
 
 // ----------------------------------------------------------------- launchers
 extern "C" int rtxdbg_read_stamps(unsigned long long* out, int reset) {   // diagnostic builds
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtx_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtx_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[16] = {0, 0, 0, 0, 0, 0, 0, 0, ~0ull, 0, 0, 0, 0, ~0ull, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(rtx_stamps), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;
@@ -1357,7 +1427,7 @@ template <bool COUNT, int MAXS, int SPH, int SRC>
 static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
   const size_t lds = lds_layout(p, SPH, BS);
-  auto kern = k_render<COUNT, MAXS, 16, RTX_WPS, SPH, SRC, BS>;
+  auto kern = k_render<COUNT, MAXS, RTX_WPS, SPH, SRC, BS>;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
@@ -1392,18 +1462,40 @@ static hipError_t launch_mode(const KParams& p, int mode, int nwork, hipStream_t
   return hipErrorInvalidValue;
 }
 
+template <int SRC>
+static hipError_t launch_src(const KParams& p, int mode, bool count, int maxs, int nwork, hipStream_t s) {
+#define RTX_L(M)                                                                                     \
+  if (maxs == M)                                                                                     \
+    return count ? launch_mode<true, M, SRC>(p, mode, nwork, s) : launch_mode<false, M, SRC>(p, mode, nwork, s);
+  RTX_L(8) RTX_L(16) RTX_L(32) RTX_L(64)
+#undef RTX_L
+  return hipErrorInvalidValue;
+}
+
+// Camera#render_at over a region: the pre samples of every pixel, the
+// reduction, then (only when max_sample_times > pre_sample_times) the extra
+// samples of the pixels whose variance asked for them and their reduction.
+// All on stream `s`; p.samples / extra_list / extra_count are the caller's.
 hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s) {
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   if (tiles == 0) return hipSuccess;
   if (count) mode = (mode == SPH_LIN_LDS || mode == SPH_BVH_LDS) ? SPH_LIN_LDS : SPH_LIN_SCALAR;
   mode = resolve_mode(p.scene, mode);
-  const int nwork = tiles * 64;
-#define RTX_L(M)                                                                                      \
-  if (maxs == M)                                                                                      \
-    return count ? launch_mode<true, M, SRC_PIXELS>(p, mode, nwork, s) : launch_mode<false, M, SRC_PIXELS>(p, mode, nwork, s);
-  RTX_L(8) RTX_L(16) RTX_L(32) RTX_L(64)
-#undef RTX_L
-  return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(p.extra_count, 0, sizeof(int32_t), s);
+  if (e == hipSuccess) e = launch_src<SRC_PIXELS>(p, mode, count, maxs, tiles * 64 * p.pre, s);
+  const int npx = p.nx * p.nrows;
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, s, p, 0);
+    e = hipGetLastError();
+  }
+  if (e != hipSuccess || p.max_samples <= p.pre) return e;
+  // extra samples: at most npx * (max - pre) items; the count is on the device
+  e = launch_src<SRC_EXTRA>(p, mode, count, maxs, npx * (p.max_samples - p.pre), s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, s, p, 1);
+    e = hipGetLastError();
+  }
+  return e;
 }
 
 hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s) {

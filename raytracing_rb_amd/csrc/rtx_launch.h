@@ -34,8 +34,16 @@ struct KParams {
   int32_t lds_leaf, lds_stack, lds_cov, lds_items;
   int32_t stk_slots;               // ray-stack entries per lane kept in LDS (set by the launcher)
   int32_t stk_slots_max;           // cap (option "lds_stack"; the stack bucket by default)
-  double* stk_glb;                 // per-lane regions: MAXS * 12 doubles of ray stack + 3 * 16 sample colours
+  double* stk_glb;                 // per-lane regions: MAXS * 12 doubles of ray stack
   int32_t stk_glb_lanes;           // lanes the buffer holds (the launcher caps the grid to it)
+  // Camera#render_at in two steps (launch_render): per (pixel, sample) records
+  // of 4 doubles {r, g, b, first raise} at samples[(pixel * max(pre, max) + j) * 4]
+  // (pixel = row * nx + column of the region), and the list of pixels whose
+  // variance asks for the extra samples.
+  int32_t pre, max_samples;        // camera pre_sample_times / max_sample_times
+  double* samples;
+  int32_t* extra_list;             // nx * nrows entries
+  int32_t* extra_count;
 };
 
 // Where the sphere walk reads its records:
