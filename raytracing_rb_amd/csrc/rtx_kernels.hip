@@ -79,6 +79,9 @@ __device__ __forceinline__ const RTX_CONST T* cptr(const T* p) {
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2 };
+#ifndef RTX_CLAIM_MAX
+#define RTX_CLAIM_MAX 32     // cap on the items a wave claims beyond its lanes' need (0: claim per refill; 128: C2 +9 %, 512: C2 x2.1 — expensive tiles pile up in one wave)
+#endif
 
 // Diagnostic build only (-DRTX_STAMPS=1): per-wave shader-clock time spent in
 // each phase of the lane state machine, summed into rtx_stamps[] (read with
@@ -989,6 +992,8 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   uint32_t err = 0;
   V3 sum = v3(0.0, 0.0, 0.0), avg = sum;
   bool started = false;              // the current item's tree has begun
+  int wbase = 0, wlim = 0;           // the wave's claimed, not yet assigned items (wave-uniform)
+  const int nwaves = (int)gridDim.x * (BS / 64);
   int sample = 0;                    // camera sample of the item = RNG key of its tree
   Item cur;
   bool have = false;                 // `cur` holds a ray not yet processed
@@ -1001,7 +1006,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   V3 qo = avg, qd = avg, qL = avg;
   double qrad = 0.0;
 
-  unsigned long long tA = 0, tB = 0, tC = 0, tD = 0, iters = 0, t0 = 0, t1;
+  unsigned long long tA = 0, tB = 0, tC = 0, tD = 0, tR = 0, iters = 0, t0 = 0, t1;
   const unsigned long long w_start = wall();
   unsigned long long w_dry = 0;                // when this lane found the work pool empty
   unsigned long long w_item = 0, w_maxitem = 0; // start of the current item, longest item
@@ -1058,16 +1063,34 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
         best = S.max_distance;
         besti = -1;
       }
-      // ---- refill: lanes whose item is finished take the next ones
+      // ---- refill: lanes whose item is finished take the next ones, first
+      // from the wave's claimed range [wbase, wlim), then from a new claim
       const uint64_t f = __ballot(mode == M_FETCH);
       if (!f) break;
-      const int src = __builtin_ctzll(f);
-      int base = 0;
-      if ((int)__lane_id() == src) base = atomicAdd(p.work, __popcll(f));
-      base = __builtin_amdgcn_readlane(base, src);
+      const int need = __popcll(f), left = wlim - wbase;
+      int base = wbase;                        // items of rank >= left come from `fresh`
+      int fresh = 0;
+      if (left < need) {
+        // guided self-scheduling: besides what the lanes need now, claim up to
+        // 1/(4 x waves) of what the last claim saw remaining (<= 128), so a
+        // wave pays the atomic's round trip once per several refills and the
+        // items held privately stay a small share of the pool at every point
+        int extra = (nwork - wlim) / (4 * nwaves);
+        extra = extra < 0 ? 0 : (extra > RTX_CLAIM_MAX ? RTX_CLAIM_MAX : extra);
+        const int claim = need - left + extra;
+        const int src = __builtin_ctzll(f);
+        const unsigned long long t_r = RTX_STAMPS == 1 ? stamp() : 0;
+        if ((int)__lane_id() == src) fresh = atomicAdd(p.work, claim);
+        fresh = __builtin_amdgcn_readlane(fresh, src);
+        if (RTX_STAMPS == 1) tR += stamp() - t_r;
+        wbase = fresh + (need - left);
+        wlim = fresh + claim;
+      } else {
+        wbase += need;
+      }
       if (mode == M_FETCH) {
-        const int k = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(f >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)f, 0u));
+        const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(f >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)f, 0u));
+        const int k = r < left ? base + r : fresh + (r - left);
         if (k >= nwork) {
           mode = M_DONE;
           if (RTX_STAMPS) w_dry = wall();
@@ -1207,6 +1230,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
     atomicAdd(&rtx_stamps[3], tD);
     atomicAdd(&rtx_stamps[4], iters);
     atomicAdd(&rtx_stamps[5], 1ull);
+    if (RTX_STAMPS == 1) atomicAdd(&rtx_stamps[6], tR);
   }
 
   if (COUNT)

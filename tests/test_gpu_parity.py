@@ -53,6 +53,14 @@ def test_gpu_matches_golden(gpu, name):
     ("c0_world.yml", "camera.yml", dict(width=96, height=54)),
     ("c2_world.yml", "c2_camera.yml", dict(width=160, height=90)),
     ("mix_world.yml", "mix_camera.yml", dict(width=64, height=36)),
+    # render_at corner cases: max < pre (a high variance rescales avg * pre / max,
+    # camera.rb:86-97), every pixel re-sampled (threshold 0), no extra samples
+    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, pre_sample_times=3, max_sample_times=2,
+                                             variant_threshold=0.0)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, pre_sample_times=2, max_sample_times=5,
+                                             variant_threshold=0.0)),
+    ("c2_world.yml", "c2_camera.yml", dict(width=48, height=27, pre_sample_times=3, max_sample_times=7,
+                                           variant_threshold=1e9)),
 ])
 def test_gpu_matches_oracle(gpu, world, camera, ov):
     from oracle.c_oracle import Oracle

@@ -1,4 +1,5 @@
 set -o pipefail
 O=gpurun_out/s18; mkdir -p $O
-timeout -k 10 300 python tools/variants.py time --scene c2 --rounds 3 > $O/variants_c2.log 2>&1
+timeout -k 10 300 python tools/variants.py time --scene c2 --rounds 3 > $O/variants_c2.log 2>&1 &&
+timeout -k 10 500 python tools/variants.py time --scene c4 --rounds 1 --reps 2 > $O/variants_c4.log 2>&1
 echo rc=$?

@@ -25,7 +25,7 @@ tot = tA + tB + tC + tD
 print("waves %d  iterations/wave %.1f" % (waves, iters / waves))
 for n, v in (("A fetch/pop/lens/highlight", tA), ("B query (object walk)", tB), ("C hit_info/lights", tC), ("D shade_finish", tD)):
     print("%-28s %5.1f%%  %.0f cycles/wave  %.0f cycles/iteration" % (n, 100 * v / tot, v / waves, v / iters))
-print("exact sphere tests: per wave-iteration %.2f (any lane), per lane-query %.3f" % (wexact / iters, lexact / (iters * 64)))
+print("of A: work refill (global atomic) %.1f%% of all, %.0f cycles/iteration" % (100 * wexact / tot, wexact / iters))
 span = w1 - w0
 print("kernel span %.3f ms (100 MHz clock); lanes %d" % (span / 1e5, lanes))
 print("lane busy (start -> pool empty) %.1f%% of lanes x span; lane resident %.1f%%" % (
