@@ -237,7 +237,8 @@ rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
          2 always; every choice renders the same bits), "bvh_min" [32], "bvh_sah" (1 [default] binned-SAH hierarchy
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
          staging, 1 scalar loads), "lds_stack" (ray-stack entries per lane kept in LDS,
-         -1 = as many as fit), "force_stack" (per-lane ray-stack bucket). */
+         -1 = as many as fit), "force_stack" (per-lane ray-stack bucket), "postpone" (hierarchy walks
+         still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

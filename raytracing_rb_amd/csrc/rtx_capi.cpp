@@ -35,6 +35,9 @@ using namespace rtx;
 #endif
 
 constexpr unsigned RTX_WORK_RING = 256;
+#ifndef RTX_POSTPONE_NODES
+#define RTX_POSTPONE_NODES 64                 // hierarchy nodes from which walks are postponed by default
+#endif
 
 struct rtx_context {
   int device = 0;
@@ -62,6 +65,7 @@ struct rtx_context {
   int64_t opt_bvh_sah = RTX_BVH_SAH;  // hierarchy splits: 1 binned SAH, 0 median (applies at the next upload)
   int64_t opt_bvh_min = 32;         // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
   int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
+  int64_t opt_postpone = -1;         // query_bvh postponing threshold in lanes (-1: auto by hierarchy size)
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
 };
 
@@ -361,6 +365,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "bvh_min")) {           // sphere count from which bvh=1 uses the hierarchy
     if (value < 0) return fail(c, RTX_EINVAL, "bvh_min must be >= 0");
     c->opt_bvh_min = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "postpone")) {          // lanes below which hierarchy walks are postponed (-1 auto, 0 never)
+    if (value < -1 || value > 64) return fail(c, RTX_EINVAL, "postpone must be in [-1, 64]");
+    c->opt_postpone = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lds_stack")) {         // ray-stack entries per lane kept in LDS (-1: as many as fit)
@@ -676,6 +685,9 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
   p.stk_slots_max = c->opt_lds_stack < 0 ? 64 : (int32_t)c->opt_lds_stack;
   p.pre = c->cam.pre;
   p.max_samples = c->cam.max_samples;
+  // Postponing long walks pays when walks are long (C4, 341 nodes: 550 -> 507 ms)
+  // and costs when they are short (C2, a few nodes: 9.0 -> 9.3 ms).
+  p.postpone = c->opt_postpone >= 0 ? (int32_t)c->opt_postpone : (c->scene.n_nodes >= RTX_POSTPONE_NODES ? 16 : 0);
   return RTX_OK;
 }
 

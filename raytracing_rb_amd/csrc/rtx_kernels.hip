@@ -433,10 +433,18 @@ __device__ __forceinline__ void push_cover(int* ci, double* cv, int& n, bool& ov
   n++;
 }
 
-template <int BS, typename NP, typename LP>
-__device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf4, int* stk, int* ci, double* cv,
+// Resumable: a lane whose walk is still running when fewer than `postpone`
+// lanes of its wave are is postponed (returns false) with its walk in
+// ref / sp (+ the LDS stack) / ncov / ovf (+ the LDS cover list) and best /
+// besti / bhit / bin, and continues where it stopped at the next call with
+// resume = true; meanwhile the wave's other lanes shade and start new
+// queries instead of idling.  Every lane visits the same nodes and leaves in
+// the same order either way, so the result is unchanged.
+template <int BS, bool PP, typename NP, typename LP>
+__device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4, int* stk, int* ci, double* cv,
                                           bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
-                                          V3& bhit, bool& bin, double& total, uint32_t& err) {
+                                          V3& bhit, bool& bin, double& total, uint32_t& err, int& ref, int& sp,
+                                          int& ncov, bool& ovf, bool resume, int postpone) {
   const double r = vr(d);
   const double r2 = r * r;                        // front.r2
   V3 dn = d;
@@ -465,17 +473,21 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf4,
     // no float32 cull is valid for this ray: the ordered linear walk (same result)
     if (!ext) total = 1.0;
     query<false>(S, cptr(S.sph32), ext, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
-    return;
+    return true;
   }
   const float rf = (float)r;
   // far bound on the ray parameter: EXTEND the current best hit, SHADOW the light
   float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + mS / rf;
-  int ncov = 0;
-  bool ovf = false;
+  if (!resume) {
+    ncov = 0;
+    ovf = false;
+    ref = S.bvh_root;
+    sp = 0;
+  }
 
   // planes and boxes first, in run order (their order does not matter either)
   const RTX_CONST Run* runs = cptr(S.runs);
-  const int n_runs = uni(S.n_runs);
+  const int n_runs = resume ? 0 : uni(S.n_runs);
   for (int ri = 0; ri < n_runs; ri++) {
     const int type = uni(runs[ri].type);
     if (type == OBJ_SPHERE) continue;
@@ -505,8 +517,6 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf4,
     }
   }
 
-  int ref = S.bvh_root;
-  int sp = 0;
   while (ref != BVH_NONE) {
     // ---- inner nodes: slab-test the four child boxes, descend into the nearest
     while (ref >= 0 && ref != BVH_NONE) {
@@ -588,6 +598,7 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf4,
       }
     }
     ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
+    if (PP && __popcll(__ballot(ref != BVH_NONE)) < postpone && ref != BVH_NONE) return false;
   }
   if (!ext) {
     total = 1.0;
@@ -598,6 +609,7 @@ __device__ __forceinline__ void query_bvh(const SceneDev& S, NP nodes, LP leaf4,
       for (int k = 0; k < ncov; k++) total -= cv[k * BS];
     }
   }
+  return true;
 }
 
 // ----------------------------------------------------------------- shading
@@ -934,7 +946,7 @@ __device__ __forceinline__ int row_to_y(const KParams& p, int row) {
 // pixels k_finalize listed.  SRC_RAYS: one lane per explicit ray running
 // RayTracer#trace_sync (rtx_trace).  SPH: where the sphere walk reads its
 // records (SphMode, rtx_launch.h).  BS: threads per workgroup.
-template <bool COUNT, int MAXS, int WPS, int SPH, int SRC, int BS>
+template <bool COUNT, int MAXS, int WPS, int SPH, int SRC, int BS, bool PP>
 __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   const double* __restrict__ rays = p.rays;
   const int32_t* __restrict__ keys = p.keys;
@@ -1005,6 +1017,8 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   V3 hit = avg, delta = avg, n = avg, nn = avg, lc = avg;
   V3 qo = avg, qd = avg, qL = avg;
   double qrad = 0.0;
+  int q_ref = BVH_NONE, q_sp = 0, q_ncov = 0;   // a postponed hierarchy walk (query_bvh)
+  bool q_ovf = false, q_resume = false;
 
   unsigned long long tA = 0, tB = 0, tC = 0, tD = 0, tR = 0, iters = 0, t0 = 0, t1;
   const unsigned long long w_start = wall();
@@ -1147,16 +1161,20 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
     else if (SPH == SPH_LIN_SCALAR)
       query<COUNT>(S, sph_k, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, cnt);
     else if (SPH == SPH_BVH_LDS)
-      query_bvh<BS>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
-                    stk, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err);
+      q_resume = !query_bvh<BS, PP>(S, reinterpret_cast<const Bvh4Node*>(lds),
+                                reinterpret_cast<const float4*>(lds + p.lds_leaf), stk, cov_i, cov_v,
+                                mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, q_ref, q_sp,
+                                q_ncov, q_ovf, q_resume, p.postpone);
     else
-      query_bvh<BS>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), stk, cov_i, cov_v, mode == M_EXTEND, qo, qd, qL, qrad, best, besti,
-                    hit, hin, total, err);
+      q_resume = !query_bvh<BS, PP>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), stk, cov_i, cov_v,
+                                mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, q_ref, q_sp,
+                                q_ncov, q_ovf, q_resume, p.postpone);
     if (RTX_STAMPS) {
       t1 = stamp();
       tB += t1 - t0;
       t0 = t1;
     }
+    if (PP && q_resume) continue;            // walk postponed: resumed at the next B
 
     // ---- C: consume the query result
     if (mode == M_EXTEND) {
@@ -1447,11 +1465,11 @@ static size_t lds_layout(KParams& p, int mode, int bs) {
 // Persistent launch: as many workgroups as can be resident at once (the
 // occupancy API; an over-estimate only leaves blocks that start after the
 // pool is empty and exit at once), never more than the work needs.
-template <bool COUNT, int MAXS, int SPH, int SRC>
+template <bool COUNT, int MAXS, int SPH, int SRC, bool PP = false>
 static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
   const size_t lds = lds_layout(p, SPH, BS);
-  auto kern = k_render<COUNT, MAXS, RTX_WPS, SPH, SRC, BS>;
+  auto kern = k_render<COUNT, MAXS, RTX_WPS, SPH, SRC, BS, PP>;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
@@ -1477,9 +1495,11 @@ static hipError_t launch_mode(const KParams& p, int mode, int nwork, hipStream_t
     case SPH_LIN_LDS: return launch_one<COUNT, MAXS, SPH_LIN_LDS, SRC>(p, nwork, s);
     case SPH_LIN_SCALAR: return launch_one<COUNT, MAXS, SPH_LIN_SCALAR, SRC>(p, nwork, s);
     case SPH_BVH_LDS:
+      if (!COUNT && p.postpone > 0) return launch_one<false, MAXS, SPH_BVH_LDS, SRC, true>(p, nwork, s);
       if (!COUNT) return launch_one<false, MAXS, SPH_BVH_LDS, SRC>(p, nwork, s);
       break;
     case SPH_BVH_GLOBAL:
+      if (!COUNT && p.postpone > 0) return launch_one<false, MAXS, SPH_BVH_GLOBAL, SRC, true>(p, nwork, s);
       if (!COUNT) return launch_one<false, MAXS, SPH_BVH_GLOBAL, SRC>(p, nwork, s);
       break;
   }

@@ -41,6 +41,7 @@ struct KParams {
   // (pixel = row * nx + column of the region), and the list of pixels whose
   // variance asks for the extra samples.
   int32_t pre, max_samples;        // camera pre_sample_times / max_sample_times
+  int32_t postpone;                // query_bvh: postpone walks when fewer lanes than this still walk (0: never)
   double* samples;
   int32_t* extra_list;             // nx * nrows entries
   int32_t* extra_count;
