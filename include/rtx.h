@@ -238,7 +238,9 @@ rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
          staging, 1 scalar loads), "lds_stack" (ray-stack entries per lane kept in LDS,
          -1 = as many as fit), "force_stack" (per-lane ray-stack bucket), "postpone" (hierarchy walks
-         still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never). */
+         still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never), "tile_order" (1 expensive
+         8x8 tiles first by a primary-hit probe, 0 row-major, -1 [default] = 1 up to 512 spheres; the order
+         changes no bit). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

@@ -36,6 +36,7 @@ using namespace rtx;
 
 constexpr unsigned RTX_WORK_RING = 256;
 #ifndef RTX_POSTPONE_NODES
+#define RTX_TILE_ORDER_SPHERES 512             // auto tile_order up to this many spheres
 #define RTX_POSTPONE_NODES 64                 // hierarchy nodes from which walks are postponed by default
 #endif
 
@@ -66,6 +67,7 @@ struct rtx_context {
   int64_t opt_bvh_min = 32;         // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
   int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
   int64_t opt_postpone = -1;         // query_bvh postponing threshold in lanes (-1: auto by hierarchy size)
+  int64_t opt_tile_order = -1;       // 1: expensive tiles first (k_tile_cost/k_tile_sort), 0: natural order, -1: auto
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
 };
 
@@ -375,6 +377,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lds_stack")) {         // ray-stack entries per lane kept in LDS (-1: as many as fit)
     if (value < -1 || value > 64) return fail(c, RTX_EINVAL, "lds_stack must be in [-1, 64]");
     c->opt_lds_stack = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "tile_order")) {        // 1: expensive tiles first; 0: natural (row-major) tile order
+    if (value < -1 || value > 1) return fail(c, RTX_EINVAL, "tile_order must be -1, 0 or 1");
+    c->opt_tile_order = value;
     return RTX_OK;
   }
   if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads
@@ -701,10 +708,17 @@ static rtx_status render_region(rtx_context* c, KParams& p, bool count, int maxs
   const size_t ms = (size_t)std::max(p.pre, p.max_samples);
   const size_t smp_bytes = npx * ms * 4 * sizeof(double);
   void* buf = nullptr;
-  HIPCHK(c, hipMallocAsync(&buf, smp_bytes + (npx + 64) * sizeof(int32_t), stream));
+  const size_t tiles = (size_t)((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
+  HIPCHK(c, hipMallocAsync(&buf, smp_bytes + (npx + 64 + 2 * tiles) * sizeof(int32_t), stream));
   p.samples = (double*)buf;
   p.extra_count = (int32_t*)((char*)buf + smp_bytes);
   p.extra_list = p.extra_count + 64;
+  p.tile_cls = p.extra_list + npx;
+  // Auto: the probe is an ordered linear walk, cheap for a few hundred spheres
+  // (C2: 9.2 -> 8.9 ms); on C4 (4,096 spheres) it costs 2.2 ms and the order
+  // gains nothing (the frame is 500 ms of evenly expensive tiles).
+  const bool order = c->opt_tile_order > 0 || (c->opt_tile_order < 0 && c->scene.n_sphere <= RTX_TILE_ORDER_SPHERES);
+  p.tile_order = order ? p.tile_cls + tiles : nullptr;
   const hipError_t e = launch_render(p, sph_mode(c), count, maxs, stream);
   const hipError_t f = hipFreeAsync(buf, stream);
   HIPCHK(c, e);

@@ -45,6 +45,9 @@ struct KParams {
   double* samples;
   int32_t* extra_list;             // nx * nrows entries
   int32_t* extra_count;
+  // SRC_PIXELS: tile visiting order (k_tile_cost + k_tile_sort), null = natural
+  int32_t* tile_order;
+  int32_t* tile_cls;
 };
 
 // Where the sphere walk reads its records:

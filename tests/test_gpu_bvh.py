@@ -175,3 +175,31 @@ def test_bvh_edge_scenes_match_oracle(gpu, tmp_path):
         sd, cd = _scene(world, "c2_camera.yml", width=48, height=27, pre_sample_times=2, max_sample_times=2)
         ref, st, rc = Oracle(sd, cd).render(seed=1)
         _check(_render(sd, cd, BVH_ALWAYS), ref, st == 0)
+
+
+# ---------------------------------------------------------------- tile order
+@pytest.mark.parametrize("world,camera,ov", [
+    ("c2_world.yml", "c2_camera.yml", dict(width=333, height=187)),          # ragged 8x8 tiles
+    ("mix_world.yml", "mix_camera.yml", dict(width=96, height=54, pre_sample_times=2, max_sample_times=5)),
+])
+def test_tile_order_changes_no_bit(gpu, world, camera, ov):
+    """Expensive tiles first (k_tile_cost + k_tile_sort) only
+    reorders work items; each item writes its own sample record."""
+    from raytracing_rb_amd.runtime import Renderer
+    sd, cd = _scene(world, camera, **ov)
+    fbs = []
+    for order in (0, 1, -1):
+        r = Renderer(sd, cd, device=0)
+        r.set_option("tile_order", order)
+        fbs.append(r.render(seed=3))
+        r.close()
+    assert _same_bits(fbs[0], fbs[1]) and _same_bits(fbs[0], fbs[2])
+
+
+def test_tile_order_option_range(gpu):
+    from raytracing_rb_amd.runtime import Renderer
+    sd, cd = _scene("c1_world.yml", "c1_camera.yml", width=16, height=8)
+    r = Renderer(sd, cd, device=0)
+    with pytest.raises(Exception):
+        r.set_option("tile_order", 2)
+    r.close()
