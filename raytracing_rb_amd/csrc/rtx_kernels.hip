@@ -80,12 +80,15 @@ __device__ __forceinline__ const RTX_CONST T* cptr(const T* p) {
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2 };
 #ifndef RTX_CLAIM_MAX
-#define RTX_CLAIM_MAX 32     // cap on the items a wave claims beyond its lanes' need (0: claim per refill; 128: C2 +9 %, 512: C2 x2.1 — expensive tiles pile up in one wave)
+#define RTX_CLAIM_MAX 64     // cap on the items a wave claims beyond its lanes' need (with expensive tiles first + Morton items: 32: C2 8.68 ms, 64: 8.30 ms, 96: 9.13 ms, 128: 9.58 ms — expensive tiles pile up in one wave)
 #endif
 
 // Diagnostic build only (-DRTX_STAMPS=1): per-wave shader-clock time spent in
 // each phase of the lane state machine, summed into rtx_stamps[] (read with
 // rtxdbg_read_stamps).  The shipped library is built without it.
+#ifndef RTX_ITEM_ORDER
+#define RTX_ITEM_ORDER 1     // SRC_PIXELS items within a tile: 1 (pixel Morton, sample; C2 8.75 -> 8.65 ms, C4 505 -> 495 ms), 0 (sample, pixel row-major)
+#endif
 #ifndef RTX_DIAG_NOEXACT
 #define RTX_DIAG_NOEXACT 0
 #endif
@@ -1117,10 +1120,19 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
           if (SRC == SRC_PIXELS) {
             const int slot = k / (64 * pre), r = k - slot * (64 * pre);
             const int tile = p.tile_order ? p.tile_order[slot] : slot;   // expensive tiles first
+#if RTX_ITEM_ORDER == 1
+            // (pixel in Morton order, sample): a wave's 64 items are the
+            // pre_sample_times samples of a compact block of pixels
+            const int l = r / pre;
+            sample = r - l * pre;
+            px_ = (tile % tiles_x) * 8 + ((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));
+            row = (tile / tiles_x) * 8 + (((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4));
+#else
             const int l = r & 63;
             sample = r >> 6;
             px_ = (tile % tiles_x) * 8 + (l & 7);
             row = (tile / tiles_x) * 8 + (l >> 3);
+#endif
           } else {
             const int e = k / n_extra;
             const int idx = p.extra_list[e];
