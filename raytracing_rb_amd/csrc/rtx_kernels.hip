@@ -1393,6 +1393,7 @@ __global__ __launch_bounds__(256) void k_finalize(KParams p, int phase) {
 // class is the sum, clamped to TILE_CLASSES - 1.  (Following the mirror
 // bounce as well measured no better on C2.)
 constexpr int TILE_CLASSES = 16;
+constexpr int TILE_SORT_LDS = 64 * 1024;          // k_tile_sort stages up to this many classes in LDS
 __global__ __launch_bounds__(256) void k_tile_cost(KParams p, int32_t* cls) {
   const int i = blockIdx.x * 256 + (int)threadIdx.x;
   const int tiles_x = (p.nx + 7) >> 3;
@@ -1442,8 +1443,13 @@ __global__ __launch_bounds__(1024) void k_tile_sort(KParams p, const int32_t* cl
   const int st = RTX_TILE_SORT_STRIDED ? 1024 : 1;
   __shared__ int cnt[TILE_CLASSES * 1024];        // [class desc][thread]
   __shared__ int part[1024];
+  __shared__ uint8_t cl8[TILE_SORT_LDS];        // the classes, staged with coalesced reads when they fit
+  const bool staged = tiles <= TILE_SORT_LDS;
+  if (staged)
+    for (int k = t; k < tiles; k += 1024) cl8[k] = (uint8_t)cls[k];
   for (int c = 0; c < TILE_CLASSES; c++) cnt[c * 1024 + t] = 0;
-  for (int k = t0; k < t1; k += st) cnt[(TILE_CLASSES - 1 - cls[k]) * 1024 + t]++;
+  __syncthreads();
+  for (int k = t0; k < t1; k += st) cnt[(TILE_CLASSES - 1 - (staged ? cl8[k] : cls[k])) * 1024 + t]++;
   __syncthreads();
   // exclusive scan of the 16384 counts: thread t scans entries [16t, 16t+16)
   int run = 0;
@@ -1463,7 +1469,7 @@ __global__ __launch_bounds__(1024) void k_tile_sort(KParams p, const int32_t* cl
   const int base = t > 0 ? part[t - 1] : 0;
   for (int j = 0; j < TILE_CLASSES; j++) cnt[t * TILE_CLASSES + j] += base;
   __syncthreads();
-  for (int k = t0; k < t1; k += st) order[cnt[(TILE_CLASSES - 1 - cls[k]) * 1024 + t]++] = k;
+  for (int k = t0; k < t1; k += st) order[cnt[(TILE_CLASSES - 1 - (staged ? cl8[k] : cls[k])) * 1024 + t]++] = k;
 }
 
 // Camera#array_to_color (camera.rb:153-156) + PNG::Canvas#point over black.
