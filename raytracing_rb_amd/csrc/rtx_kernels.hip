@@ -86,6 +86,12 @@ enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2 };
 // Diagnostic build only (-DRTX_STAMPS=1): per-wave shader-clock time spent in
 // each phase of the lane state machine, summed into rtx_stamps[] (read with
 // rtxdbg_read_stamps).  The shipped library is built without it.
+#ifndef RTX_CLAIM_DIV
+#define RTX_CLAIM_DIV 2      // a claim's extra items: at most remaining / (RTX_CLAIM_DIV x waves) (C2: 2: 8.27 ms, 4: 8.35-8.48 ms, 8: 8.37 ms)
+#endif
+#ifndef RTX_CLAIM_ALIGN
+#define RTX_CLAIM_ALIGN 1    // claims rounded up to a multiple of this (every claimed range then starts aligned; 64: C2 9.2 ms, worse)
+#endif
 #ifndef RTX_ITEM_ORDER
 #define RTX_ITEM_ORDER 1     // SRC_PIXELS items within a tile: 1 (pixel Morton, sample; C2 8.75 -> 8.65 ms, C4 505 -> 495 ms), 0 (sample, pixel row-major)
 #endif
@@ -1092,9 +1098,10 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
         // 1/(4 x waves) of what the last claim saw remaining (<= 128), so a
         // wave pays the atomic's round trip once per several refills and the
         // items held privately stay a small share of the pool at every point
-        int extra = (nwork - wlim) / (4 * nwaves);
+        int extra = (nwork - wlim) / (RTX_CLAIM_DIV * nwaves);
         extra = extra < 0 ? 0 : (extra > RTX_CLAIM_MAX ? RTX_CLAIM_MAX : extra);
-        const int claim = need - left + extra;
+        int claim = need - left + extra;
+        if (RTX_CLAIM_ALIGN > 1) claim = (claim + RTX_CLAIM_ALIGN - 1) / RTX_CLAIM_ALIGN * RTX_CLAIM_ALIGN;
         const int src = __builtin_ctzll(f);
         const unsigned long long t_r = RTX_STAMPS == 1 ? stamp() : 0;
         if ((int)__lane_id() == src) fresh = atomicAdd(p.work, claim);

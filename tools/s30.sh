@@ -1,0 +1,7 @@
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/s30; mkdir -p $O
+timeout -k 10 400 python tools/variants.py time --scene c2 --rounds 3 --reps 5 > $O/variants_c2.log 2>&1 &&
+
+timeout -k 10 600 python tools/variants.py time --scene c4 --rounds 1 --reps 1 > $O/variants_c4.log 2>&1
+echo rc=$?
