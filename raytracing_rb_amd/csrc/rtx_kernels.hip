@@ -92,6 +92,9 @@ enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2 };
 #ifndef RTX_CLAIM_ALIGN
 #define RTX_CLAIM_ALIGN 1    // claims rounded up to a multiple of this (every claimed range then starts aligned; 64: C2 9.2 ms, worse)
 #endif
+#ifndef RTX_PROBE_W
+#define RTX_PROBE_W 0        // k_tile_cost hit weights: 0 (1, +1 reflective, +3 refractive), 1 (1, +1/+2 by reflectance, +6 refractive)
+#endif
 #ifndef RTX_ITEM_ORDER
 #define RTX_ITEM_ORDER 1     // SRC_PIXELS items within a tile: 1 (pixel Morton, sample; C2 8.75 -> 8.65 ms, C4 505 -> 495 ms), 0 (sample, pixel row-major)
 #endif
@@ -1424,7 +1427,16 @@ __global__ __launch_bounds__(256) void k_tile_cost(KParams p, int32_t* cls) {
       query<false>(S, cptr(S.sph32), true, r.o, r.d, hit, 0.0, best, besti, hit, hin, total, err, nullptr);
       if (besti >= 0) {
         const Material& m = S.mat[besti];
+#if RTX_PROBE_W == 1
+        const double ra = vr(v3p(m.refl_att));
+        w = 1 + (ra >= 0.0001 ? (ra >= 0.5 ? 2 : 1) : 0) + (m.has_rr && vr(v3p(m.refr_att)) >= 0.0001 ? 6 : 0);
+#elif RTX_PROBE_W == 2
+        w = 1 + (vr(v3p(m.refl_att)) >= 0.0001 ? 1 : 0) + (m.has_rr && vr(v3p(m.refr_att)) >= 0.0001 ? 2 : 0);
+#elif RTX_PROBE_W == 3
+        w = (m.has_rr && vr(v3p(m.refr_att)) >= 0.0001) ? 2 : 1;
+#else
         w = 1 + (vr(v3p(m.refl_att)) >= 0.0001 ? 1 : 0) + (m.has_rr && vr(v3p(m.refr_att)) >= 0.0001 ? 3 : 0);
+#endif
       }
     }
   }
