@@ -1352,9 +1352,21 @@ __global__ __launch_bounds__(256) void k_finalize(KParams p, int phase) {
   const double* q = p.samples + (size_t)idx * ms * 4;
   uint32_t err = 0;
   V3 avg = v3(0.0, 0.0, 0.0);
-  for (int j = 0; j < pre; j++) {
-    avg = vadd(avg, v3(q[4 * j], q[4 * j + 1], q[4 * j + 2]));
-    if (!err) err = (uint32_t)__builtin_bit_cast(uint64_t, q[4 * j + 3]);
+  if (phase == 0 && pre == 4) {                      // the common 4x case: all 8 loads in flight at once
+    const double2* q2 = reinterpret_cast<const double2*>(q);
+    double2 a[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = q2[k];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      avg = vadd(avg, v3(a[2 * j].x, a[2 * j].y, a[2 * j + 1].x));
+      if (!err) err = (uint32_t)__builtin_bit_cast(uint64_t, a[2 * j + 1].y);
+    }
+  } else {
+    for (int j = 0; j < pre; j++) {
+      avg = vadd(avg, v3(q[4 * j], q[4 * j + 1], q[4 * j + 2]));
+      if (!err) err = (uint32_t)__builtin_bit_cast(uint64_t, q[4 * j + 3]);
+    }
   }
   avg = vdiv(avg, (double)pre);
   if (phase == 0) {
