@@ -39,11 +39,11 @@ def main():
         ov.update(pre_sample_times=a.spp, max_sample_times=a.spp)
     sd, cd = config.load_scene(os.path.join(ROOT, "scenes", a.scene + "_world.yml"),
                                os.path.join(ROOT, "scenes", a.scene + "_camera.yml"), camera_overrides=ov)
-    r = Renderer(sd, cd)
     out = torch.empty((cd.height, cd.width, 3), dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream()
     for o in (a.opts or ["{}"]):
         opts = json.loads(o)
+        r = Renderer(sd, cd)              # a fresh context per option set: options do not carry over
         for k, v in opts.items():
             r.set_option(k, v)
         r.render_device(out.data_ptr(), stream=s.cuda_stream)
@@ -57,6 +57,7 @@ def main():
             e1.synchronize()
             ts.append(e0.elapsed_time(e1))
         r.sync(s.cuda_stream)
+        r.close()
         ts.sort()
         sha = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
         print("%-8s %-40s min %9.3f ms  median %9.3f ms  %8.2f Mpix/s  sha %s" % (
