@@ -2,23 +2,37 @@
 """Headline benchmark: Mpixels/s at 1920x1080, 4x AA, depth 5, 64 spheres (C2).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+                    [--workload c2|c4] [--emulate-rank k/N] [--no-projection]
 
 One step = one complete C2 frame (BASELINE.json configs[2]): 1920x1080 pixels,
 Camera#render_at with pre = max = 4 samples, trace_depth 5, 64 spheres + ground
 plane + area light, counter RNG seed 1, scene resident in HBM before timing.
-For N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL) the frame
-is split into 8-row tiles dealt round-robin over the ranks and gathered to rank
-0 with one RCCL gather per frame (strong scaling of the C3 configuration).
+
+Multi-GPU (C3, BASELINE.json configs[3]): one process per GPU.  Under
+torch.distributed.run (WORLD_SIZE set) this process is one rank; with
+`--gpus N > 1` and no WORLD_SIZE it launches the N ranks itself
+(torch.distributed.run as a child process, started before this process makes
+any GPU call) and exits with their status.  A world size that differs from
+--gpus is an error, never a silent 1-GPU run.  The frame is split into 8-row
+tiles dealt round-robin over the ranks (rtx_render_tiles_device, the
+replacement of camera.rb:41-68 / fork_jobs.rb:1-33) and gathered to rank 0
+with ONE RCCL gather per frame: strong scaling of the C2 frame.
+
+`--emulate-rank k/N` times rank k's share of an N-rank frame on one GPU;
+the default 1-GPU run also reports `projection`: every rank's share for
+N = 2, 4, 8 timed on this GPU, the max over ranks, and the projected speedup.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
-`roofline` (FP64: counted algorithmic ops / kernel time vs 78.6 TF; HBM write
-fraction beside it) and `cpu_baseline` (the C restatement of the reference
-with its fork_jobs column bands, on the host cores, bounded sample).
+`roofline` (FP64 VALU: hardware FP64 rate from the committed PMC pass of this
+kernel build vs 78.6 TF; measured HBM traffic; the reference-work rate and the
+HBM-write fraction beside it) and `cpu_baseline` (the C restatement of the
+reference with its fork_jobs column bands, on the host cores, bounded sample).
 """
 
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -37,14 +51,29 @@ CAMERA = os.path.join(ROOT, "scenes", WORKLOADS["c2"][1])
 WORKLOAD = WORKLOADS["c2"][2]
 METRIC = "Mpixels/sec at 1920×1080, 4× AA, depth 5; per-channel RMS vs ref"
 TILE_ROWS = 8
+PROJECT_N = (2, 4, 8)
+XGMI_LINK_GBS = 153.0            # one xGMI link (MI355X_MICROARCH.md); the gather's estimate only
 
 
-def cpu_baseline(col_stride=4, max_procs=16):
+def host_cores():
+    """CPUs this job may use: the affinity mask, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = max(1, min(n, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(col_stride=4):
     """Time the C restatement (fork per core, camera.rb:54 column bands) on a
     strided column sample, in a child process started before any GPU init."""
-    nprocs = max(1, min(max_procs, os.cpu_count() or 1))
+    nprocs = host_cores()
     if WORLD.endswith("c4_world.yml"):
-        col_stride = col_stride * 64           # C4: ~300x the work per pixel; keep the sample ~10-30 s
+        col_stride = col_stride * 64           # C4: ~300x the work per pixel; keep the sample ~10-30 s of CPU
     code = (
         "import sys, time, json; sys.path.insert(0, %r)\n"
         "from raytracing_rb_amd import config\n"
@@ -68,9 +97,71 @@ def cpu_baseline(col_stride=4, max_procs=16):
     except Exception:
         pass
     return {"value": round(r["px"] / r["dt"] / 1e6, 5), "unit": "Mpixels/s", "cores": nprocs, "kind": "port",
-            "sample": "every %dth column of the %s frame (%d px), %d forked processes "
-                      "with camera.rb:54 column bands; %.1f s wall; CPU: %s" % (col_stride, WORKLOAD.split(":")[0],
-                                                                              r["px"], nprocs, r["dt"], model)}
+            "host_cpus": os.cpu_count(),
+            "sample": "every %dth column of the %s frame (%d px), %d forked processes (one per CPU this job may "
+                      "use: affinity mask / cgroup quota) with camera.rb:54 column bands; %.1f s wall; CPU: %s"
+                      % (col_stride, WORKLOAD.split(":")[0], r["px"], nprocs, r["dt"], model)}
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without torch.distributed.run: start the N ranks as a child
+    torch.distributed.run (this process never touches the GPU) and return its status."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def pmc_profile(workload, engine):
+    """The committed PMC pass of this kernel build (tools/pmc_json.py), or None."""
+    from raytracing_rb_amd import roofline
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        pm = json.load(f)
+    stale = pm.get("source_sha") != roofline.kernel_source_sha() or pm.get("engine") != engine
+    return pm, stale
+
+
+def stub_main(args, world, rank):
+    """Test-only (tests/test_host.py): the rank plumbing of the multi-GPU bench on
+    CPU — ranks launched by launch_ranks, a gloo group, a stub tile "render" that
+    writes each packed row's image row index, the one gather, the JSON line.
+    No GPU and no librtx are touched; the JSON says "stub": true."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from raytracing_rb_amd.tiles import DistributedFrame, rank_rows
+    W, H = 40, 37
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
+    df = DistributedFrame(W, H, TILE_ROWS, rank, world, "cpu")
+    ys = torch.as_tensor(rank_rows(H, TILE_ROWS, rank, world), dtype=torch.float64)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        df.packed.copy_(ys[:, None, None].expand_as(df.packed))
+        frame = df.gather()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank == 0:
+        ok = bool(np.array_equal(frame[:, :, 0].numpy(), np.repeat(np.arange(H, dtype=np.float64)[:, None], W, 1)))
+        print(json.dumps({"metric": METRIC, "value": W * H * args.steps / elapsed / 1e6, "unit": "Mpixels/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "stub": True,
+                          "frame_rows_ok": ok}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
 
 
 def main():
@@ -79,10 +170,30 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-projection", action="store_true")
+    ap.add_argument("--emulate-rank", default=None, metavar="k/N",
+                    help="time rank k's share of an N-rank tiled frame on this one GPU")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
                     help="c2: the metric's configuration (default); c4: the 4096-sphere stress scene")
     ap.add_argument("--bvh", type=int, default=1, help="sphere walk: 0 ordered linear, 1 auto, 2 hierarchy")
+    ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra rtx_set_option before timing (experiments)")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # CPU test of the rank plumbing
     args = ap.parse_args()
+
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(launch_ranks(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d: refusing to measure a different GPU count"
+              % (world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub:
+        return stub_main(args, world, rank)
+
     global WORLD, CAMERA, WORKLOAD, METRIC
     if args.workload != "c2":
         if args.workload == "c4":
@@ -94,14 +205,16 @@ def main():
         WORKLOAD = WORKLOADS[args.workload][2]
         METRIC = "Mpixels/sec at 3840×2160, 8× AA, depth 8 (C4, 4096 spheres)"
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print("warning: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+    emulate = None
+    if args.emulate_rank:
+        k, n = (int(v) for v in args.emulate_rank.split("/"))
+        if world != 1 or not (0 <= k < n):
+            print("bench.py: --emulate-rank k/N needs one process and 0 <= k < N", file=sys.stderr)
+            sys.exit(2)
+        emulate = (k, n)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and emulate is None:
         cpu = cpu_baseline()              # before this process touches the GPU
 
     import numpy as np
@@ -110,26 +223,45 @@ def main():
 
     from raytracing_rb_amd import config, roofline
     from raytracing_rb_amd.runtime import Renderer
-    from raytracing_rb_amd.tiles import DistributedFrame
+    from raytracing_rb_amd.tiles import DistributedFrame, rows_per_rank
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            print("bench.py: process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus),
+                  file=sys.stderr)
+            sys.exit(2)
 
     scene, cam = config.load_scene(WORLD, CAMERA)
     W, H = cam.width, cam.height
     r = Renderer(scene, cam, device=local_rank)
     r.set_option("bvh", args.bvh)
+    for kv in args.option:
+        key, val = kv.split("=", 1)
+        r.set_option(key, int(val))
+    engine = r.engine()
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
-    if world == 1:
+    packed_for = {}
+
+    def share_step(k, n):
+        if (k, n) not in packed_for:
+            packed_for[(k, n)] = torch.empty((rows_per_rank(H, TILE_ROWS, n), W, 3), dtype=torch.float64,
+                                             device=dev)
+        r.render_tiles_device(packed_for[(k, n)].data_ptr(), TILE_ROWS, k, n, seed=1, stream=sp)
+
+    if world == 1 and emulate is None:
         frame = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
 
         def step():
             r.render_device(frame.data_ptr(), seed=1, stream=sp)
+    elif world == 1:
+        def step():
+            share_step(*emulate)
     else:
         df = DistributedFrame(W, H, TILE_ROWS, rank, world, dev)
 
@@ -148,13 +280,10 @@ def main():
     r.sync(sp)                              # raises if a reference raise site fired
 
     # ---- timed region: exactly K steps, barrier + synchronize on both sides
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
         step()
-        ev[i][1].record(stream)
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
@@ -163,44 +292,65 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     r.sync(sp)
-    step_ms = [a.elapsed_time(b) for a, b in ev]
 
-    # ---- kernel-only timing of the dominant kernel (k_render) on its stream
-    kern_ms = []
+    # ---- the dominant kernel alone: HIP events on its launch stream around
+    # every ray-tree kernel launch (rtx_kernel_time), outside the timed region
+    r.set_option("kernel_events", 1)
+    kern_ms, kern_launches = [], 0
     for _ in range(max(3, min(args.steps, 10))):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        if world == 1:
+        if world == 1 and emulate is None:
             r.render_device(frame.data_ptr(), seed=1, stream=sp)
+        elif world == 1:
+            share_step(*emulate)
         else:
             r.render_tiles_device(df.packed.data_ptr(), TILE_ROWS, rank, world, seed=1, stream=sp)
-        b.record(stream)
-        b.synchronize()
-        kern_ms.append(a.elapsed_time(b))
-    kern_avg_ms = float(np.mean(kern_ms))
+        ms, kern_launches = r.kernel_time()
+        kern_ms.append(ms)
+    r.set_option("kernel_events", 0)
+    kern_frame_ms = float(np.median(kern_ms))
+
+    # ---- 1-GPU projection of the tile-sharded frame (C3) for N = 2, 4, 8
+    projection = None
+    if world == 1 and emulate is None and not args.no_projection:
+        def timed(fn, reps=3):
+            fn()
+            torch.cuda.synchronize(dev)
+            ts = []
+            for _ in range(reps):
+                a = time.perf_counter()
+                fn()
+                torch.cuda.synchronize(dev)
+                ts.append(time.perf_counter() - a)
+            return float(np.median(ts)) * 1e3
+        full_ms = timed(step)
+        projection = {"method": "each rank's share rendered alone on this GPU (rtx_render_tiles_device), "
+                                "median of 3 after 1 warm-up; projected frame = max over ranks; the RCCL "
+                                "gather is estimated separately at %.0f GB/s per xGMI link" % XGMI_LINK_GBS,
+                      "full_frame_ms": round(full_ms, 4), "per_n": {}}
+        for n in PROJECT_N:
+            shares = [timed(lambda k=k: share_step(k, n)) for k in range(n)]
+            packed_bytes = rows_per_rank(H, TILE_ROWS, n) * W * 3 * 8
+            gather_ms = packed_bytes / (XGMI_LINK_GBS * 1e9) * 1e3
+            mx = max(shares)
+            projection["per_n"][str(n)] = {
+                "rank_ms": [round(v, 4) for v in shares], "max_rank_ms": round(mx, 4),
+                "gather_est_ms": round(gather_ms, 4),
+                "projected_speedup": round(full_ms / (mx + gather_ms), 3),
+                "projected_speedup_no_gather": round(full_ms / mx, 3)}
 
     if rank == 0:
-        # HBM traffic of one k_render launch: the committed rocprofv3 PMC passes of
-        # this workload (tools/gpu_session.sh -> profiles/pmc_k_render.json)
-        traffic, traffic_src = None, None
-        pj = os.path.join(ROOT, "profiles", "pmc_k_render.json")
-        if world == 1 and os.path.exists(pj):
-            with open(pj) as f:
-                pm = json.load(f)
-            if pm.get("workload") == args.workload and pm.get("traffic_bytes"):
-                traffic = int(pm["traffic_bytes"])
-                traffic_src = {"read_bytes": int(pm["read_bytes"]), "write_bytes": int(pm["write_bytes"]),
-                               "correction": pm["correction"], "source": pm["source"]}
         counts = r.count_work(seed=1)           # one counting launch, outside the timed region
-        ops_frame = roofline.algorithmic_ops(counts)
-        ops_launch = ops_frame if world == 1 else ops_frame / world
-        px_launch = W * H if world == 1 else W * H / world
-        achieved_tf = ops_launch / (kern_avg_ms * 1e-3) / 1e12
-        wr_gbs = px_launch * roofline.FRAMEBUFFER_BYTES_PER_PX / (kern_avg_ms * 1e-3) / 1e9
-        value = W * H * args.steps / elapsed / 1e6
+        n_share = emulate[1] if emulate else world
+        px_frame = W * H if n_share == 1 else W * H / n_share
+        ops_frame = roofline.algorithmic_ops(counts) / n_share
+        ref_rate_tf = ops_frame / (kern_frame_ms * 1e-3) / 1e12
+        wr_gbs = px_frame * roofline.FRAMEBUFFER_BYTES_PER_PX / (kern_frame_ms * 1e-3) / 1e9
+        value = W * H * args.steps / elapsed / 1e6 if emulate is None else None
+        pm, stale = pmc_profile(args.workload, engine) if (world == 1 and emulate is None) else (None, None)
+        hw = roofline.hw_fp64(pm, kern_frame_ms) if pm else None
         line = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": round(value, 3) if value is not None else None,
             "unit": "Mpixels/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -212,31 +362,47 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": WORKLOAD, "width": W, "height": H, "samples_per_pixel": cam.pre_sample_times,
-                       "trace_depth": cam.trace_depth, "objects": scene.n_objects, "seed": 1,
+                       "trace_depth": cam.trace_depth, "objects": scene.n_objects, "seed": 1, "engine": engine,
                        "parallelism": "tiles%d-rr x %d ranks, 1 RCCL gather/frame" % (TILE_ROWS, world)
                        if world > 1 else "1 GPU"},
             "roofline": {
-                "bound": "mfma",
+                "bound": "valu_fp64",
                 "unit": "TFLOP/s",
-                "achieved": round(achieved_tf, 4),
+                "achieved": hw["achieved_tflops"] if hw else None,
                 "peak": roofline.FP64_PEAK_TFLOPS,
-                "frac": round(achieved_tf / roofline.FP64_PEAK_TFLOPS, 5),
-                "traffic": traffic,
-                "kernel": "k_render",
-                "kernel_avg_ms": round(kern_avg_ms, 4),
-                "algorithmic_fp64_ops_per_launch": int(ops_launch),
-                "note": "FP64 VALU-bound path (no dense contraction): peak = MI355X dense FP64 78.6 TF "
-                        "(vector == matrix rate); ops = device-counted reference events x frozen cost table "
-                        "(raytracing_rb_amd/roofline.py)",
-                "traffic_detail": traffic_src,
+                "frac": hw["frac"] if hw else None,
+                "traffic": (int(pm["traffic_bytes_per_frame"]) if pm and pm.get("traffic_bytes_per_frame")
+                            else None),
+                "kernel": pm["kernel"] if pm else roofline.DOMINANT_KERNEL[engine],
+                "kernel_ms_per_frame": round(kern_frame_ms, 4),
+                "kernel_launches_per_frame": kern_launches,
+                "kernel_avg_ms": round(kern_frame_ms / max(1, kern_launches), 4),
+                "hw": hw,
+                "pmc_source": ({"file": "profiles/pmc_%s.json" % args.workload, "stale": stale,
+                                "source_sha": pm.get("source_sha"), "session": pm.get("session")}
+                               if pm else None),
+                "note": "FP64 VALU-bound path (no dense contraction, no MFMA): achieved = FP64 FLOP per frame from "
+                        "the committed PMC pass of this kernel build (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64 x active "
+                        "lanes) / the live HIP-event kernel time; peak = MI355X vector FP64 78.6 TF; traffic = "
+                        "2 x FETCH_SIZE + WRITE_SIZE per frame (MI355X_MICROARCH.md HBM corrections)",
+                "reference_work_rate": {"achieved_tflops": round(ref_rate_tf, 4),
+                                        "algorithmic_fp64_ops_per_frame": int(ops_frame),
+                                        "note": "the brute-force reference algorithm's ops (device-counted events "
+                                                "x frozen cost table, raytracing_rb_amd/roofline.py) per kernel "
+                                                "second: a work rate, not a utilisation (the exact culls and the "
+                                                "hierarchy skip most of these ops)"},
                 "hbm_write": {"achieved": round(wr_gbs, 3), "peak": roofline.HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(wr_gbs / roofline.HBM_PEAK_GBS, 7),
                               "bytes_per_px": roofline.FRAMEBUFFER_BYTES_PER_PX},
             },
             "cpu_baseline": cpu,
             "work_counts": counts,
-            "step_ms_median": round(float(np.median(step_ms)), 4),
         }
+        if emulate:
+            line["emulate_rank"] = {"rank": emulate[0], "nranks": emulate[1],
+                                    "rank_ms_per_frame": round(elapsed / args.steps * 1e3, 4)}
+        if projection:
+            line["projection"] = projection
         print(json.dumps(line), flush=True)
     r.close()
     if world > 1:

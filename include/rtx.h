@@ -231,8 +231,14 @@ enum {
 };
 rtx_status rtx_count_work(rtx_context* ctx, uint64_t seed, uint64_t counts[RTX_NCOUNT]);
 
+/* Device time of the ray-tree kernel launches of the last render call on this
+ * context (HIP events recorded on the launch stream around each launch; needs
+ * option "kernel_events" = 1 before the call).  Waits for those events. */
+rtx_status rtx_kernel_time(rtx_context* ctx, double* total_ms, int32_t* launches);
+
 /* Kernel-variant control for experiments; 0 = default. */
 rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
+rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
 /* keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
          2 always; every choice renders the same bits), "bvh_min" [32], "bvh_sah" (1 [default] binned-SAH hierarchy
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
@@ -240,7 +246,7 @@ rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
          -1 = as many as fit), "force_stack" (per-lane ray-stack bucket), "postpone" (hierarchy walks
          still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never), "tile_order" (1 expensive
          8x8 tiles first by a primary-hit probe, 0 row-major, -1 [default] = 1 up to 512 spheres; the order
-         changes no bit). */
+         changes no bit), "kernel_events" (1: time the ray-tree launches, rtx_kernel_time). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

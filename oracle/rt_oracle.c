@@ -472,12 +472,16 @@ static void push(Stack* st, Item it) {
   st->a[st->n++] = it;
 }
 
-typedef struct { const Scene* s; uint64_t seed; int x, y, sample; Stack st; Lit* lit; } Tr;
+typedef struct { const Scene* s; uint64_t seed; int x, y, sample; Stack st; Lit* lit; int gt1; } Tr;
 
-static void add_leaf(V* sum, V c, T* t) {                          /* ray_tracer.rb:292-298 */
+/* ray_tracer.rb:292-298.  The running sum is the FIFO drain's (leaves in
+ * emission order), but the drain runs after the whole tree (:39-45): a
+ * "color greater than 1" is raised only once every rt_map of the tree has run,
+ * so an rt_map raise anywhere in the tree comes first (trace_sync below). */
+static void add_leaf(Tr* tr, V* sum, V c) {
   if (rto_debug > 0) fprintf(stderr, "leaf %.17g %.17g %.17g\n", c.x, c.y, c.z);
   *sum = vadd(*sum, c);
-  if (!(sum->x <= 1 && sum->y <= 1 && sum->z <= 1)) raise_(t, RTX_ECOLOR_GT1, "color greater than 1");
+  if (!(sum->x <= 1 && sum->y <= 1 && sum->z <= 1)) tr->gt1 = 1;
 }
 
 static void rt_map(Tr* tr, Item it, V* sum, T* t) {                /* ray_tracer.rb:50-164 */
@@ -496,7 +500,7 @@ static void rt_map(Tr* tr, Item it, V* sum, T* t) {                /* ray_tracer
   if (nfired) {
     for (int k = 0; k < nfired; k++) {
       const Light* L = &s->light[tr->lit[k].light];
-      add_leaf(sum, vdiv(vmul(it.att, vsc(L->color, L->hl_rate)), (double)nfired), t);
+      add_leaf(tr, sum, vdiv(vmul(it.att, vsc(L->color, L->hl_rate)), (double)nfired));
     }
     return;
   }
@@ -574,7 +578,7 @@ static void rt_map(Tr* tr, Item it, V* sum, T* t) {                /* ray_tracer
         filter = vmul(texcolor(&s->tex[o->tex], o->hs, o->vs, 0.0, 0.0, u, v, t), filter);
       }
     }
-    add_leaf(sum, vmul(it.att, local_lighting(o, h.hit, tr->lit, nl, s, n, has_filter, filter, t)), t);
+    add_leaf(tr, sum, vmul(it.att, local_lighting(o, h.hit, tr->lit, nl, s, n, has_filter, filter, t)));
   }
 }
 
@@ -583,10 +587,12 @@ static V trace_sync(Tr* tr, Ray ray, T* t) {                      /* ray_tracer.
   tr->st.n = 0;
   Item root = {ray, tr->s->cam.trace_depth, vmk(1.0, 1.0, 1.0), 1};
   push(&tr->st, root);
+  tr->gt1 = 0;
   while (tr->st.n > 0) {
     Item it = tr->st.a[--tr->st.n];
     rt_map(tr, it, &sum, t);
   }
+  if (tr->gt1) raise_(t, RTX_ECOLOR_GT1, "color greater than 1");   /* the drain, after the tree */
   return sum;
 }
 

@@ -69,6 +69,13 @@ struct rtx_context {
   int64_t opt_postpone = -1;         // query_bvh postponing threshold in lanes (-1: auto by hierarchy size)
   int64_t opt_tile_order = -1;       // 1: expensive tiles first (k_tile_cost/k_tile_sort), 0: natural order, -1: auto
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
+  int64_t opt_engine = 0;            // 0: persistent lanes (per-lane LIFO ray tree), 1: bounce levels
+  int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
+  bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
+  // rtx_kernel_time: event pairs around each ray-tree kernel launch of the last render call
+  static constexpr int MAX_EV = 32;
+  hipEvent_t ev[2 * MAX_EV] = {};
+  int n_ev = 0;
 };
 
 static rtx_status fail(rtx_context* c, rtx_status s, const char* fmt, ...) {
@@ -346,11 +353,33 @@ void rtx_context_destroy(rtx_context* c) {
   hipFree(c->d_scratch);
   hipFree(c->d_stk);
   hipFree(c->d_work);
+  for (hipEvent_t ev : c->ev)
+    if (ev) (void)hipEventDestroy(ev);
   delete c;
+}
+
+rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
+  if (!c || !key || !value) return RTX_EINVAL;
+  const struct { const char* k; int64_t v; } tab[] = {
+      {"engine", c->opt_engine},       {"force_stack", c->opt_force_stack}, {"bvh", c->opt_bvh},
+      {"bvh_sah", c->opt_bvh_sah},     {"bvh_min", c->opt_bvh_min},         {"postpone", c->opt_postpone},
+      {"lds_stack", c->opt_lds_stack}, {"tile_order", c->opt_tile_order},   {"sphere_src", c->opt_sphere_src},
+      {"kernel_events", c->opt_kernel_events}};
+  for (const auto& t : tab)
+    if (!strcmp(key, t.k)) {
+      *value = t.v;
+      return RTX_OK;
+    }
+  return fail(c, RTX_EINVAL, "unknown option '%s'", key);
 }
 
 rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!c || !key) return RTX_EINVAL;
+  if (!strcmp(key, "engine")) {            // 0: persistent lanes (one ray tree per lane), 1: bounce levels
+    if (value < 0 || value > 1) return fail(c, RTX_EINVAL, "engine must be 0 or 1");
+    c->opt_engine = value;
+    return RTX_OK;
+  }
   if (!strcmp(key, "force_stack")) {
     c->opt_force_stack = value;
     return RTX_OK;
@@ -382,6 +411,10 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "tile_order")) {        // 1: expensive tiles first; 0: natural (row-major) tile order
     if (value < -1 || value > 1) return fail(c, RTX_EINVAL, "tile_order must be -1, 0 or 1");
     c->opt_tile_order = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "kernel_events")) {     // 1: HIP events around the ray-tree launches (rtx_kernel_time)
+    c->opt_kernel_events = value != 0;
     return RTX_OK;
   }
   if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads
@@ -612,6 +645,13 @@ rtx_status rtx_camera_set(rtx_context* c, const rtx_camera_desc* d) {
   if (d->pre_sample_times < 1 || d->pre_sample_times > 16)
     return fail(c, RTX_EINVAL, "pre_sample_times must be in [1, 16]");
   if (d->max_sample_times < 0) return fail(c, RTX_EINVAL, "max_sample_times must be >= 0");
+  {
+    // device work items are 32-bit: every (8x8-padded) pixel x sample of the frame must fit
+    const size_t padded = (size_t)((d->width + 7) / 8) * (size_t)((d->height + 7) / 8) * 64;
+    const size_t ms = (size_t)std::max(d->pre_sample_times, d->max_sample_times);
+    if (padded * ms > (size_t)INT32_MAX)
+      return fail(c, RTX_EINVAL, "%dx%d pixels x %zu samples exceed 2^31 work items", d->width, d->height, ms);
+  }
   if (d->trace_depth < 0 || d->trace_depth > 1000) return fail(c, RTX_EINVAL, "bad trace_depth");
   if (d->monte_carlo_diffusion_times < 1) return fail(c, RTX_EINVAL, "monte_carlo_diffusion_times must be >= 1");
   uint32_t err = 0;
@@ -680,6 +720,10 @@ static rtx_status ensure_stack(rtx_context* c, KParams& p, int maxs) {
 }
 
 static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
+  // The context's device first: every allocation below and in ensure_stack /
+  // ensure_scratch, and every launch, must land on it whatever device the
+  // calling thread had selected.
+  HIPCHK(c, hipSetDevice(c->device));
   if (!c->have_scene) return fail(c, RTX_EINVAL, "no scene uploaded");
   if (!c->have_cam) return fail(c, RTX_EINVAL, "no camera set");
   memset(&p, 0, sizeof p);
@@ -706,6 +750,10 @@ static rtx_status render_region(rtx_context* c, KParams& p, bool count, int maxs
   const size_t npx = (size_t)p.nx * p.nrows;
   if (npx == 0) return RTX_OK;
   const size_t ms = (size_t)std::max(p.pre, p.max_samples);
+  // Work items are 32-bit on the device: (8x8-padded pixels) x samples must fit.
+  const size_t padded = (size_t)((p.nx + 7) / 8) * ((p.nrows + 7) / 8) * 64;
+  if (padded * ms > (size_t)INT32_MAX)
+    return fail(c, RTX_EINVAL, "%zu pixels x %zu samples exceed the 2^31 work items of one launch", npx, ms);
   const size_t smp_bytes = npx * ms * 4 * sizeof(double);
   void* buf = nullptr;
   const size_t tiles = (size_t)((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
@@ -719,7 +767,13 @@ static rtx_status render_region(rtx_context* c, KParams& p, bool count, int maxs
   // gains nothing (the frame is 500 ms of evenly expensive tiles).
   const bool order = c->opt_tile_order > 0 || (c->opt_tile_order < 0 && c->scene.n_sphere <= RTX_TILE_ORDER_SPHERES);
   p.tile_order = order ? p.tile_cls + tiles : nullptr;
-  const hipError_t e = launch_render(p, sph_mode(c), count, maxs, stream);
+  KernelEvents kev{c->ev, 0, rtx_context::MAX_EV};
+  if (c->opt_kernel_events && !count && !c->ev[0]) {
+    for (int k = 0; k < 2 * rtx_context::MAX_EV; k++) HIPCHK(c, hipEventCreate(&c->ev[k]));
+  }
+  const hipError_t e = launch_render(p, sph_mode(c), count, maxs, stream,
+                                     c->opt_kernel_events && !count ? &kev : nullptr);
+  if (c->opt_kernel_events && !count) c->n_ev = kev.n;
   const hipError_t f = hipFreeAsync(buf, stream);
   HIPCHK(c, e);
   HIPCHK(c, f);
@@ -777,6 +831,21 @@ rtx_status rtx_render_tiles_device(rtx_context* c, int32_t tile_rows, int32_t ra
   return render_region(c, p, false, maxs, (hipStream_t)stream);
 }
 
+rtx_status rtx_kernel_time(rtx_context* c, double* total_ms, int32_t* launches) {
+  if (!c || !total_ms) return fail(c, RTX_EINVAL, "null argument");
+  HIPCHK(c, hipSetDevice(c->device));
+  double sum = 0.0;
+  for (int k = 0; k < c->n_ev; k++) {
+    float ms = 0.0f;
+    HIPCHK(c, hipEventSynchronize(c->ev[2 * k + 1]));
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev[2 * k], c->ev[2 * k + 1]));
+    sum += ms;
+  }
+  *total_ms = sum;
+  if (launches) *launches = c->n_ev;
+  return RTX_OK;
+}
+
 rtx_status rtx_sync(rtx_context* c, void* stream) {
   if (!c) return RTX_EINVAL;
   hipSetDevice(c->device);
@@ -796,9 +865,11 @@ rtx_status rtx_sync(rtx_context* c, void* stream) {
       pix = e.first[code];
       first = status_of[code];
     }
-  const long long W = c->have_cam ? c->cam.width : 1;
-  return fail(c, first, "%s at pixel (%lld,%lld)%s", rtx_status_string(first), (long long)(pix % W),
-              (long long)(pix / W), __builtin_popcount(e.flags) > 1 ? " (and other errors)" : "");
+  const char* more = __builtin_popcount(e.flags) > 1 ? " (and other errors)" : "";
+  if (c->err_keys_rays) return fail(c, first, "%s at ray %llu%s", rtx_status_string(first), pix, more);
+  // pixel keys are x * height + y: render_sync's x-outer, y-inner order (camera.rb:102-103)
+  const unsigned long long H = c->have_cam ? (unsigned long long)c->cam.height : 1;
+  return fail(c, first, "%s at pixel (%llu,%llu)%s", rtx_status_string(first), pix / H, pix % H, more);
 }
 
 static rtx_status ensure_scratch(rtx_context* c, size_t bytes) {
@@ -881,7 +952,10 @@ rtx_status rtx_trace(rtx_context* c, int32_t n, const double* rays, const int32_
   p.nrays = n;
   HIPCHK(c, launch_trace(p, sph_mode(c), maxs, nullptr));
   HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
-  return rtx_sync(c, nullptr);
+  c->err_keys_rays = true;
+  const rtx_status st = rtx_sync(c, nullptr);
+  c->err_keys_rays = false;
+  return st;
 }
 
 rtx_status rtx_path_trace(rtx_context* c, int32_t n, const double* rays, double* out) {
@@ -902,7 +976,10 @@ rtx_status rtx_path_trace(rtx_context* c, int32_t n, const double* rays, double*
   p.nrays = n;
   HIPCHK(c, launch_path_trace(p, nullptr));
   HIPCHK(c, hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
-  return rtx_sync(c, nullptr);
+  c->err_keys_rays = true;
+  const rtx_status st = rtx_sync(c, nullptr);
+  c->err_keys_rays = false;
+  return st;
 }
 
 rtx_status rtx_count_work(rtx_context* c, uint64_t seed, uint64_t counts[RTX_NCOUNT]) {

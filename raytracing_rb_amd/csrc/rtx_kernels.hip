@@ -154,8 +154,16 @@ RTX_MATH_FN void rx_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 #define RTX_SINCOS(x, s, c) rx_sincos((x), (s), (c))
 #endif
 
+// A lane's first raise (low byte) plus GT1_PENDING: rt_reduce's "color greater
+// than 1" is raised by the FIFO drain after the whole tree (ray_tracer.rb:39-45),
+// so it is held back and applies only if no rt_map of the tree raised (end_tree).
+constexpr uint32_t GT1_PENDING = 0x80000000u;
 __device__ __forceinline__ void seterr(uint32_t& err, uint32_t code) {
-  if (!err) err = code;
+  if (!(err & 0xffu)) err = (err & GT1_PENDING) | code;
+}
+__device__ __forceinline__ uint32_t end_tree(uint32_t err) {
+  const uint32_t code = err & 0xffu;
+  return code ? code : ((err & GT1_PENDING) ? (uint32_t)ERR_COLOR_GT1 : 0u);
 }
 
 // ----------------------------------------------------------------- spheres
@@ -773,7 +781,7 @@ struct Stack {
 
 __device__ __forceinline__ void add_leaf(V3& sum, V3 c, uint32_t& err) {   // ray_tracer.rb:292-298
   sum = vadd(sum, c);
-  if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) seterr(err, ERR_COLOR_GT1);
+  if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) err |= GT1_PENDING;
 }
 
 // Children are generated in the reference's push order; the most recent live
@@ -940,9 +948,15 @@ __device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3
   return true;
 }
 
-__device__ __forceinline__ void record_error(ErrState* e, uint32_t code, int x, int y, int W) {
+// `key` orders the raise sites as the reference meets them: x * height + y for
+// pixels (render_sync runs x in the outer loop, y in the inner one,
+// camera.rb:102-103), the ray index for rtx_trace.
+__device__ __forceinline__ void record_error(ErrState* e, uint32_t code, unsigned long long key) {
   atomicOr(&e->flags, 1u << code);
-  atomicMin(&e->first[code], (unsigned long long)y * (unsigned long long)W + (unsigned long long)x);
+  atomicMin(&e->first[code], key);
+}
+__device__ __forceinline__ unsigned long long px_key(int x, int y, int H) {
+  return (unsigned long long)x * (unsigned long long)H + (unsigned long long)y;
 }
 
 __device__ __forceinline__ int row_to_y(const KParams& p, int row) {
@@ -1048,11 +1062,12 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
         } else {
           // the current tree is complete: the item's result
           if (started) {
+            err = end_tree(err);
             if (SRC == SRC_RAYS) {
               p.out[3 * row] = sum.x;
               p.out[3 * row + 1] = sum.y;
               p.out[3 * row + 2] = sum.z;
-              if (err) record_error(p.err, err, row, 0, 0x7fffffff);
+              if (err) record_error(p.err, err, (unsigned long long)row);
             } else {                            // one camera sample: colour + first raise
               double2* q = reinterpret_cast<double2*>(p.samples + ((size_t)row * p.nx + px_) * ms * 4 +
                                                       (size_t)sample * 4);
@@ -1098,7 +1113,8 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
       int fresh = 0;
       if (left < need) {
         // guided self-scheduling: besides what the lanes need now, claim up to
-        // 1/(4 x waves) of what the last claim saw remaining (<= 128), so a
+        // 1/(RTX_CLAIM_DIV x waves) of what the last claim saw remaining (at
+        // most RTX_CLAIM_MAX), so a
         // wave pays the atomic's round trip once per several refills and the
         // items held privately stay a small share of the pool at every point
         int extra = (nwork - wlim) / (RTX_CLAIM_DIV * nwaves);
@@ -1323,7 +1339,7 @@ __global__ __launch_bounds__(256) void k_path_trace(KParams p) {
   p.out[3 * (size_t)i] = sum.x;
   p.out[3 * (size_t)i + 1] = sum.y;
   p.out[3 * (size_t)i + 2] = sum.z;
-  if (err) record_error(p.err, err, i, 0, 0x7fffffff);
+  if (err) record_error(p.err, err, (unsigned long long)i);
 }
 
 // Camera#render_at's reduction (camera.rb:70-99) over the sample records of
@@ -1382,7 +1398,7 @@ __global__ __launch_bounds__(256) void k_finalize(KParams p, int phase) {
     if (variance >= cam.variant_threshold) {
       if (p.max_samples > pre) {                     // more samples: the SRC_EXTRA launch
         p.extra_list[atomicAdd(p.extra_count, 1)] = idx;
-        if (err) record_error(p.err, err, x, y, cam.width);
+        if (err) record_error(p.err, err, px_key(x, y, cam.height));
         return;
       }
       avg = vdiv(vadd(vsc(avg, (double)pre), v3(0.0, 0.0, 0.0)), (double)p.max_samples);
@@ -1399,7 +1415,7 @@ __global__ __launch_bounds__(256) void k_finalize(KParams p, int phase) {
   o[0] = avg.x;
   o[1] = avg.y;
   o[2] = avg.z;
-  if (err) record_error(p.err, err, x, y, cam.width);
+  if (err) record_error(p.err, err, px_key(x, y, cam.height));
 }
 
 // ----------------------------------------------------------------- tile order
@@ -1598,6 +1614,8 @@ static size_t lds_layout(KParams& p, int mode, int bs) {
   return off;
 }
 
+static thread_local KernelEvents* g_kev = nullptr;   // set by launch_render for its launches
+
 // Persistent launch: as many workgroups as can be resident at once (the
 // occupancy API; an over-estimate only leaves blocks that start after the
 // pool is empty and exit at once), never more than the work needs.
@@ -1621,8 +1639,15 @@ static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   if (blocks <= 0) return hipSuccess;
   e = hipMemsetAsync(p.work, 0, sizeof(int), s);
   if (e != hipSuccess) return e;
+  KernelEvents* kev = g_kev && g_kev->n < g_kev->max ? g_kev : nullptr;
+  if (kev) (void)hipEventRecord(kev->ev[2 * kev->n], s);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BS), lds, s, p);
-  return hipGetLastError();
+  e = hipGetLastError();
+  if (kev) {
+    (void)hipEventRecord(kev->ev[2 * kev->n + 1], s);
+    kev->n++;
+  }
+  return e;
 }
 
 template <bool COUNT, int MAXS, int SRC>
@@ -1656,9 +1681,15 @@ static hipError_t launch_src(const KParams& p, int mode, bool count, int maxs, i
 // reduction, then (only when max_sample_times > pre_sample_times) the extra
 // samples of the pixels whose variance asked for them and their reduction.
 // All on stream `s`; p.samples / extra_list / extra_count are the caller's.
-hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s) {
+struct KevScope {                   // g_kev for the duration of one launch_render
+  explicit KevScope(KernelEvents* k) { g_kev = k; }
+  ~KevScope() { g_kev = nullptr; }
+};
+
+hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s, KernelEvents* kev) {
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   if (tiles == 0) return hipSuccess;
+  KevScope kscope(count ? nullptr : kev);
   if (count) mode = (mode == SPH_LIN_LDS || mode == SPH_BVH_LDS) ? SPH_LIN_LDS : SPH_LIN_SCALAR;
   mode = resolve_mode(p.scene, mode);
   hipError_t e = hipMemsetAsync(p.extra_count, 0, sizeof(int32_t), s);

@@ -13,7 +13,7 @@ namespace rtx {
 struct ErrState {
   unsigned int flags;              // bit (1 << code) for every code raised
   unsigned int pad;
-  unsigned long long first[5];     // per ERR_ code (rtx_vec3.h): min linear pixel index (y*W + x)
+  unsigned long long first[5];     // per ERR_ code (rtx_vec3.h): min key (pixels: x*H + y, render_sync order; rays: index)
 };
 
 struct KParams {
@@ -58,11 +58,18 @@ enum SphMode : int {
   SPH_BVH_GLOBAL = 3,    // four-wide ball hierarchy, nodes + leaf records by scalar loads
 };
 
+// HIP event pairs recorded on the launch stream around every ray-tree kernel
+// launch of one render call (option "kernel_events", rtx_kernel_time).
+struct KernelEvents {
+  hipEvent_t* ev;                  // 2 * max events: start, end of launch k at ev[2k], ev[2k+1]
+  int n, max;
+};
+
 int stack_bucket(int need);
 // mode: SphMode; a linear mode whose records exceed the LDS budget falls back to
 // SPH_LIN_SCALAR, a BVH mode to SPH_BVH_GLOBAL.  Counting launches always walk
 // linearly (the counters are the reference's brute-force events).
-hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s);
+hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s, KernelEvents* kev = nullptr);
 hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s);
 hipError_t launch_path_trace(KParams p, hipStream_t s);
 int resolve_mode(const SceneDev& S, int mode);

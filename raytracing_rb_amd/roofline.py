@@ -38,3 +38,58 @@ FRAMEBUFFER_BYTES_PER_PX = 24      # float64 RGB written once per pixel
 
 def algorithmic_ops(counts):
     return sum(COST[k] * int(counts.get(k, 0)) for k in COST)
+
+# The dominant (ray-tree) kernel of each engine, as rocprofv3 names it.
+DOMINANT_KERNEL = {"lanes": "k_render", "levels": "k_level"}
+
+# FP64 FLOP per lane of one wave instruction of each counted class.
+F64_FLOP = {"SQ_INSTS_VALU_FMA_F64": 2, "SQ_INSTS_VALU_ADD_F64": 1, "SQ_INSTS_VALU_MUL_F64": 1,
+            "SQ_INSTS_VALU_TRANS_F64": 1}
+
+
+def kernel_source_sha():
+    """Identity of the kernel build: sha256 over the device sources and build flags."""
+    import hashlib
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    h = hashlib.sha256()
+    for f in ("rtx_kernels.hip", "rtx_vec3.h", "rtx_scene.h", "rtx_launch.h", "rtx_capi.cpp"):
+        with open(os.path.join(here, "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    from . import _build
+    h.update(" ".join(_build.FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def active_lanes(per_frame):
+    """Mean active lanes per VALU wave instruction: thread-cycles / instruction-cycles
+    when SQ_INST_CYCLES_VALU was collected, else thread-cycles / instructions (this
+    treats every VALU instruction as one issue cycle: a lower bound on the lanes
+    when some take more)."""
+    tc = per_frame.get("SQ_THREAD_CYCLES_VALU")
+    ic = per_frame.get("SQ_INST_CYCLES_VALU")
+    ni = per_frame.get("SQ_INSTS_VALU")
+    if tc and ic:
+        return min(64.0, tc / ic), "SQ_THREAD_CYCLES_VALU / SQ_INST_CYCLES_VALU"
+    if tc and ni:
+        return min(64.0, tc / ni), "SQ_THREAD_CYCLES_VALU / SQ_INSTS_VALU"
+    return None, None
+
+
+def hw_fp64(pm, kernel_ms_per_frame):
+    """Hardware FP64 rate of the dominant kernel from a PMC profile (tools/pmc_json.py)."""
+    pf = pm.get("per_frame") or {}
+    if not all(k in pf for k in F64_FLOP):
+        return None
+    lanes, how = active_lanes(pf)
+    if lanes is None:
+        return None
+    wave_flop = sum(F64_FLOP[k] * pf[k] for k in F64_FLOP)      # FP64 FLOP per lane, summed over waves
+    flop = wave_flop * lanes
+    ach = flop / (kernel_ms_per_frame * 1e-3) / 1e12
+    return {"achieved_tflops": round(ach, 4), "frac": round(ach / FP64_PEAK_TFLOPS, 5),
+            "fp64_flop_per_frame": flop, "f64_wave_instrs_per_frame": {k: pf[k] for k in F64_FLOP},
+            "active_lanes": round(lanes, 2), "active_lanes_from": how,
+            "valu_wave_instrs_per_frame": pf.get("SQ_INSTS_VALU"),
+            "f64_share_of_valu": round(sum(pf[k] for k in F64_FLOP) / pf["SQ_INSTS_VALU"], 4)
+            if pf.get("SQ_INSTS_VALU") else None}

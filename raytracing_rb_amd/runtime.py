@@ -124,6 +124,25 @@ class Renderer:
         self._check(self.lib.rtx_render_tiles_device(self.h, tile_rows, rank, nranks, seed, C.c_void_p(d_packed),
                                                      C.c_void_p(stream or 0)))
 
+    def get_option(self, key):
+        v = C.c_int64()
+        self._check(self.lib.rtx_get_option(self.h, key.encode(), C.byref(v)))
+        return v.value
+
+    ENGINES = {0: "lanes", 1: "levels"}
+
+    def engine(self):
+        """Name of the ray-tree engine the next render uses (option "engine")."""
+        return self.ENGINES[self.get_option("engine")]
+
+    def kernel_time(self):
+        """(total ms, launches) of the ray-tree kernel launches of the last render
+        call (HIP events on the launch stream; needs set_option("kernel_events", 1))."""
+        ms = C.c_double()
+        n = C.c_int32()
+        self._check(self.lib.rtx_kernel_time(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
     def sync(self, stream=None):
         self._check(self.lib.rtx_sync(self.h, C.c_void_p(stream or 0)))
 

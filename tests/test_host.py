@@ -232,3 +232,28 @@ def test_distributed_gather_gloo_world2():
                                camera_overrides={"width": W, "height": H})
     ref, st, rc = Oracle(sd, cd).render()
     assert np.array_equal(frame, ref)
+
+
+def test_bench_launches_its_own_ranks_gloo_stub():
+    """bench.py --gpus 2 without torch.distributed.run starts the 2 ranks itself
+    (launch_ranks), the world size is checked, the one gather runs and rank 0
+    prints the JSON line (stub tile render on CPU/gloo: no GPU, no librtx)."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub", "--gpus", "2", "--steps", "2"],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["stub"] and line["frame_rows_ok"]
+
+
+def test_bench_refuses_mismatched_world_size():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub", "--gpus", "2"],
+                         capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode == 2 and "refusing" in out.stderr

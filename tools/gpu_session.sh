@@ -1,21 +1,71 @@
 #!/bin/bash
-# One GPU session (round evidence): tests, smoke, PMC traffic passes, bench, kernel-trace stats.
-#   bash tools/gpu_session.sh TAG
+# One GPU session (round evidence), run on the GPU box from the repo root:
+#   bash tools/gpu_session.sh TAG [MODE] [ENGINE]
+# MODE: full (default) = tests, smoke, PMC passes, bench (+ projection), kernel-trace stats, C4 bench
+#       quick          = tests + bench
+#       pmc            = PMC passes + bench + kernel-trace stats
+#       bench          = bench + kernel-trace stats
+# ENGINE: rtx engine option for the PMC passes (0 lanes, 1 levels; default: the library default)
 # Every GPU step has its own time limit; steps are chained with && (stop at the first failure).
 set -o pipefail
 export TMPDIR=/tmp
-TAG=${1:-r01}
+TAG=${1:-r02}
+MODE=${2:-full}
+ENGINE=${3:-}
 OUT=gpurun_out/$TAG
-mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
-timeout -k 10 -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o pf --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1 && \
-timeout -k 10 -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o pw --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_write.log 2>&1 && \
-python tools/pmc_json.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_k_render.json --workload c2 > /dev/null && \
-mkdir -p profiles && cp $OUT/pmc_k_render.json profiles/pmc_k_render.json && \
-timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o kt --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.log 2>&1 && \
-timeout -k 10 600 python bench.py --workload c4 --steps 3 --warmup 1 > $OUT/bench_c4.json 2> $OUT/bench_c4.err
+mkdir -p $OUT profiles
+ENGOPT='{}'
+ENGNAME=$(python3 -c "import sys; sys.path.insert(0,'.'); print({'0':'lanes','1':'levels'}.get('$ENGINE','default'))")
+if [ -n "$ENGINE" ]; then ENGOPT="{\"engine\": $ENGINE}"; fi
+
+tests() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+}
+smoke() {
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+}
+pmcpass() {  # name counters...   (one rocprofv3 run per pass; 1 warm-up + 3 timed frames)
+  local n=$1; shift
+  timeout -k 5 -s KILL 180 rocprofv3 --pmc "$@" --kernel-trace -d $OUT/pmc_$n -o $n --output-format csv -- \
+    python3 tools/timing.py --scene c2 --reps 3 "$ENGOPT" > $OUT/pmc_$n.log 2>&1
+}
+pmc() {
+  (timeout -k 5 -s KILL 60 rocprofv3 -L > $OUT/rocprof_counters.txt 2>&1 || true) && \
+  pmcpass a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY && \
+  pmcpass b SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR && \
+  pmcpass c FETCH_SIZE && \
+  pmcpass d WRITE_SIZE && \
+  { if grep -q "SQ_INST_CYCLES_VALU" $OUT/rocprof_counters.txt; then pmcpass e SQ_INST_CYCLES_VALU SQ_INSTS_VALU; else true; fi; } && \
+  DIRS="$OUT/pmc_a $OUT/pmc_b $OUT/pmc_c $OUT/pmc_d" && \
+  { [ -d $OUT/pmc_e ] && DIRS="$DIRS $OUT/pmc_e"; true; } && \
+  python3 tools/pmc_json.py $OUT/pmc_c2.json $DIRS --workload c2 --frames 4 --skip 1 --session $TAG \
+    --engine $(python3 -c "
+import sys; sys.path.insert(0,'.')
+from raytracing_rb_amd import config
+from raytracing_rb_amd.runtime import Renderer
+import json
+sd, cd = config.load_scene('scenes/c2_world.yml', 'scenes/c2_camera.yml', camera_overrides={'width': 8, 'height': 8})
+r = Renderer(sd, cd)
+for k, v in json.loads('$ENGOPT').items(): r.set_option(k, v)
+print(r.engine())") > $OUT/pmc_json.log 2>&1 && \
+  cp $OUT/pmc_c2.json profiles/pmc_c2.json
+}
+bench() {
+  timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err && \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o kt --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-projection > $OUT/prof_bench.log 2>&1
+}
+bench_c4() {
+  timeout -k 10 600 python bench.py --workload c4 --steps 3 --warmup 1 > $OUT/bench_c4.json 2> $OUT/bench_c4.err
+}
+
+case $MODE in
+  full)  tests && smoke && pmc && bench && bench_c4 ;;
+  quick) tests && timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err ;;
+  pmc)   pmc && bench ;;
+  bench) bench ;;
+  *) echo "unknown mode $MODE"; false ;;
+esac
 rc=$?
-echo "session rc=$rc"
+echo "session $TAG $MODE rc=$rc"
 exit $rc

@@ -1,57 +1,79 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of k_render from two rocprofv3 PMC passes.
+"""Per-frame PMC counters of the ray-tree kernel from rocprofv3 passes.
 
-    python tools/pmc_json.py FETCH_DIR WRITE_DIR OUT.json --workload c2
+    python tools/pmc_json.py OUT.json --workload c2 --engine lanes --frames 4 --skip 1 \
+        --session r02a PASS_DIR [PASS_DIR ...]
 
-FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB per dispatch
-(memory-side L2 requests).  MI355X_MICROARCH.md: on gfx950 FETCH_SIZE reports
-half the bytes of wide (16 B/lane) coalesced reads, so the corrected read bytes
-are 2 x FETCH_SIZE; WRITE_SIZE reads 16 B/lane stores exactly.  Other access
-widths are uncalibrated there, so both the raw and the corrected values are
-kept.  Counting launches (k_render<true,...>) are excluded.
+Each PASS_DIR is one `rocprofv3 --pmc ... -d PASS_DIR` run of
+`tools/timing.py --reps F-1` (F frames: one warm-up + F-1 timed).  Counter
+values of every dispatch of the engine's ray-tree kernel are summed; the first
+`--skip` frames' dispatches are dropped (launches per frame = dispatches /
+frames) and the rest averaged per frame.
+
+HBM traffic: FETCH_SIZE / WRITE_SIZE are KiB per dispatch (memory-side L2
+requests).  MI355X_MICROARCH.md: on gfx950 FETCH_SIZE reports half the bytes of
+wide (16 B/lane) coalesced reads, so read bytes = 2 x FETCH_SIZE; WRITE_SIZE
+reads 16 B/lane stores exactly.  Raw values are kept beside the corrected ones.
 """
 import argparse
 import csv
 import glob
 import json
 import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
-def per_launch(d, counter):
-    vals = {}
-    for f in glob.glob(os.path.join(d, "*_counter_collection.csv")):
+def dispatch_values(d, kernel):
+    """{counter: [value per dispatch in dispatch order]} for kernels whose name starts with `kernel`
+    (counting launches, k_render<true,...>, excluded)."""
+    per = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            if r["Counter_Name"] != counter or "k_render" not in name or "k_renderILb1E" in name:
+            short = name.split("(")[0].split("<")[0].strip()
+            if short.split("::")[-1] != kernel or "k_renderILb1E" in name or "<true" in name:
                 continue
-            key = (f, r["Dispatch_Id"])
-            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
-    v = sorted(vals.values())
-    if not v:
-        return None, 0
-    v = v[1:] if len(v) > 2 else v          # drop the first (cold) launch
-    return sum(v) / len(v), len(v)
+            key = int(r["Dispatch_Id"])
+            per.setdefault(r["Counter_Name"], {}).setdefault(key, 0.0)
+            per[r["Counter_Name"]][key] += float(r["Counter_Value"])
+    return {c: [v[k] for k in sorted(v)] for c, v in per.items()}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("fetch_dir")
-    ap.add_argument("write_dir")
     ap.add_argument("out")
+    ap.add_argument("dirs", nargs="+")
     ap.add_argument("--workload", default="c2")
+    ap.add_argument("--engine", default="lanes")
+    ap.add_argument("--frames", type=int, required=True)
+    ap.add_argument("--skip", type=int, default=1)
+    ap.add_argument("--session", default="")
     a = ap.parse_args()
-    fk, nf = per_launch(a.fetch_dir, "FETCH_SIZE")
-    wk, nw = per_launch(a.write_dir, "WRITE_SIZE")
-    out = {
-        "workload": a.workload,
-        "kernel": "k_render",
-        "fetch_size_kib": fk, "write_size_kib": wk, "launches": [nf, nw],
-        "read_bytes": None if fk is None else 2.0 * fk * 1024,
-        "write_bytes": None if wk is None else wk * 1024,
-        "correction": "read = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM section); write = WRITE_SIZE",
-        "source": [os.path.relpath(a.fetch_dir), os.path.relpath(a.write_dir)],
-    }
-    out["traffic_bytes"] = None if fk is None or wk is None else out["read_bytes"] + out["write_bytes"]
+    from raytracing_rb_amd import roofline
+    kernel = roofline.DOMINANT_KERNEL[a.engine]
+    per_frame, launches = {}, None
+    for d in a.dirs:
+        for c, vals in dispatch_values(d, kernel).items():
+            if len(vals) % a.frames:
+                raise SystemExit("%s: %d dispatches of %s is not a multiple of %d frames" % (d, len(vals), c, a.frames))
+            lpf = len(vals) // a.frames
+            launches = lpf
+            kept = vals[a.skip * lpf:]
+            per_frame[c] = sum(kept) / (a.frames - a.skip)
+    out = {"workload": a.workload, "engine": a.engine, "kernel": kernel, "session": a.session,
+           "source_sha": roofline.kernel_source_sha(), "launches_per_frame": launches,
+           "frames": a.frames - a.skip, "per_frame": per_frame,
+           "source": [os.path.relpath(d, ROOT) for d in a.dirs]}
+    if "FETCH_SIZE" in per_frame and "WRITE_SIZE" in per_frame:
+        rd, wr = 2.0 * per_frame["FETCH_SIZE"] * 1024, per_frame["WRITE_SIZE"] * 1024
+        out.update(read_bytes_per_frame=rd, write_bytes_per_frame=wr, traffic_bytes_per_frame=rd + wr,
+                   correction="read = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM section); write = WRITE_SIZE")
+    lanes, how = roofline.active_lanes(per_frame)
+    if lanes:
+        out.update(active_lanes=lanes, active_lanes_from=how)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
