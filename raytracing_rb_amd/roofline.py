@@ -62,15 +62,16 @@ def kernel_source_sha():
 
 
 def active_lanes(per_frame):
-    """Mean active lanes per VALU wave instruction: thread-cycles / instruction-cycles
-    when SQ_INST_CYCLES_VALU was collected, else thread-cycles / instructions (this
-    treats every VALU instruction as one issue cycle: a lower bound on the lanes
-    when some take more)."""
+    """Mean active lanes of the VALU: rocprofv3's own VALUUtilization expression on
+    gfx950 (profiles/gfx950_counters.txt) is 100 * SQ_THREAD_CYCLES_VALU /
+    (SQ_ACTIVE_INST_VALU * 64), so the lanes are THREAD_CYCLES / ACTIVE_INST_VALU.
+    Without SQ_ACTIVE_INST_VALU: THREAD_CYCLES / SQ_INSTS_VALU (one issue cycle per
+    instruction)."""
     tc = per_frame.get("SQ_THREAD_CYCLES_VALU")
-    ic = per_frame.get("SQ_INST_CYCLES_VALU")
+    ac = per_frame.get("SQ_ACTIVE_INST_VALU")
     ni = per_frame.get("SQ_INSTS_VALU")
-    if tc and ic:
-        return min(64.0, tc / ic), "SQ_THREAD_CYCLES_VALU / SQ_INST_CYCLES_VALU"
+    if tc and ac:
+        return min(64.0, tc / ac), "SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU (rocprofv3 VALUUtilization)"
     if tc and ni:
         return min(64.0, tc / ni), "SQ_THREAD_CYCLES_VALU / SQ_INSTS_VALU"
     return None, None
@@ -87,7 +88,14 @@ def hw_fp64(pm, kernel_ms_per_frame):
     wave_flop = sum(F64_FLOP[k] * pf[k] for k in F64_FLOP)      # FP64 FLOP per lane, summed over waves
     flop = wave_flop * lanes
     ach = flop / (kernel_ms_per_frame * 1e-3) / 1e12
-    return {"achieved_tflops": round(ach, 4), "frac": round(ach / FP64_PEAK_TFLOPS, 5),
+    direct = None
+    if "SQ_INSTS_VALU_FLOPS_FP64" in pf:             # the SQ's own FP64 FLOP counters (per lane)
+        df = pf["SQ_INSTS_VALU_FLOPS_FP64"] + pf.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)
+        direct = {"fp64_flop_per_frame": df, "achieved_tflops": round(df / (kernel_ms_per_frame * 1e-3) / 1e12, 4),
+                  "from": "SQ_INSTS_VALU_FLOPS_FP64 + SQ_INSTS_VALU_FLOPS_FP64_TRANS"}
+    return {"achieved_tflops": round(ach, 4), "frac": round(ach / FP64_PEAK_TFLOPS, 5), "direct_counter": direct,
+            "method": "sum over FP64 VALU classes of FLOP/lane (FMA 2, ADD/MUL/TRANS 1) x wave instructions "
+                      "x mean active lanes",
             "fp64_flop_per_frame": flop, "f64_wave_instrs_per_frame": {k: pf[k] for k in F64_FLOP},
             "active_lanes": round(lanes, 2), "active_lanes_from": how,
             "valu_wave_instrs_per_frame": pf.get("SQ_INSTS_VALU"),

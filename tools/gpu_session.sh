@@ -35,8 +35,9 @@ pmc() {
   pmcpass b SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR && \
   pmcpass c FETCH_SIZE && \
   pmcpass d WRITE_SIZE && \
+  pmcpass f SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY && \
   { if grep -q "SQ_INST_CYCLES_VALU" $OUT/rocprof_counters.txt; then pmcpass e SQ_INST_CYCLES_VALU SQ_INSTS_VALU; else true; fi; } && \
-  DIRS="$OUT/pmc_a $OUT/pmc_b $OUT/pmc_c $OUT/pmc_d" && \
+  DIRS="$OUT/pmc_a $OUT/pmc_b $OUT/pmc_c $OUT/pmc_d $OUT/pmc_f" && \
   { [ -d $OUT/pmc_e ] && DIRS="$DIRS $OUT/pmc_e"; true; } && \
   python3 tools/pmc_json.py $OUT/pmc_c2.json $DIRS --workload c2 --frames 4 --skip 1 --session $TAG \
     --engine $(python3 -c "
