@@ -236,6 +236,12 @@ rtx_status rtx_count_work(rtx_context* ctx, uint64_t seed, uint64_t counts[RTX_N
  * option "kernel_events" = 1 before the call).  Waits for those events. */
 rtx_status rtx_kernel_time(rtx_context* ctx, double* total_ms, int32_t* launches);
 
+/* Bounce-level engine statistics of the last render call (summed over its
+ * batches): out[0] camera samples re-rendered by the lanes engine (buffer
+ * overflow), out[1] child rays that found no room, out[2 + d] rays of tree
+ * level d (d = 0 .. 64).  Synchronous.  Zeros for the lanes engine. */
+rtx_status rtx_level_stats(rtx_context* ctx, int64_t* out, int32_t n);
+
 /* Kernel-variant control for experiments; 0 = default. */
 rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
 rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
@@ -246,7 +252,11 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          -1 = as many as fit), "force_stack" (per-lane ray-stack bucket), "postpone" (hierarchy walks
          still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never), "tile_order" (1 expensive
          8x8 tiles first by a primary-hit probe, 0 row-major, -1 [default] = 1 up to 512 spheres; the order
-         changes no bit), "kernel_events" (1: time the ray-tree launches, rtx_kernel_time). */
+         changes no bit), "kernel_events" (1: time the ray-tree launches, rtx_kernel_time),
+         "engine" (0 persistent lanes: one camera sample's ray tree per lane; 1 bounce levels: one launch
+         per tree level, one ray per lane; same bits), "lv_batch" (bounce levels: camera samples per batch,
+         2^23), "lv_stage_pct" / "lv_rec_pct" (bounce-level buffer capacities in % of a batch's samples,
+         250 / 800; samples that overflow them are re-rendered by the lanes engine, same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

@@ -94,6 +94,7 @@ SIGNATURES = [
     ("rtx_count_work", _I, [_P, _U64, C.POINTER(C.c_uint64)]),
     ("rtx_set_option", _I, [_P, C.c_char_p, C.c_int64]),
     ("rtx_get_option", _I, [_P, C.c_char_p, C.POINTER(C.c_int64)]),
+    ("rtx_level_stats", _I, [_P, C.POINTER(C.c_int64), _I]),
     ("rtx_kernel_time", _I, [_P, _DP, C.POINTER(C.c_int32)]),
     ("rtx_vec3_from_a", Vec3T, [_D, _D, _D]),
     ("rtx_vec3_r", _D, [Vec3T]),

@@ -70,6 +70,10 @@ struct rtx_context {
   int64_t opt_tile_order = -1;       // 1: expensive tiles first (k_tile_cost/k_tile_sort), 0: natural order, -1: auto
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
   int64_t opt_engine = 0;            // 0: persistent lanes (per-lane LIFO ray tree), 1: bounce levels
+  int64_t opt_lv_batch = 1 << 23;    // bounce levels: level-0 items (camera samples) per batch
+  int64_t opt_lv_stage_pct = 250;    // bounce levels: ray records per staging buffer, % of the batch items
+  int64_t opt_lv_rec_pct = 800;      // bounce levels: tree records of a batch (all levels), % of the batch items
+  unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
   // rtx_kernel_time: event pairs around each ray-tree kernel launch of the last render call
@@ -353,6 +357,7 @@ void rtx_context_destroy(rtx_context* c) {
   hipFree(c->d_scratch);
   hipFree(c->d_stk);
   hipFree(c->d_work);
+  hipFree(c->d_lvstats);
   for (hipEvent_t ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
   delete c;
@@ -364,7 +369,8 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"engine", c->opt_engine},       {"force_stack", c->opt_force_stack}, {"bvh", c->opt_bvh},
       {"bvh_sah", c->opt_bvh_sah},     {"bvh_min", c->opt_bvh_min},         {"postpone", c->opt_postpone},
       {"lds_stack", c->opt_lds_stack}, {"tile_order", c->opt_tile_order},   {"sphere_src", c->opt_sphere_src},
-      {"kernel_events", c->opt_kernel_events}};
+      {"kernel_events", c->opt_kernel_events}, {"lv_batch", c->opt_lv_batch},
+      {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -411,6 +417,16 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "tile_order")) {        // 1: expensive tiles first; 0: natural (row-major) tile order
     if (value < -1 || value > 1) return fail(c, RTX_EINVAL, "tile_order must be -1, 0 or 1");
     c->opt_tile_order = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_batch")) {          // bounce levels: camera samples per batch
+    if (value < 1 || value > (1 << 28)) return fail(c, RTX_EINVAL, "lv_batch must be in [1, 2^28]");
+    c->opt_lv_batch = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_stage_pct") || !strcmp(key, "lv_rec_pct")) {   // bounce-level buffer capacities
+    if (value < 1 || value > 10000) return fail(c, RTX_EINVAL, "%s must be in [1, 10000]", key);
+    (!strcmp(key, "lv_stage_pct") ? c->opt_lv_stage_pct : c->opt_lv_rec_pct) = value;
     return RTX_OK;
   }
   if (!strcmp(key, "kernel_events")) {     // 1: HIP events around the ray-tree launches (rtx_kernel_time)
@@ -746,9 +762,74 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
 // allocated stream-ordered (the device's default pool keeps the memory, so
 // after the first frame this costs no hipMalloc) and freed after the launch,
 // so launches of one context on different streams never share them.
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// The bounce-level engine can take this camera: its levels and child slots.
+static bool levels_engine(const rtx_context* c) {
+  return c->opt_engine == 1 && c->cam.depth <= LV_MAXL && c->cam.pt + 2 <= 16 && c->scene.n_light <= 255;
+}
+
+// render_region for the bounce-level engine: batches of
+// 8x8 tiles, one launch per tree level, the trees reduced by k_tree_finalize.
+// Buffers for one batch, stream-ordered from the device pool like the lanes
+// engine's: staging (2 x lv_stage_pct % of the batch items x 96 B), tree
+// records (lv_rec_pct % x 32 B with one light), the re-render list.
+static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_t stream) {
+  const size_t npx = (size_t)p.nx * p.nrows;
+  const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
+  const int per_tile = 64 * p.pre;
+  const int batch_tiles = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, tiles));
+  // level-0 items of one batch: pass 0 (tiles) or pass 1 (>= one pixel's extra samples)
+  const size_t n0 = std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, p.max_samples - p.pre));
+  const size_t scap = std::max<size_t>(64, n0 * (size_t)c->opt_lv_stage_pct / 100);
+  const size_t lcap = std::max<size_t>(n0, n0 * (size_t)c->opt_lv_rec_pct / 100);
+  if (scap > UINT32_MAX / 2 || lcap > UINT32_MAX / 2)
+    return fail(c, RTX_EINVAL, "bounce-level buffers exceed 2^31 records: lower lv_batch");
+  const int rec_bytes = levels_rec_bytes(c->scene.n_light);
+  const size_t sz_ctl = al256(sizeof(LevelCtl)), sz_redo = al256(n0 * 4), sz_smp = al256(n0 * 32),
+               sz_stage = al256(scap * RAY_BYTES), sz_rec = al256(lcap * (size_t)rec_bytes),
+               sz_extra = al256((npx + 64) * 4);
+  const size_t total = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_extra;
+  if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
+  HIPCHK(c, hipMemsetAsync(c->d_lvstats, 0, sizeof(unsigned long long) * (LV_MAXL + 3), stream));
+  char* buf = nullptr;
+  HIPCHK(c, hipMallocAsync((void**)&buf, total, stream));
+  char* q = buf;
+  p.lv_ctl = (LevelCtl*)q;                  q += sz_ctl;
+  p.lv_redo_of = (int32_t*)q;               q += sz_redo;
+  p.lv_redo_list = (int32_t*)q;             q += sz_redo;
+  p.lv_redo_smp = (double*)q;               q += sz_smp;
+  p.lv_stage[0] = (double*)q;               q += sz_stage;
+  p.lv_stage[1] = (double*)q;               q += sz_stage;
+  p.lv_rec = q;                             q += sz_rec;
+  p.extra_count = (int32_t*)q;
+  p.extra_list = p.extra_count + 64;
+  p.lv_scap = (uint32_t)scap;
+  p.lv_lcap = (uint32_t)lcap;
+  p.lv_rec_bytes = rec_bytes;
+  p.lv_acc = c->d_lvstats;
+  p.samples = nullptr;
+  KernelEvents kev{c->ev, 0, rtx_context::MAX_EV};
+  if (c->opt_kernel_events && !c->ev[0])
+    for (int k = 0; k < 2 * rtx_context::MAX_EV; k++) HIPCHK(c, hipEventCreate(&c->ev[k]));
+  const hipError_t e = launch_levels(p, sph_mode(c), maxs, std::max(1, c->cam.depth), batch_tiles, stream,
+                                     c->opt_kernel_events ? &kev : nullptr);
+  if (c->opt_kernel_events) c->n_ev = kev.n;
+  const hipError_t f = hipFreeAsync(buf, stream);
+  HIPCHK(c, e);
+  HIPCHK(c, f);
+  return RTX_OK;
+}
+
 static rtx_status render_region(rtx_context* c, KParams& p, bool count, int maxs, hipStream_t stream) {
   const size_t npx = (size_t)p.nx * p.nrows;
   if (npx == 0) return RTX_OK;
+  if (!count && levels_engine(c)) {
+    const size_t padded = (size_t)((p.nx + 7) / 8) * ((p.nrows + 7) / 8) * 64;
+    if (padded * (size_t)std::max(p.pre, p.max_samples) > (size_t)INT32_MAX)
+      return fail(c, RTX_EINVAL, "%zu pixels x samples exceed the 2^31 work items of one launch", npx);
+    return render_levels(c, p, maxs, stream);
+  }
   const size_t ms = (size_t)std::max(p.pre, p.max_samples);
   // Work items are 32-bit on the device: (8x8-padded pixels) x samples must fit.
   const size_t padded = (size_t)((p.nx + 7) / 8) * ((p.nrows + 7) / 8) * 64;
@@ -829,6 +910,18 @@ rtx_status rtx_render_tiles_device(rtx_context* c, int32_t tile_rows, int32_t ra
   p.out = d_packed;
   p.stride = (size_t)c->cam.width * 3;
   return render_region(c, p, false, maxs, (hipStream_t)stream);
+}
+
+rtx_status rtx_level_stats(rtx_context* c, int64_t* out, int32_t n) {
+  if (!c || !out || n < 0) return fail(c, RTX_EINVAL, "bad arguments");
+  HIPCHK(c, hipSetDevice(c->device));
+  unsigned long long v[LV_MAXL + 3] = {0};
+  if (c->d_lvstats) {
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(v, c->d_lvstats, sizeof v, hipMemcpyDeviceToHost));
+  }
+  for (int k = 0; k < n; k++) out[k] = k < LV_MAXL + 3 ? (int64_t)v[k] : 0;
+  return RTX_OK;
 }
 
 rtx_status rtx_kernel_time(rtx_context* c, double* total_ms, int32_t* launches) {

@@ -16,6 +16,16 @@ struct ErrState {
   unsigned long long first[5];     // per ERR_ code (rtx_vec3.h): min key (pixels: x*H + y, render_sync order; rays: index)
 };
 
+// Bounce-level engine: one launch per tree level; the device
+// counts of every level and the work claims of each launch.
+constexpr int LV_MAXL = 64;                     // levels (= trace_depth) the engine supports
+struct LevelCtl {
+  uint32_t count[LV_MAXL + 1];                  // rays of level d (count[0]: level-0 items of the batch)
+  uint32_t claim[LV_MAXL + 1];                  // 64-ray chunks claimed by the level-d launch
+  uint32_t redo_n;                              // level-0 items handed to the lanes engine (capacity overflow)
+  uint32_t dropped;                             // child rays that found no room (diagnostic)
+};
+
 struct KParams {
   SceneDev scene;                  // by value: read by scalar loads from the kernarg segment
   const CameraDev* cam;            // device copy (uploaded by rtx_camera_set)
@@ -48,6 +58,21 @@ struct KParams {
   // SRC_PIXELS: tile visiting order (k_tile_cost + k_tile_sort), null = natural
   int32_t* tile_order;
   int32_t* tile_cls;
+  // bounce-level engine: one batch = pass 0 (the pre samples of the pixels of
+  // tiles [lv_t0, lv_t0 + lv_tiles)) or pass 1 (the extra samples of extra-list
+  // entries [lv_e0, lv_e0 + lv_entries)); level-0 item k of the batch is
+  // decode_item(k); trees are stored per level in lv_rec (lv_rec_bytes each).
+  int32_t lv_pass, lv_t0, lv_tiles, lv_e0, lv_entries;
+  uint32_t lv_scap;                // ray records per staging buffer (levels >= 1)
+  uint32_t lv_lcap;                // tree records in lv_rec
+  int32_t lv_rec_bytes;
+  LevelCtl* lv_ctl;
+  double* lv_stage[2];             // level d reads lv_stage[d & 1], writes lv_stage[(d + 1) & 1]
+  char* lv_rec;
+  int32_t* lv_redo_of;             // per level-0 item: -1, or its entry in lv_redo_list
+  int32_t* lv_redo_list;           // level-0 items re-rendered by the lanes engine (SRC_LIST)
+  double* lv_redo_smp;             // their sample records {r, g, b, first raise}
+  unsigned long long* lv_acc;      // per call: {redo_n, dropped, count[0..LV_MAXL]} summed over batches (or null)
 };
 
 // Where the sphere walk reads its records:
@@ -71,6 +96,17 @@ int stack_bucket(int need);
 // linearly (the counters are the reference's brute-force events).
 hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t s, KernelEvents* kev = nullptr);
 hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s);
+// Camera#render_at over the region of `p` with the bounce-level engine: nlev =
+// trace_depth level launches per batch of `batch_tiles` 8x8 tiles (pass 0) or
+// of batch_tiles * 64 * pre / (max - pre) extra-list entries (pass 1).  The
+// lv_* buffers of `p` are the caller's: lv_redo_of / lv_rec / staging sized for
+// batch_tiles * 64 * pre level-0 items; lanes-engine buffers (stk_glb) too, for
+// the overflow re-render.
+hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tiles, hipStream_t s,
+                         KernelEvents* kev = nullptr);
+// Tree-record bytes for a scene with n_light lights (one leaf per fired light).
+int levels_rec_bytes(int n_light);
+constexpr size_t RAY_BYTES = 96;                // staged ray record of the bounce-level engine
 hipError_t launch_path_trace(KParams p, hipStream_t s);
 int resolve_mode(const SceneDev& S, int mode);
 // LDS bytes a hierarchy workgroup needs (nodes + leaf records + traversal

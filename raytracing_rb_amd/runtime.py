@@ -135,6 +135,16 @@ class Renderer:
         """Name of the ray-tree engine the next render uses (option "engine")."""
         return self.ENGINES[self.get_option("engine")]
 
+    def level_stats(self):
+        """Bounce-level engine statistics of the last render call: {"redo", "dropped", "rays": [per level]}."""
+        n = 2 + 65
+        out = (C.c_int64 * n)()
+        self._check(self.lib.rtx_level_stats(self.h, out, n))
+        rays = list(out[2:])
+        while rays and rays[-1] == 0:
+            rays.pop()
+        return {"redo": out[0], "dropped": out[1], "rays": rays}
+
     def kernel_time(self):
         """(total ms, launches) of the ray-tree kernel launches of the last render
         call (HIP events on the launch stream; needs set_option("kernel_events", 1))."""

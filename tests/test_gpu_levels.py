@@ -1,0 +1,173 @@
+"""The bounce-level engine (option "engine" = 1) against the
+oracle and against the lanes engine.
+
+The two engines run the same binary64 operations on every ray and sum each
+camera sample's leaves in trace_sync's order, so their frames must be
+identical bit for bit, at every size, batch size and buffer
+capacity (overflowing samples are re-rendered by the lanes engine).
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, SCENES
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-4          # north-star tolerance, per channel
+MAXABS_TOL = 1e-9
+
+
+def _scene(world, camera, **ov):
+    from raytracing_rb_amd import config
+    return config.load_scene(os.path.join(SCENES, world), os.path.join(SCENES, camera), camera_overrides=ov)
+
+
+def _renderer(sd, cd, engine, **opts):
+    from raytracing_rb_amd.runtime import Renderer
+    r = Renderer(sd, cd, device=0)
+    r.set_option("engine", engine)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    return r
+
+
+def _same(a, b):
+    """Bit-identical frames (also -0.0 vs 0.0 and NaN payloads)."""
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+def _check(gpu_fb, ref, ok=None, min_exact=0.9):
+    ok = np.ones(ref.shape[:2], bool) if ok is None else ok
+    d = (gpu_fb - ref)[ok]
+    rms = np.sqrt((d ** 2).mean(axis=0))
+    assert (rms <= RMS_TOL).all(), rms
+    assert np.abs(d).max() <= MAXABS_TOL, np.abs(d).max()
+    exact = np.mean(np.all(gpu_fb == ref, axis=-1)[ok])
+    assert exact >= min_exact, exact
+
+
+SCENES_SMALL = [
+    ("c1_world.yml", "c1_camera.yml", dict(width=192, height=108)),
+    ("c0_world.yml", "camera.yml", dict(width=96, height=54)),
+    ("c2_world.yml", "c2_camera.yml", dict(width=160, height=90)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=64, height=36)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, pre_sample_times=3, max_sample_times=2,
+                                             variant_threshold=0.0)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, pre_sample_times=2, max_sample_times=5,
+                                             variant_threshold=0.0)),
+    ("c2_world.yml", "c2_camera.yml", dict(width=48, height=27, pre_sample_times=3, max_sample_times=7,
+                                           variant_threshold=1e9)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=33, height=19, trace_depth=1)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=33, height=19, trace_depth=0)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=33, height=19, monte_carlo_diffusion_times=3, trace_depth=4)),
+]
+
+
+@pytest.mark.parametrize("world,camera,ov", SCENES_SMALL)
+def test_levels_bit_identical_to_lanes_and_match_oracle(gpu, world, camera, ov):
+    from oracle.c_oracle import Oracle
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=3)
+    r = _renderer(sd, cd, 1)
+    lv = r.render(seed=3)
+    assert _same(lv, lanes)
+    st = r.level_stats()
+    assert st["redo"] == 0 and st["dropped"] == 0
+    ref, status, rc = Oracle(sd, cd).render(seed=3)
+    _check(lv, ref, status == 0)
+
+
+@pytest.mark.parametrize("name", ["c1_64x36", "c0_48x27", "c2_32x18", "mix_24x14", "c4_48x27"])
+def test_levels_match_golden(gpu, name):
+    if name == "c4_48x27":
+        import sys
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import make_scenes
+        make_scenes.ensure_c4()
+    z = np.load(os.path.join(GOLDEN, "frame_%s.npz" % name))
+    sd, cd = _scene(str(z["world"]), str(z["camera"]), **eval(str(z["overrides"]), {}))
+    fb = _renderer(sd, cd, 1).render(seed=int(z["seed"]))
+    _check(fb, z["frame"], z["status"] == 0)
+
+
+@pytest.mark.parametrize("opts", [
+    dict(lv_batch=512),                                  # many batches (8x8 tiles x 4 samples = 256 per tile)
+    dict(lv_batch=1),                                    # one tile per batch
+    dict(lv_stage_pct=5),                                # staging overflow: re-rendered by the lanes engine
+    dict(lv_rec_pct=101),                                # tree-record overflow at level 1
+    dict(lv_batch=1000, lv_stage_pct=20, lv_rec_pct=150),
+])
+def test_levels_batches_and_overflow_change_no_bit(gpu, opts):
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
+    lanes = _renderer(sd, cd, 0).render(seed=5)
+    r = _renderer(sd, cd, 1, **opts)
+    lv = r.render(seed=5)
+    assert _same(lv, lanes)
+    st = r.level_stats()
+    if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
+        assert st["redo"] > 0, st                         # the overflow path ran
+    assert sum(st["rays"]) > 0
+
+
+def test_levels_adaptive_extras_batched(gpu):
+    """render_at's extra samples (camera.rb:86-97) in several pass-1 batches."""
+    sd, cd = _scene("mix_world.yml", "mix_camera.yml", width=64, height=36, pre_sample_times=2,
+                    max_sample_times=6, variant_threshold=1e-4)
+    lanes = _renderer(sd, cd, 0).render(seed=9)
+    for opts in (dict(), dict(lv_batch=300), dict(lv_batch=64, lv_stage_pct=30)):
+        assert _same(_renderer(sd, cd, 1, **opts).render(seed=9), lanes), opts
+
+
+def test_levels_c2_full_frame_identical_to_lanes(gpu):
+    """C2 (the metric config) at full 1920x1080, 4xAA, depth 5: every pixel of
+    the bounce-level frame equals the lanes engine's, no sample overflowed."""
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml")
+    lanes = _renderer(sd, cd, 0).render()
+    r = _renderer(sd, cd, 1)
+    lv = r.render()
+    assert _same(lv, lanes)
+    st = r.level_stats()
+    assert st["redo"] == 0 and st["rays"][0] == 32400 * 256, st
+
+
+def test_levels_tiles_and_subregions(gpu):
+    import torch
+    from raytracing_rb_amd import tiles
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=200, height=77)
+    r = _renderer(sd, cd, 1)
+    full = r.render()
+    assert _same(full, _renderer(sd, cd, 0).render())
+    for n in (2, 3, 8):
+        R = r.rows_per_rank(8, n)
+        packed = torch.zeros((n * R, 200, 3), dtype=torch.float64, device="cuda")
+        for k in range(n):
+            r.render_tiles_device(packed[k * R:(k + 1) * R].data_ptr(), 8, k, n)
+        r.sync()
+        assert _same(tiles.unpack(packed, 77, 8, n).cpu().numpy(), full), n
+    out = torch.zeros((20, 30, 3), dtype=torch.float64, device="cuda")
+    r.render_device(out.data_ptr(), x0=10, y0=5, x1=40, y1=25)
+    r.sync()
+    assert _same(out.cpu().numpy(), full[5:25, 10:40])
+    assert _same(r.render_at(33, 17), full[17, 33])
+
+
+def test_levels_color_gt1_error_reported(gpu, tmp_path):
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import RtxError
+    src = open(os.path.join(SCENES, "c1_world.yml")).read()
+    src = src.replace("diffuse_rate:           [0.5, 0.5, 0.5]", "diffuse_rate:           [0.99, 0.99, 0.99]")
+    src = src.replace("ambient:                [0.05, 0.05, 0.05]", "ambient:                [0.3, 0.3, 0.3]", 1)
+    p = tmp_path / "bright.yml"
+    p.write_text(src)
+    sd, cd = config.load_scene(str(p), os.path.join(SCENES, "c1_camera.yml"), camera_overrides=dict(width=24, height=14))
+    msgs = []
+    for engine in (0, 1):
+        with pytest.raises(RtxError) as e:
+            _renderer(sd, cd, engine).render()
+        assert e.value.kind == "color_gt1" and "color greater than 1" in str(e.value)
+        msgs.append(str(e.value))
+    assert msgs[0] == msgs[1]                             # same first erring pixel (render_sync order)
