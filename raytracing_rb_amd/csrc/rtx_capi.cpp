@@ -73,6 +73,7 @@ struct rtx_context {
   int64_t opt_lv_batch = 1 << 23;    // bounce levels: level-0 items (camera samples) per batch
   int64_t opt_lv_stage_pct = 250;    // bounce levels: ray records per staging buffer, % of the batch items
   int64_t opt_lv_rec_pct = 800;      // bounce levels: tree records of a batch (all levels), % of the batch items
+  int64_t opt_lv_floor = 1 << 20;    // bounce levels: at least this many staging and 4x this many tree records
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
@@ -370,7 +371,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"bvh_sah", c->opt_bvh_sah},     {"bvh_min", c->opt_bvh_min},         {"postpone", c->opt_postpone},
       {"lds_stack", c->opt_lds_stack}, {"tile_order", c->opt_tile_order},   {"sphere_src", c->opt_sphere_src},
       {"kernel_events", c->opt_kernel_events}, {"lv_batch", c->opt_lv_batch},
-      {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}};
+      {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -427,6 +428,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_stage_pct") || !strcmp(key, "lv_rec_pct")) {   // bounce-level buffer capacities
     if (value < 1 || value > 10000) return fail(c, RTX_EINVAL, "%s must be in [1, 10000]", key);
     (!strcmp(key, "lv_stage_pct") ? c->opt_lv_stage_pct : c->opt_lv_rec_pct) = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_floor")) {          // bounce levels: minimum buffer records (small frames, deep trees)
+    if (value < 0 || value > (1 << 26)) return fail(c, RTX_EINVAL, "lv_floor must be in [0, 2^26]");
+    c->opt_lv_floor = value;
     return RTX_OK;
   }
   if (!strcmp(key, "kernel_events")) {     // 1: HIP events around the ray-tree launches (rtx_kernel_time)
@@ -781,8 +787,9 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const int batch_tiles = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, tiles));
   // level-0 items of one batch: pass 0 (tiles) or pass 1 (>= one pixel's extra samples)
   const size_t n0 = std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, p.max_samples - p.pre));
-  const size_t scap = std::max<size_t>(64, n0 * (size_t)c->opt_lv_stage_pct / 100);
-  const size_t lcap = std::max<size_t>(n0, n0 * (size_t)c->opt_lv_rec_pct / 100);
+  const size_t fl = (size_t)c->opt_lv_floor;
+  const size_t scap = std::max<size_t>(std::max<size_t>(64, fl), n0 * (size_t)c->opt_lv_stage_pct / 100);
+  const size_t lcap = std::max<size_t>(std::max(n0, 4 * fl), n0 * (size_t)c->opt_lv_rec_pct / 100);
   if (scap > UINT32_MAX / 2 || lcap > UINT32_MAX / 2)
     return fail(c, RTX_EINVAL, "bounce-level buffers exceed 2^31 records: lower lv_batch");
   const int rec_bytes = levels_rec_bytes(c->scene.n_light);

@@ -91,15 +91,17 @@ def test_levels_match_golden(gpu, name):
     z = np.load(os.path.join(GOLDEN, "frame_%s.npz" % name))
     sd, cd = _scene(str(z["world"]), str(z["camera"]), **eval(str(z["overrides"]), {}))
     fb = _renderer(sd, cd, 1).render(seed=int(z["seed"]))
-    _check(fb, z["frame"], z["status"] == 0)
+    # C4 (depth 8, textured ground): more ocml-vs-glibc ulp differences (as test_gpu_bvh)
+    _check(fb, z["frame"], z["status"] == 0, min_exact=0.8 if name == "c4_48x27" else 0.9)
+    assert _same(fb, _renderer(sd, cd, 0).render(seed=int(z["seed"])))
 
 
 @pytest.mark.parametrize("opts", [
     dict(lv_batch=512),                                  # many batches (8x8 tiles x 4 samples = 256 per tile)
     dict(lv_batch=1),                                    # one tile per batch
-    dict(lv_stage_pct=5),                                # staging overflow: re-rendered by the lanes engine
-    dict(lv_rec_pct=101),                                # tree-record overflow at level 1
-    dict(lv_batch=1000, lv_stage_pct=20, lv_rec_pct=150),
+    dict(lv_stage_pct=5, lv_floor=0),                    # staging overflow: re-rendered by the lanes engine
+    dict(lv_rec_pct=101, lv_floor=0),                    # tree-record overflow at level 1
+    dict(lv_batch=1000, lv_stage_pct=20, lv_rec_pct=150, lv_floor=0),
 ])
 def test_levels_batches_and_overflow_change_no_bit(gpu, opts):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
@@ -118,7 +120,7 @@ def test_levels_adaptive_extras_batched(gpu):
     sd, cd = _scene("mix_world.yml", "mix_camera.yml", width=64, height=36, pre_sample_times=2,
                     max_sample_times=6, variant_threshold=1e-4)
     lanes = _renderer(sd, cd, 0).render(seed=9)
-    for opts in (dict(), dict(lv_batch=300), dict(lv_batch=64, lv_stage_pct=30)):
+    for opts in (dict(), dict(lv_batch=300), dict(lv_batch=64, lv_stage_pct=30, lv_floor=0)):
         assert _same(_renderer(sd, cd, 1, **opts).render(seed=9), lanes), opts
 
 
