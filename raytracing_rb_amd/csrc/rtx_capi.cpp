@@ -71,8 +71,8 @@ struct rtx_context {
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
   int64_t opt_engine = 0;            // 0: persistent lanes (per-lane LIFO ray tree), 1: bounce levels
   int64_t opt_lv_batch = 1 << 23;    // bounce levels: level-0 items (camera samples) per batch
-  int64_t opt_lv_stage_pct = 250;    // bounce levels: ray records per staging buffer, % of the batch items
-  int64_t opt_lv_rec_pct = 800;      // bounce levels: tree records of a batch (all levels), % of the batch items
+  int64_t opt_lv_stage_pct = 300;    // bounce levels: ray records per staging buffer, % of the batch items
+  int64_t opt_lv_rec_pct = 1600;      // bounce levels: tree records of a batch (all levels), % of the batch items
   int64_t opt_lv_floor = 1 << 20;    // bounce levels: at least this many staging and 4x this many tree records
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)

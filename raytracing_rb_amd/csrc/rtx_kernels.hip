@@ -1813,9 +1813,11 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
 // Sum of one camera sample's tree (level-0 item `root`) in trace_sync's
 // order: pre-order, children in reverse slot order; `base` = first record of
 // every level.  Returns the first raise (rt_map's first, else rt_reduce's).
+// The walk keeps one pending child range per level below the root in
+// lo[k * st] / hi[k * st], k < sd (LDS, word-major over the block's threads,
+// or a private array with st = 1).
 __device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base, int root, int nlev,
-                                          uint32_t& err_out) {
-  uint32_t lo[LV_MAXL], hi[LV_MAXL];         // pending child ranges, one per level below the root
+                                          uint32_t* lo, uint32_t* hi, int st, int sd, uint32_t& err_out) {
   int sp = 0;
   V3 sum = v3(0.0, 0.0, 0.0);
   uint32_t err = 0;
@@ -1825,36 +1827,36 @@ __device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base
   while (true) {
     const char* rec = p.lv_rec + (size_t)(base[lev] + q) * p.lv_rec_bytes;
     const uint2 hdr = *reinterpret_cast<const uint2*>(rec);
+    const double* lf = reinterpret_cast<const double*>(rec + 8);
+    const double2 l01 = *reinterpret_cast<const double2*>(lf);   // the first leaf, with the header's sector
+    const double l2 = lf[2];
     if (!err) err = hdr.x & 0xffu;
     const int nleaf = (int)(hdr.x >> 8 & 0xffu);
-    const double* lf = reinterpret_cast<const double*>(rec + 8);
-    for (int k = 0; k < nleaf; k++) {        // rt_reduce (ray_tracer.rb:292-298), in emission order
-      sum = vadd(sum, v3(lf[3 * k], lf[3 * k + 1], lf[3 * k + 2]));
+    if (nleaf > 0) {                           // rt_reduce (ray_tracer.rb:292-298), in emission order
+      sum = vadd(sum, v3(l01.x, l01.y, l2));
       if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) gt1 = true;
+      for (int k = 1; k < nleaf; k++) {
+        sum = vadd(sum, v3(lf[3 * k], lf[3 * k + 1], lf[3 * k + 2]));
+        if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) gt1 = true;
+      }
     }
     const uint32_t nch = (uint32_t)__popc(hdr.x >> 16);
-    if (nch && lev + 1 < nlev && sp < LV_MAXL) {
-      lo[sp] = hdr.y;
-      hi[sp] = hdr.y + nch;
+    if (nch && lev + 1 < nlev && sp < sd) {
+      lo[sp * st] = hdr.y;
+      hi[sp * st] = hdr.y + nch;
       sp++;
     }
     // next: the last unvisited child of the deepest pending range (LIFO pop)
-    while (sp > 0 && hi[sp - 1] == lo[sp - 1]) sp--;
+    while (sp > 0 && hi[(sp - 1) * st] == lo[(sp - 1) * st]) sp--;
     if (sp == 0) break;
-    q = --hi[sp - 1];
+    q = --hi[(sp - 1) * st];
     lev = sp;
   }
   err_out = err ? err : (gt1 ? (uint32_t)ERR_COLOR_GT1 : 0u);
   return sum;
 }
 
-// Camera#render_at's reduction (camera.rb:70-99) over the trees of one batch.
-// Pass 0: one thread per pixel of the batch's tiles: its pre samples' trees,
-// the mean and variance test, then the pixel or (max_sample_times > pre) an
-// extra-list entry with the pre mean parked in the output.  Pass 1: one
-// thread per extra-list entry of the batch: (mean * pre + extras) / max.
-__global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
-  __shared__ uint32_t base[LV_MAXL + 1];
+__device__ __forceinline__ void lv_bases(const KParams& p, int nlev, uint32_t* base) {
   if (threadIdx.x == 0) {
     uint32_t b = 0;
     for (int d = 0; d <= nlev && d <= LV_MAXL; d++) {
@@ -1863,92 +1865,134 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
     }
   }
   __syncthreads();
-  const int t = blockIdx.x * 256 + (int)threadIdx.x;
-  const CameraDev& cam = *p.cam;
-  const int pre = p.pre;
-  int px_, row, idx, first_item;
-  if (p.lv_pass == 0) {
-    if (t >= p.lv_tiles * 64) return;
-    const int tiles_x = (p.nx + 7) >> 3;
-    const int tile = p.lv_t0 + (t >> 6), l = t & 63;
-    px_ = (tile % tiles_x) * 8 + ((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));
-    row = (tile / tiles_x) * 8 + (((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4));
-    if (px_ >= p.nx || row >= p.nrows) return;
-    idx = row * p.nx + px_;
-    first_item = (t >> 6) * 64 * pre + l * pre;
-  } else {
-    if (t >= p.lv_entries || p.lv_e0 + t >= *p.extra_count) return;
-    idx = p.extra_list[p.lv_e0 + t];
-    px_ = idx % p.nx;
-    row = idx / p.nx;
-    first_item = t * (p.max_samples - pre);
+}
+
+// One camera sample's colour and first raise: its tree, or the lanes engine's
+// record when the sample overflowed the level buffers.
+__device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, int item, int nlev, uint32_t* lo,
+                                        uint32_t* hi, int st, int sd, uint32_t& e) {
+  const int r = p.lv_redo_of[item];
+  if (r >= 0) {
+    const double* q = p.lv_redo_smp + (size_t)r * 4;
+    e = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
+    return v3(q[0], q[1], q[2]);
   }
+  return lv_tree_sum(p, base, item, nlev, lo, hi, st, sd, e);
+}
+
+// Camera#render_at's reduction (camera.rb:70-99) of pass 0: one 256-thread
+// block per 8x8 tile of the batch.  The block's threads sum the tile's
+// 64 x pre sample trees (item order (pixel, sample): a wave's trees are
+// neighbours), park colour and raise in LDS, then 64 threads do the pixels:
+// mean in sample order, the variance test, then the pixel or (max_sample_times
+// > pre) an extra-list entry with the pre mean parked in the output.
+// Dynamic LDS: SD * 2 words of walk stack per thread, then 64 * pre samples.
+template <int SD>
+__global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
+  extern __shared__ uint32_t lds_fin[];
+  lv_bases(p, nlev, base);
+  const int pre = p.pre;
+  const int slot = blockIdx.x;                 // tile of the batch
+  uint32_t* lo = lds_fin + threadIdx.x;
+  uint32_t* hi = lo + SD * 256;
+  double* scol = reinterpret_cast<double*>(lds_fin + 2 * SD * 256);   // 64 * pre * 3
+  uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
+  uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];  // deep trees: private stack
+  const int n_items = 64 * pre;
+  const int item0 = slot * n_items;
+  for (int it = (int)threadIdx.x; it < n_items; it += 256) {
+    const ItemPos ip = decode_item(p, item0 + it);
+    if (!ip.valid) continue;
+    uint32_t e = 0;
+    const V3 c = SD > 16 ? lv_sample(p, base, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
+                         : lv_sample(p, base, item0 + it, nlev, lo, hi, 256, SD, e);
+    scol[3 * it] = c.x;
+    scol[3 * it + 1] = c.y;
+    scol[3 * it + 2] = c.z;
+    serr[it] = e;
+  }
+  __syncthreads();
+  const int l = (int)threadIdx.x;
+  if (l >= 64) return;
+  const int tiles_x = (p.nx + 7) >> 3;
+  const int tile = p.lv_t0 + slot;
+  const int px_ = (tile % tiles_x) * 8 + ((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));
+  const int row = (tile / tiles_x) * 8 + (((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4));
+  if (px_ >= p.nx || row >= p.nrows) return;
   const int y = row_to_y(p, row);
+  const CameraDev& cam = *p.cam;
   if (y >= cam.height) return;
   const int x = p.x0 + px_;
-  auto sample_of = [&](int item, uint32_t& e) -> V3 {
-    const int r = p.lv_redo_of[item];
-    if (r >= 0) {                              // re-rendered by the lanes engine
-      const double* q = p.lv_redo_smp + (size_t)r * 4;
-      e = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
-      return v3(q[0], q[1], q[2]);
-    }
-    return lv_tree_sum(p, base, item, nlev, e);
-  };
-  double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
+  const double* sc = scol + 3 * l * pre;
   uint32_t err = 0;
-  if (p.lv_pass == 0) {
-    V3 smp[16];                                // pre_sample_times <= 16 (rtx_camera_set)
-    V3 avg = v3(0.0, 0.0, 0.0);
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      if (j < pre) {
-        uint32_t e = 0;
-        smp[j] = sample_of(first_item + j, e);
-        if (!err) err = e;
-        avg = vadd(avg, smp[j]);
-      }
-    }
-    avg = vdiv(avg, (double)pre);
-    double variance = 0.0;                     // camera.rb:80-85
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      if (j < pre) {
-        const V3 dd = vsub(smp[j], avg);
-        double mx = dd.x;
-        if (dd.y > mx) mx = dd.y;
-        if (dd.z > mx) mx = dd.z;
-        variance += mx * mx;                   // .max ** 2
-      }
-    }
-    variance /= (double)pre;
-    if (variance >= cam.variant_threshold) {
-      if (p.max_samples > pre) {               // extra samples: pass 1 finishes this pixel
-        p.extra_list[atomicAdd(p.extra_count, 1)] = idx;
-        o[0] = avg.x;
-        o[1] = avg.y;
-        o[2] = avg.z;
-        if (err) record_error(p.err, err, px_key(x, y, cam.height));
-        return;
-      }
-      avg = vdiv(vadd(vsc(avg, (double)pre), v3(0.0, 0.0, 0.0)), (double)p.max_samples);
-    }
-    o[0] = avg.x;
-    o[1] = avg.y;
-    o[2] = avg.z;
-  } else {
-    const V3 avg = v3(o[0], o[1], o[2]);      // the pre mean parked by pass 0
-    V3 cv = v3(0.0, 0.0, 0.0);
-    for (int j = pre; j < p.max_samples; j++) {
-      uint32_t e = 0;
-      cv = vadd(cv, sample_of(first_item + (j - pre), e));
-      if (!err) err = e;
-    }
-    const V3 r = vdiv(vadd(vsc(avg, (double)pre), cv), (double)p.max_samples);
-    o[0] = r.x;
-    o[1] = r.y;
-    o[2] = r.z;
+  V3 avg = v3(0.0, 0.0, 0.0);
+  for (int j = 0; j < pre; j++) {
+    avg = vadd(avg, v3(sc[3 * j], sc[3 * j + 1], sc[3 * j + 2]));
+    if (!err) err = serr[l * pre + j];
   }
+  avg = vdiv(avg, (double)pre);
+  double variance = 0.0;                       // camera.rb:80-85
+  for (int j = 0; j < pre; j++) {
+    const V3 dd = vsub(v3(sc[3 * j], sc[3 * j + 1], sc[3 * j + 2]), avg);
+    double mx = dd.x;
+    if (dd.y > mx) mx = dd.y;
+    if (dd.z > mx) mx = dd.z;
+    variance += mx * mx;                       // .max ** 2
+  }
+  variance /= (double)pre;
+  double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
+  if (variance >= cam.variant_threshold) {
+    if (p.max_samples > pre) {                 // extra samples: pass 1 finishes this pixel
+      p.extra_list[atomicAdd(p.extra_count, 1)] = row * p.nx + px_;
+      o[0] = avg.x;
+      o[1] = avg.y;
+      o[2] = avg.z;
+      if (err) record_error(p.err, err, px_key(x, y, cam.height));
+      return;
+    }
+    avg = vdiv(vadd(vsc(avg, (double)pre), v3(0.0, 0.0, 0.0)), (double)p.max_samples);
+  }
+  o[0] = avg.x;
+  o[1] = avg.y;
+  o[2] = avg.z;
+  if (err) record_error(p.err, err, px_key(x, y, cam.height));
+}
+
+// Pass 1: one thread per extra-list entry of the batch: (pre mean * pre +
+// the extra samples in order) / max_sample_times.
+template <int SD>
+__global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
+  extern __shared__ uint32_t lds_fin[];
+  lv_bases(p, nlev, base);
+  uint32_t* lo = lds_fin + threadIdx.x;
+  uint32_t* hi = lo + SD * 256;
+  uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];
+  const int t = blockIdx.x * 256 + (int)threadIdx.x;
+  if (t >= p.lv_entries || p.lv_e0 + t >= *p.extra_count) return;
+  const int idx = p.extra_list[p.lv_e0 + t];
+  const int px_ = idx % p.nx, row = idx / p.nx;
+  const int y = row_to_y(p, row);
+  const CameraDev& cam = *p.cam;
+  if (y >= cam.height) return;
+  const int x = p.x0 + px_;
+  const int pre = p.pre, n_extra = p.max_samples - pre;
+  double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
+  const V3 avg = v3(o[0], o[1], o[2]);         // the pre mean parked by pass 0
+  V3 cv = v3(0.0, 0.0, 0.0);
+  uint32_t err = 0;
+  for (int j = 0; j < n_extra; j++) {
+    uint32_t e = 0;
+    const int item = t * n_extra + j;
+    cv = vadd(cv, SD > 16 ? lv_sample(p, base, item, nlev, lo_p, hi_p, 1, LV_MAXL, e)
+                          : lv_sample(p, base, item, nlev, lo, hi, 256, SD, e));
+    if (!err) err = e;
+  }
+  const V3 r = vdiv(vadd(vsc(avg, (double)pre), cv), (double)p.max_samples);
+  o[0] = r.x;
+  o[1] = r.y;
+  o[2] = r.z;
   if (err) record_error(p.err, err, px_key(x, y, cam.height));
 }
 
@@ -2321,6 +2365,24 @@ static hipError_t launch_level_mode(const KParams& p, int mode, int level, long 
   return hipErrorInvalidValue;
 }
 
+template <int SD>
+static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStream_t s) {
+  const size_t stack = SD > 16 ? 0 : (size_t)SD * 2 * 256 * 4;
+  if (q.lv_pass == 0) {                        // n = tiles of the batch
+    const size_t lds = stack + (size_t)64 * q.pre * 28;
+    hipLaunchKernelGGL(k_tree_finalize<SD>, dim3((unsigned)n), dim3(256), lds, s, q, nlev);
+  } else {                                     // n = extra-list entries of the batch
+    hipLaunchKernelGGL(k_tree_finalize_extra<SD>, dim3((unsigned)((n + 255) / 256)), dim3(256), stack, s, q, nlev);
+  }
+  return hipGetLastError();
+}
+
+static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t s) {
+  if (nlev <= 8) return launch_finalize_sd<8>(q, nlev, n, s);
+  if (nlev <= 16) return launch_finalize_sd<16>(q, nlev, n, s);
+  return launch_finalize_sd<64>(q, nlev, n, s);
+}
+
 // One batch: reset, the levels, the lanes-engine re-render of overflowed
 // samples (exits at once when there are none), the tree reduction.
 static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_max, int fin_threads, hipStream_t s,
@@ -2331,10 +2393,7 @@ static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_ma
   for (int d = 0; d < nlev && e == hipSuccess; d++)
     e = launch_level_mode(q, mode, d, d == 0 ? (long)n0_max : (long)q.lv_scap, s, kev);
   if (e == hipSuccess) e = launch_src<SRC_LIST>(q, mode, false, maxs, n0_max, s);
-  if (e == hipSuccess && fin_threads > 0) {
-    hipLaunchKernelGGL(k_tree_finalize, dim3((unsigned)((fin_threads + 255) / 256)), dim3(256), 0, s, q, nlev);
-    e = hipGetLastError();
-  }
+  if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
   if (e == hipSuccess && q.lv_acc) {
     hipLaunchKernelGGL(k_level_acc, dim3(1), dim3(128), 0, s, q.lv_ctl, q.lv_acc);
     e = hipGetLastError();
@@ -2357,7 +2416,7 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
     q.lv_t0 = t0;
     q.lv_tiles = std::min(batch_tiles, tiles - t0);
     q.lv_e0 = q.lv_entries = 0;
-    e = level_batch(q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles * 64, s, kev);
+    e = level_batch(q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles, s, kev);
   }
   if (e != hipSuccess || p.max_samples <= p.pre) return e;
   // extra samples of the pixels the variance test listed (count on the device)

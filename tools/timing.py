@@ -57,11 +57,15 @@ def main():
             e1.synchronize()
             ts.append(e0.elapsed_time(e1))
         r.sync(s.cuda_stream)
+        st = r.level_stats() if r.engine() == "levels" else None
         r.close()
         ts.sort()
         sha = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
         print("%-8s %-40s min %9.3f ms  median %9.3f ms  %8.2f Mpix/s  sha %s" % (
             a.scene, o, ts[0], ts[len(ts) // 2], cd.width * cd.height / ts[len(ts) // 2] / 1e3, sha), flush=True)
+        if st:
+            print("         levels: rays per level %s, redo %d, dropped %d" % (st["rays"], st["redo"], st["dropped"]),
+                  flush=True)
 
 
 if __name__ == "__main__":
