@@ -253,7 +253,7 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never), "tile_order" (1 expensive
          8x8 tiles first by a primary-hit probe, 0 row-major, -1 [default] = 1 up to 512 spheres; the order
          changes no bit), "kernel_events" (1: time the ray-tree launches, rtx_kernel_time),
-         "engine" (0 persistent lanes: one camera sample's ray tree per lane; 1 bounce levels: one launch
+         "engine" (0 persistent lanes: one camera sample's ray tree per lane; 1 [default] bounce levels: one launch
          per tree level, one ray per lane; same bits), "lv_batch" (bounce levels: camera samples per batch,
          2^23), "lv_stage_pct" / "lv_rec_pct" (bounce-level buffer capacities in % of a batch's samples,
          300 / 1600, and at least "lv_floor" staging / 4 x "lv_floor" tree records, 2^20; samples that

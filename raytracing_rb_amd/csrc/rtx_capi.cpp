@@ -69,7 +69,7 @@ struct rtx_context {
   int64_t opt_postpone = -1;         // query_bvh postponing threshold in lanes (-1: auto by hierarchy size)
   int64_t opt_tile_order = -1;       // 1: expensive tiles first (k_tile_cost/k_tile_sort), 0: natural order, -1: auto
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
-  int64_t opt_engine = 0;            // 0: persistent lanes (per-lane LIFO ray tree), 1: bounce levels
+  int64_t opt_engine = 1;            // 0: persistent lanes (per-lane LIFO ray tree), 1: bounce levels (default: faster, same bits)
   int64_t opt_lv_batch = 1 << 23;    // bounce levels: level-0 items (camera samples) per batch
   int64_t opt_lv_stage_pct = 300;    // bounce levels: ray records per staging buffer, % of the batch items
   int64_t opt_lv_rec_pct = 1600;      // bounce levels: tree records of a batch (all levels), % of the batch items

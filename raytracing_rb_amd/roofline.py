@@ -89,10 +89,16 @@ def hw_fp64(pm, kernel_ms_per_frame):
     flop = wave_flop * lanes
     ach = flop / (kernel_ms_per_frame * 1e-3) / 1e12
     direct = None
-    if "SQ_INSTS_VALU_FLOPS_FP64" in pf:             # the SQ's own FP64 FLOP counters (per lane)
+    if "SQ_INSTS_VALU_FLOPS_FP64" in pf:
+        # The SQ's own FP64 FLOP counter sums FLOP per lane over wave
+        # instructions (measured: it equals 2 FMA + ADD + MUL of the class
+        # counters, profiles/r02e), i.e. it is not lane-weighted either: the
+        # cross-check of `wave_flop`.
         df = pf["SQ_INSTS_VALU_FLOPS_FP64"] + pf.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)
-        direct = {"fp64_flop_per_frame": df, "achieved_tflops": round(df / (kernel_ms_per_frame * 1e-3) / 1e12, 4),
-                  "from": "SQ_INSTS_VALU_FLOPS_FP64 + SQ_INSTS_VALU_FLOPS_FP64_TRANS"}
+        direct = {"wave_flop_per_frame": df, "class_wave_flop_per_frame": wave_flop,
+                  "fp64_flop_per_frame": df * lanes,
+                  "achieved_tflops": round(df * lanes / (kernel_ms_per_frame * 1e-3) / 1e12, 4),
+                  "from": "(SQ_INSTS_VALU_FLOPS_FP64 + SQ_INSTS_VALU_FLOPS_FP64_TRANS) x mean active lanes"}
     return {"achieved_tflops": round(ach, 4), "frac": round(ach / FP64_PEAK_TFLOPS, 5), "direct_counter": direct,
             "method": "sum over FP64 VALU classes of FLOP/lane (FMA 2, ADD/MUL/TRANS 1) x wave instructions "
                       "x mean active lanes",

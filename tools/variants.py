@@ -8,7 +8,7 @@ process); rounds are interleaved across variants (methodology rule 24).
 """
 import glob, json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VDIR = os.path.join(ROOT, "build", "variants")
+VDIR = os.path.join(ROOT, "_variants")       # not under build/: variants must travel to the GPU box
 sys.path.insert(0, ROOT)
 
 CHILD = r"""
