@@ -18,6 +18,8 @@
  *   rtx_render_device     (same, device-resident output, async on a HIP stream)
  *   rtx_render_tiles_device  the per-child work of Camera#render_fork +
  *                          fork_jobs                      src/camera.rb:53-65, src/fork_jobs.rb:5-22
+ *   rtx_render_multi      Camera#render_fork + fork_jobs over the node's GPUs with an RCCL gather
+ *                                                         src/camera.rb:41-68, src/fork_jobs.rb:1-33
  *   rtx_render_at         Camera#render_at(x, y)         src/camera.rb:70-99
  *   rtx_trace             RayTracer#trace_sync(x, y, ray) src/ray_tracer.rb:16-46
  *   rtx_path_trace        RayTracer#path_trace_sync(x, y, ray) src/ray_tracer.rb:181-289 (dead code there)
@@ -180,6 +182,18 @@ rtx_status rtx_render_tiles_device(rtx_context* ctx, int32_t tile_rows, int32_t 
  * Camera#render_fork (camera.rb:41-68) in a single-process, multi-GPU host. */
 rtx_status rtx_render_tiles(rtx_context* ctx, int32_t tile_rows, int32_t rank, int32_t nranks, uint64_t seed,
                             double* packed);
+
+/* Camera#render_fork(path, n) + fork_jobs in one process (camera.rb:41-68,
+ * fork_jobs.rb:5-22): ctxs[k] (each with the same scene and camera uploaded,
+ * one per worker, normally one per GPU) renders rank k's share of the frame
+ * cut into tile_rows-row tiles dealt round-robin; the packed tiles are
+ * gathered to ctxs[0]'s device with ONE grouped RCCL ncclSend/ncclRecv over
+ * xGMI (device copies instead when several contexts share a device),
+ * unpacked there and copied into the caller's host buffer out_rgb (layout of
+ * rtx_render).  Synchronous.  RTX_ERCCL when the collective fails; a rank's
+ * reference raise is returned as in rtx_render. */
+rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, uint64_t seed,
+                            double* out_rgb, size_t row_stride);
 
 /* Number of HIP devices visible to this process (the node's GPUs). */
 int32_t    rtx_device_count(void);

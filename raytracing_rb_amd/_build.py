@@ -22,6 +22,10 @@ FLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fno-fast-math",
          "-shared", "-Wall", "-Wno-unused-result", "-Wno-unused-value"]
 
 
+# RCCL for rtx_render_multi's gather over xGMI (librccl.so ships with ROCm).
+LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+
+
 CLI_SRC = os.path.join(HERE, "cli", "rtx_main.cpp")
 CLI_DEPS = [CLI_SRC] + [os.path.join(HERE, "cli", f) for f in ("yaml_lite.hpp", "png_io.hpp", "scene_load.hpp")] + [
     os.path.join(ROOT, "include", "rtx.h")]
@@ -54,7 +58,7 @@ def build(force=False, verbose=False, out=None, defines=()):
     if not force and out == OUT and not stale():
         return OUT
     # `defines`: NAME[=VALUE] macros; entries starting with "-" are raw compiler flags
-    cmd = [HIPCC] + FLAGS + [d if d.startswith("-") else "-D" + d for d in defines] + ["-o", out + ".tmp"] + SOURCES
+    cmd = [HIPCC] + FLAGS + [d if d.startswith("-") else "-D" + d for d in defines] + ["-o", out + ".tmp"] + SOURCES + LIBS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -45,6 +45,7 @@ struct Opts {
   bool blend = true, dump = false;
   std::map<std::string, double> set;
   std::map<std::string, std::string> remap;
+  std::map<std::string, long long> opt;          // --option key=value: rtx_set_option
 };
 
 // The reference's raise sites surface as this process's error message + exit 1.
@@ -129,39 +130,22 @@ rtx_context* make_context(int device, const Scene& sc, const rtx_camera_desc& ca
   return c;
 }
 
-// Camera#render_fork: worker k of n renders the tiles t with t % n == k on GPU
-// (device + k) % ngpu; the parent scatters the packed rows into the frame.
+// Camera#render_fork (camera.rb:41-68): worker k of n renders the tiles t
+// with t % n == k on GPU (device + k) % ngpu; rtx_render_multi gathers the
+// packed tiles to the first worker's GPU with one RCCL send/recv group (device
+// copies when workers share a GPU) and returns the frame.
 std::vector<double> render_fork(const Opts& o, const Scene& sc, const rtx_camera_desc& cam, int n) {
   const int W = cam.width, H = cam.height;
   const int ngpu = rtx_device_count();
   if (ngpu < 1) die("no GPU visible");
-  const int R = rtx_tiles_rows_per_rank(H, TILE_ROWS, n);
-  std::vector<std::vector<double>> packed(n, std::vector<double>((size_t)R * W * 3));
-  std::vector<std::string> errs(n);
-  std::vector<std::thread> th;
+  std::vector<rtx_context*> ctx(n, nullptr);
+  for (int k = 0; k < n; k++) ctx[k] = make_context((o.device + k) % ngpu, sc, cam);
   for (int k = 0; k < n; k++)
-    th.emplace_back([&, k] {
-      const int dev = (o.device + k) % ngpu;
-      rtx_context* c = nullptr;
-      if (rtx_context_create(dev, &c) != RTX_OK) {
-        errs[k] = "cannot create a context on GPU " + std::to_string(dev);
-        return;
-      }
-      rtx_status s = rtx_scene_upload(c, &sc.desc);
-      if (!s) s = rtx_camera_set(c, &cam);
-      if (!s) s = rtx_render_tiles(c, TILE_ROWS, k, n, o.seed, packed[k].data());
-      if (s) errs[k] = std::string(rtx_status_string(s)) + " (" + rtx_last_error(c) + ")";
-      rtx_context_destroy(c);
-    });
-  for (auto& t : th) t.join();
-  for (int k = 0; k < n; k++)
-    if (!errs[k].empty()) die("worker " + std::to_string(k) + ": " + errs[k]);
+    for (const auto& kv : o.opt) check(ctx[k], rtx_set_option(ctx[k], kv.first.c_str(), kv.second), "option");
   std::vector<double> fb((size_t)W * H * 3);
-  for (int k = 0; k < n; k++)
-    for (int r = 0; r < R; r++) {
-      const int y = ((r / TILE_ROWS) * n + k) * TILE_ROWS + r % TILE_ROWS;
-      if (y < H) memcpy(&fb[(size_t)y * W * 3], &packed[k][(size_t)r * W * 3], sizeof(double) * W * 3);
-    }
+  const rtx_status s = rtx_render_multi(ctx.data(), n, TILE_ROWS, o.seed, fb.data(), (size_t)W * 3);
+  if (s) die(std::string("render_fork: ") + rtx_status_string(s) + " (" + rtx_last_error(ctx[0]) + ")");
+  for (rtx_context* c : ctx) rtx_context_destroy(c);
   return fb;
 }
 
@@ -194,6 +178,10 @@ Opts parse_args(int argc, char** argv) {
       std::string k, v;
       kv(val(), k, v);
       o.remap[k] = v;
+    } else if (a == "--option") {
+      std::string k, v;
+      kv(val(), k, v);
+      o.opt[k] = strtoll(v.c_str(), nullptr, 10);
     } else pos.push_back(a);
   }
   if (!o.decode_png.empty()) return o;
@@ -240,6 +228,7 @@ int main(int argc, char** argv) {
     int workers = 1;
     if (o.mode == "s") {                                           // Camera#render_sync
       rtx_context* c = make_context(o.device, sc, cam);
+      for (const auto& kv : o.opt) check(c, rtx_set_option(c, kv.first.c_str(), kv.second), "option");
       fb.resize((size_t)W * H * 3);
       check(c, rtx_render(c, 0, 0, W, H, o.seed, fb.data(), (size_t)W * 3), "render_sync");
       rtx_context_destroy(c);

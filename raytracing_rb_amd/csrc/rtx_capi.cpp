@@ -6,6 +6,7 @@
 // src/camera.rb:26-34,129-151) with the same operation order, so every
 // constant the device uses has the bits the Ruby code would compute.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <math.h>
 
@@ -77,6 +78,14 @@ struct rtx_context {
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
+  // rtx_render_multi: this context's packed tiles; on the call's first context
+  // also the gathered tiles + frame, and the RCCL clique over the call's devices
+  double* d_multi = nullptr;
+  size_t multi_bytes = 0;
+  double* d_gather = nullptr;
+  size_t gather_bytes = 0;
+  std::vector<int> comm_devs;
+  std::vector<ncclComm_t> comms;
   // rtx_kernel_time: event pairs around each ray-tree kernel launch of the last render call
   static constexpr int MAX_EV = 32;
   hipEvent_t ev[2 * MAX_EV] = {};
@@ -359,6 +368,13 @@ void rtx_context_destroy(rtx_context* c) {
   hipFree(c->d_stk);
   hipFree(c->d_work);
   hipFree(c->d_lvstats);
+  hipFree(c->d_multi);
+  hipFree(c->d_gather);
+  for (size_t k = 0; k < c->comms.size(); k++) {
+    hipSetDevice(c->comm_devs[k]);
+    ncclCommDestroy(c->comms[k]);
+  }
+  hipSetDevice(c->device);
   for (hipEvent_t ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
   delete c;
@@ -1015,6 +1031,98 @@ rtx_status rtx_render_tiles(rtx_context* c, int32_t tile_rows, int32_t rank, int
   if ((s = rtx_render_tiles_device(c, tile_rows, rank, nranks, seed, c->d_scratch, nullptr))) return s;
   HIPCHK(c, hipMemcpy(packed, c->d_scratch, bytes, hipMemcpyDeviceToHost));
   return rtx_sync(c, nullptr);
+}
+
+static rtx_status grow(rtx_context* c, double** buf, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return RTX_OK;
+  hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  HIPCHK(c, hipMalloc((void**)buf, bytes));
+  *cap = bytes;
+  return RTX_OK;
+}
+
+#define NCCLCHK(c, expr)                                                                      \
+  do {                                                                                        \
+    ncclResult_t r_ = (expr);                                                                 \
+    if (r_ != ncclSuccess) return fail(c, RTX_ERCCL, "%s: %s", #expr, ncclGetErrorString(r_)); \
+  } while (0)
+
+rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, uint64_t seed, double* out,
+                            size_t row_stride) {
+  if (!ctxs || n < 1 || !ctxs[0]) return RTX_EINVAL;
+  rtx_context* c0 = ctxs[0];
+  if (!out || tile_rows <= 0) return fail(c0, RTX_EINVAL, "bad arguments");
+  std::vector<int> devs(n);
+  for (int k = 0; k < n; k++) {
+    rtx_context* c = ctxs[k];
+    if (!c || !c->have_scene || !c->have_cam) return fail(c0, RTX_EINVAL, "context %d has no scene or camera", k);
+    if (c->cam.width != c0->cam.width || c->cam.height != c0->cam.height)
+      return fail(c0, RTX_EINVAL, "context %d renders a different image size", k);
+    devs[k] = c->device;
+  }
+  const int W = c0->cam.width, H = c0->cam.height;
+  if (row_stride < (size_t)W * 3) return fail(c0, RTX_EINVAL, "row_stride too small");
+  const int R = rtx_tiles_rows_per_rank(H, tile_rows, n);
+  const size_t count = (size_t)R * W * 3;                      // doubles per rank
+  for (int k = 0; k < n; k++) (void)rtx_sync(ctxs[k], nullptr);   // clear stale device errors
+  // every rank renders its tiles on its own device; the devices run concurrently
+  for (int k = 0; k < n; k++) {
+    rtx_context* c = ctxs[k];
+    HIPCHK(c0, hipSetDevice(c->device));
+    rtx_status s = grow(c, &c->d_multi, &c->multi_bytes, count * sizeof(double));
+    if (!s) s = rtx_render_tiles_device(c, tile_rows, k, n, seed, c->d_multi, nullptr);
+    if (s) return fail(c0, s, "rank %d: %s", k, rtx_last_error(c));
+  }
+  HIPCHK(c0, hipSetDevice(c0->device));
+  rtx_status s = grow(c0, &c0->d_gather, &c0->gather_bytes, ((size_t)n * count + (size_t)W * H * 3) * sizeof(double));
+  if (s) return s;
+  double* gathered = c0->d_gather;
+  double* frame = c0->d_gather + (size_t)n * count;
+  bool distinct = true;
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++) distinct = distinct && devs[a] != devs[b];
+  if (distinct) {
+    // ONE gather to rank 0 over RCCL (xGMI): grouped ncclSend / ncclRecv on
+    // every device's stream, ordered after that device's render.
+    if (c0->comm_devs != devs) {
+      for (size_t k = 0; k < c0->comms.size(); k++) {
+        hipSetDevice(c0->comm_devs[k]);
+        ncclCommDestroy(c0->comms[k]);
+      }
+      c0->comms.assign(n, nullptr);
+      c0->comm_devs.clear();
+      NCCLCHK(c0, ncclCommInitAll(c0->comms.data(), n, devs.data()));
+      c0->comm_devs = devs;
+    }
+    NCCLCHK(c0, ncclGroupStart());
+    for (int k = 0; k < n; k++) {
+      hipSetDevice(devs[k]);
+      NCCLCHK(c0, ncclSend(ctxs[k]->d_multi, count, ncclFloat64, 0, c0->comms[k], nullptr));
+    }
+    hipSetDevice(devs[0]);
+    for (int k = 0; k < n; k++)
+      NCCLCHK(c0, ncclRecv(gathered + (size_t)k * count, count, ncclFloat64, k, c0->comms[0], nullptr));
+    NCCLCHK(c0, ncclGroupEnd());
+  } else {
+    // several ranks on one device (more workers than GPUs): device copies
+    for (int k = 0; k < n; k++) {
+      HIPCHK(c0, hipSetDevice(devs[k]));
+      HIPCHK(c0, hipDeviceSynchronize());
+      HIPCHK(c0, hipMemcpyPeer(gathered + (size_t)k * count, devs[0], ctxs[k]->d_multi, devs[k],
+                               count * sizeof(double)));
+    }
+  }
+  HIPCHK(c0, hipSetDevice(devs[0]));
+  HIPCHK(c0, launch_unpack(gathered, W, H, tile_rows, n, R, frame, (size_t)W * 3, nullptr));
+  HIPCHK(c0, hipMemcpy2D(out, row_stride * sizeof(double), frame, (size_t)W * 3 * sizeof(double),
+                         (size_t)W * 3 * sizeof(double), H, hipMemcpyDeviceToHost));
+  for (int k = 0; k < n; k++) {                 // the ranks' reference raises
+    const rtx_status e = rtx_sync(ctxs[k], nullptr);
+    if (e) return fail(c0, e, "rank %d: %s", k, rtx_last_error(ctxs[k]));
+  }
+  return RTX_OK;
 }
 
 int32_t rtx_device_count(void) {

@@ -1585,7 +1585,18 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     }
   };
 
+  unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
+#define RTX_LV_STAMP(k)  \
+  if (RTX_STAMPS) {      \
+    t1 = stamp();        \
+    tS[k] += t1 - t0;    \
+    t0 = t1;             \
+  }
   while (true) {
+    if (RTX_STAMPS) {
+      t0 = stamp();
+      nchunks++;
+    }
     int chunk = 0;
     if (lane == 0) chunk = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
     chunk = __shfl(chunk, 0);
@@ -1647,6 +1658,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
         nleaf++;
       }, errA);
 
+    RTX_LV_STAMP(0)
     // ---- World#intersect (world.rb:37-59)
     const bool ext = alive && !fired;
     double best = S.max_distance, total = 0.0;
@@ -1655,6 +1667,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     bool hin = true;
     if (ext) walk(true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
     const bool shade = ext && besti >= 0;
+    RTX_LV_STAMP(1)
 
     V3 delta = hit, nrm = hit, nn = hit;
     double c = 0.0;
@@ -1664,6 +1677,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
       c = vcos(cur.ray.d, nrm, errS);         // ray.front.cos(-n): same bits as cos(n)
     }
 
+    RTX_LV_STAMP(2)
     // ---- World#local_lights (world.rb:72-80) fused with local_lighting's
     // light loop (world_object.rb:51-74): one SHADOW walk per light
     V3 lc = v3(0.0, 0.0, 0.0);
@@ -1692,6 +1706,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
       }
     }
 
+    RTX_LV_STAMP(3)
     // ---- which children pass rt_map's cutoff (ray_tracer.rb:52) at depth - 1
     uint32_t mask = 0;
     double rate = 0.0;
@@ -1729,6 +1744,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
       wbase = __shfl(wbase, 0);
     }
     const uint32_t child0 = wbase + (uint32_t)(incl - cnt);
+    RTX_LV_STAMP(4)
 
     // ---- children in the reference's push order (ray_tracer.rb:84-143), then the leaf
     if (shade) {
@@ -1807,6 +1823,13 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
       uint2* hdr = reinterpret_cast<uint2*>(rec);
       *hdr = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8) | (mask << 16), child0);
     }
+    RTX_LV_STAMP(5)
+  }
+#undef RTX_LV_STAMP
+  if (RTX_STAMPS && lane == 0) {
+    for (int k = 0; k < 6; k++) atomicAdd(&rtx_stamps[k], tS[k]);
+    atomicAdd(&rtx_stamps[6], nchunks);
+    atomicAdd(&rtx_stamps[7], 1ull);
   }
 }
 
@@ -2124,6 +2147,22 @@ __global__ __launch_bounds__(1024) void k_tile_sort(KParams p, const int32_t* cl
   for (int j = 0; j < TILE_CLASSES; j++) cnt[t * TILE_CLASSES + j] += base;
   __syncthreads();
   for (int k = t0; k < t1; k += st) order[cnt[(TILE_CLASSES - 1 - (staged ? cl8[k] : cls[k])) * 1024 + t]++] = k;
+}
+
+// rtx_render_multi: the rank-major packed tiles gathered on one device ->
+// the frame (camera.rb:42-51 merges the children's bands the same way).  One
+// thread per double of the frame; packed row r of rank k is image row
+// ((r / tile_rows) * n + k) * tile_rows + r % tile_rows.
+__global__ void k_unpack(const double* __restrict__ gathered, int w, int h, int tile_rows, int n, int rows_per_rank,
+                         double* __restrict__ out, size_t stride) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per_row = (long)w * 3;
+  if (i >= (long)n * rows_per_rank * per_row) return;
+  const int src_row = (int)(i / per_row);
+  const int k = src_row / rows_per_rank, r = src_row - k * rows_per_rank;
+  const int y = ((r / tile_rows) * n + k) * tile_rows + r % tile_rows;
+  if (y >= h) return;
+  out[(size_t)y * stride + (i - (long)src_row * per_row)] = gathered[i];
 }
 
 // Camera#array_to_color (camera.rb:153-156) + PNG::Canvas#point over black.
@@ -2449,6 +2488,15 @@ hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s) {
 hipError_t launch_path_trace(KParams p, hipStream_t s) {
   if (p.nrays <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_path_trace, dim3((unsigned)((p.nrays + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack(const double* gathered, int w, int h, int tile_rows, int n, int rows_per_rank,
+                         double* out, size_t stride, hipStream_t s) {
+  const long total = (long)n * rows_per_rank * w * 3;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, gathered, w, h, tile_rows, n,
+                     rows_per_rank, out, stride);
   return hipGetLastError();
 }
 

@@ -115,5 +115,8 @@ size_t bvh_lds_bytes(int n_nodes, int n_slots, int bvh_stack);
 size_t bvh_lds_budget();
 hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int blend, uint8_t* out,
                            hipStream_t s);
+// Rank-major packed tiles (n ranks x rows_per_rank rows x w x 3) -> frame rows.
+hipError_t launch_unpack(const double* gathered, int w, int h, int tile_rows, int n, int rows_per_rank,
+                         double* out, size_t stride, hipStream_t s);
 
 }  // namespace rtx

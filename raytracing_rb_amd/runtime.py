@@ -165,6 +165,26 @@ class Renderer:
             raise RtxError(st, "rtx_quantize_device failed")
 
 
+def render_multi(renderers, tile_rows=8, seed=1):
+    """Camera#render_fork over several contexts in one process (rtx_render_multi):
+    renderer k renders rank k's tiles on its device, ONE RCCL gather to the first
+    renderer's device.  Returns the float64 frame [H, W, 3]."""
+    if not renderers:
+        raise ValueError("no renderers")
+    lib = load_library()
+    r0 = renderers[0]
+    hs = (C.c_void_p * len(renderers))(*[r.h.value for r in renderers])
+    out = np.empty((r0.height, r0.width, 3), np.float64)
+    st = lib.rtx_render_multi(hs, len(renderers), tile_rows, seed, _dp(out), r0.width * 3)
+    if st:
+        raise RtxError(st, lib.rtx_last_error(r0.h).decode())
+    return out
+
+
+def device_count():
+    return load_library().rtx_device_count()
+
+
 def quantize(rgb, png_gem_blend=True):
     """array_to_color + canvas point (camera.rb:105,153-156) on the GPU -> RGBA8 [H, W, 4]."""
     lib = load_library()
@@ -181,4 +201,4 @@ def vec3_lib():
     return load_library()
 
 
-__all__ = ["Renderer", "RtxError", "quantize", "_abi"]
+__all__ = ["Renderer", "RtxError", "quantize", "render_multi", "device_count", "_abi"]

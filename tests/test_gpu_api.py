@@ -68,3 +68,25 @@ def test_cli(gpu, tmp_path):
     assert main(["s", out, os.path.join(SCENES, "c1_world.yml"), str(cam_yml)]) == 0
     assert png.decode_rgb8(out).shape == (36, 64, 3)
     assert main(["s", out]) == 1                                      # "parameter error"
+
+
+def test_render_multi_rccl_gather_matches_render(gpu):
+    """rtx_render_multi (Camera#render_fork over the node's GPUs, camera.rb:41-68):
+    one context per visible GPU, ONE RCCL ncclSend/ncclRecv group to the first
+    (on a 1-GPU box a 1-rank clique sending to itself), bit-identical to
+    rtx_render; then more workers than GPUs (device copies)."""
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import Renderer, device_count, render_multi
+    sd, cd = config.load_scene(os.path.join(SCENES, "c2_world.yml"), os.path.join(SCENES, "c2_camera.yml"),
+                               camera_overrides=dict(width=200, height=77))
+    n = device_count()
+    assert n >= 1
+    rs = [Renderer(sd, cd, device=k) for k in range(n)]
+    full = rs[0].render(seed=4)
+    got = render_multi(rs, tile_rows=8, seed=4)
+    assert np.array_equal(got.view(np.uint64), full.view(np.uint64))
+    got = render_multi(rs, tile_rows=8, seed=4)            # the cached clique again
+    assert np.array_equal(got.view(np.uint64), full.view(np.uint64))
+    rs3 = [Renderer(sd, cd, device=k % n) for k in range(3)]
+    got3 = render_multi(rs3, tile_rows=5, seed=4)
+    assert np.array_equal(got3.view(np.uint64), full.view(np.uint64))

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Phase breakdown of k_level from a -DRTX_STAMPS=1 build (diagnostic only):
+    RTX_LIB=_variants/librtx_stamps.so python tools/stamps_levels.py c2
+Per-wave shader-clock cycles (s_memtime) summed over every level launch of one frame."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import torch
+from raytracing_rb_amd import config, _abi
+from raytracing_rb_amd.runtime import Renderer
+scene = sys.argv[1] if len(sys.argv) > 1 else "c2"
+if scene == "c4":
+    import make_scenes
+    make_scenes.ensure_c4()
+ov = dict(width=960, height=540) if scene == "c4" else {}
+sd, cd = config.load_scene(os.path.join(ROOT, "scenes", scene + "_world.yml"),
+                           os.path.join(ROOT, "scenes", scene + "_camera.yml"), camera_overrides=ov)
+r = Renderer(sd, cd)
+r.set_option("engine", 1)
+for kv in sys.argv[2:]:
+    k, v = kv.split("=")
+    r.set_option(k, int(v))
+lib = _abi.load_library()
+out = torch.empty((cd.height, cd.width, 3), dtype=torch.float64, device="cuda")
+r.render_device(out.data_ptr()); r.sync()
+st = (ctypes.c_ulonglong * 16)()
+lib.rtxdbg_read_stamps(st, 1)
+r.render_device(out.data_ptr()); r.sync()
+lib.rtxdbg_read_stamps(st, 1)
+v = list(st)
+tot = sum(v[:6])
+names = ["A claim/load/lens/highlight", "B EXTEND walk", "C hit_info/normal/cos", "D SHADOW walks + lights",
+         "E child mask + wave prefix + atomic", "F children/leaf/record stores"]
+print("waves %d  chunks %d  cycles/chunk %.0f" % (v[7], v[6], tot / max(1, v[6])))
+for n, x in zip(names, v[:6]):
+    print("%-38s %5.1f%%  %8.0f cycles/chunk" % (n, 100.0 * x / tot, x / max(1, v[6])))
