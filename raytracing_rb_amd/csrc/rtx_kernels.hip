@@ -107,6 +107,9 @@ enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2, SRC_LIST = 3 };
 #ifndef RTX_LVL_WPS
 #define RTX_LVL_WPS 2        // waves per SIMD k_level is compiled for
 #endif
+#ifndef RTX_LV_CLAIM_AHEAD
+#define RTX_LV_CLAIM_AHEAD 0 // k_level claims its next 64-ray chunk while working on the current one (C2 6.26 vs 6.22 ms: off)
+#endif
 __device__ unsigned long long rtx_stamps[16];
 __device__ __forceinline__ unsigned long long wall() {   // 100 MHz constant clock, same on every XCD
 #if RTX_STAMPS
@@ -1518,14 +1521,17 @@ __device__ __forceinline__ void lv_redo(const KParams& p, int root) {
   }
 }
 
-__device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, uint64_t path, int root) {
+// root: the level-0 item of the ray's tree; (x, y, sample): its RNG key.
+__device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, uint64_t path, int root, int x, int y,
+                                             int sample) {
   double2* q = reinterpret_cast<double2*>(dst);
   q[0] = make_double2(r.o.x, r.o.y);
   q[1] = make_double2(r.o.z, r.d.x);
   q[2] = make_double2(r.d.y, r.d.z);
   q[3] = make_double2(att.x, att.y);
   q[4] = make_double2(att.z, __builtin_bit_cast(double, path));
-  q[5] = make_double2(__builtin_bit_cast(double, (int64_t)root), 0.0);
+  q[5] = make_double2(__builtin_bit_cast(double, (uint64_t)(uint32_t)root | (uint64_t)(uint32_t)sample << 32),
+                      __builtin_bit_cast(double, (uint64_t)(uint32_t)x | (uint64_t)(uint32_t)y << 32));
 }
 
 // Launch `level` (0 .. trace_depth-1) of one batch.  Persistent: every wave
@@ -1592,15 +1598,27 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     tS[k] += t1 - t0;    \
     t0 = t1;             \
   }
+  // Chunk claims: one atomic per 64 rays (RTX_LV_CLAIM_AHEAD issues the next
+  // claim when a chunk starts instead; measured no faster).
+  int next = 0;
+  if (RTX_LV_CLAIM_AHEAD) {
+    if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
+  }
   while (true) {
     if (RTX_STAMPS) {
       t0 = stamp();
       nchunks++;
     }
     int chunk = 0;
-    if (lane == 0) chunk = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
-    chunk = __shfl(chunk, 0);
-    if ((uint32_t)chunk * 64u >= n) break;
+    if (RTX_LV_CLAIM_AHEAD) {
+      chunk = __shfl(next, 0);
+      if ((uint32_t)chunk * 64u >= n) break;
+      if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
+    } else {
+      if (lane == 0) chunk = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
+      chunk = __shfl(chunk, 0);
+      if ((uint32_t)chunk * 64u >= n) break;
+    }
     const uint32_t i = (uint32_t)chunk * 64u + (uint32_t)lane;
     bool active = i < n;
 
@@ -1618,13 +1636,18 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
         cur.ray.d = v3(b.y, c.x, c.y);
         cur.att = v3(d.x, d.y, e.x);
         cur.path = __builtin_bit_cast(uint64_t, e.y);
-        root = (int)__builtin_bit_cast(int64_t, f.x);
+        const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
+        root = (int)(uint32_t)rs;
+        sample = (int)(rs >> 32);
+        x = (int)(uint32_t)xy;
+        y = (int)(xy >> 32);
       }
-      const ItemPos ip = decode_item(p, root);
-      x = p.x0 + ip.px;
-      y = row_to_y(p, ip.row);
-      sample = ip.sample;
       if (level == 0) {
+        p.lv_redo_of[i] = -1;                 // no overflow yet (lv_redo)
+        const ItemPos ip = decode_item(p, root);
+        x = p.x0 + ip.px;
+        y = row_to_y(p, ip.row);
+        sample = ip.sample;
         if (ip.valid) {
           cur.ray = lens_ray(cam, lens_target(cam, x, y), x, y, sample, p.seed);
           cur.att = v3(1.0, 1.0, 1.0);
@@ -1676,16 +1699,18 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
       nn = vnorm(nrm, errS);                  // n.normalize (world_object.rb:123)
       c = vcos(cur.ray.d, nrm, errS);         // ray.front.cos(-n): same bits as cos(n)
     }
+    const V3 qo = vadd(hit, delta);           // the shadow rays' target point (world.rb:76)
 
     RTX_LV_STAMP(2)
     // ---- World#local_lights (world.rb:72-80) fused with local_lighting's
-    // light loop (world_object.rb:51-74): one SHADOW walk per light
+    // light loop (world_object.rb:51-74): one SHADOW walk per light.  (Holding
+    // delta / n / n.normalize across the walks measured faster than
+    // recomputing them after: 6.22 vs 6.40 ms on C2.)
     V3 lc = v3(0.0, 0.0, 0.0);
     int nl = 0;
     for (int li = 0; li < S.n_light; li++) {
       if (!shade) continue;
       const LightDev& L = S.light[li];
-      const V3 qo = vadd(hit, delta);
       const V3 qL = v3p(L.pos);
       double tot = 1.0;
       double b2 = 0.0;
@@ -1705,7 +1730,6 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
         lc = vadd(lc, vsc(lcol, ldn));
       }
     }
-
     RTX_LV_STAMP(3)
     // ---- which children pass rt_map's cutoff (ray_tracer.rb:52) at depth - 1
     uint32_t mask = 0;
@@ -1750,7 +1774,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     if (shade) {
       uint32_t slot = child0;
       auto put = [&](const Ray& r, V3 att, uint64_t path) {
-        if (slot < p.lv_scap) lv_store_ray(outs + (size_t)slot * RAY_DOUBLES, r, att, path, root);
+        if (slot < p.lv_scap) lv_store_ray(outs + (size_t)slot * RAY_DOUBLES, r, att, path, root, x, y, sample);
         else {
           lv_redo(p, root);
           atomicAdd(&p.lv_ctl->dropped, 1u);
@@ -2029,7 +2053,8 @@ __global__ void k_level_acc(const LevelCtl* ctl, unsigned long long* acc) {
 }
 
 // Per batch: the control block, count[0] = the batch's level-0 items (pass 1:
-// from the device-side extra count), every redo slot -1.
+// from the device-side extra count).  (Every level-0 lane sets its item's redo
+// slot to -1.)
 __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max) {
   const int t = blockIdx.x * 256 + (int)threadIdx.x;
   if (t < 2 * (LV_MAXL + 1) + 2) {
@@ -2045,7 +2070,6 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max) {
     }
     reinterpret_cast<uint32_t*>(p.lv_ctl)[t] = v;
   }
-  for (int i = t; i < n0_max; i += gridDim.x * 256) p.lv_redo_of[i] = -1;
 }
 
 // ----------------------------------------------------------------- tile order
@@ -2426,8 +2450,7 @@ static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t
 // samples (exits at once when there are none), the tree reduction.
 static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_max, int fin_threads, hipStream_t s,
                               KernelEvents* kev) {
-  const int gb = std::max(1, std::min(1024, (n0_max + 255) / 256));
-  hipLaunchKernelGGL(k_level_begin, dim3((unsigned)gb), dim3(256), 0, s, q, n0_max);
+  hipLaunchKernelGGL(k_level_begin, dim3(1), dim3(256), 0, s, q, n0_max);
   hipError_t e = hipGetLastError();
   for (int d = 0; d < nlev && e == hipSuccess; d++)
     e = launch_level_mode(q, mode, d, d == 0 ? (long)n0_max : (long)q.lv_scap, s, kev);
