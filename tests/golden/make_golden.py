@@ -8,6 +8,8 @@ Fixtures (numpy .npz, data only):
                     committed scene at a reduced size (scene YAML sha256 kept to
                     detect drift)
   vectors.npz       counter-RNG values, Camera#lens_func rays, trace_sync colours
+  c2_full_columns64.npz  every 64th column of the full-size C2 frame, by the C
+                    restatement (the GPU test renders the whole frame)
   frame_c4_48x27.npz the 4096-sphere C4 scene: rendered by the C restatement
                     (oracle/rt_oracle.c, bit-checked against rt_ref.py on the other
                     frames and on sampled C4 pixels in tests/test_oracle.py), since
@@ -91,6 +93,21 @@ def render_c(world, camera, ov, seed=1):
     return fb, st.astype(np.int32)
 
 
+def c2_columns(stride=64, nprocs=8):
+    """C2 (the metric config) at its full 1920x1080, 4xAA, depth 5: every
+    `stride`-th column (30 columns, 32,400 pixels) by the C restatement in
+    forked column bands (oracle/rt_oracle.c rto_render_fork)."""
+    from oracle.c_oracle import Oracle
+    from raytracing_rb_amd import config
+    sd, cd = config.load_scene(os.path.join(SC, "c2_world.yml"), os.path.join(SC, "c2_camera.yml"))
+    full = Oracle(sd, cd).render_fork(nprocs, stride)
+    cols = np.arange(0, cd.width, stride)
+    np.savez_compressed(os.path.join(HERE, "c2_full_columns%d.npz" % stride), columns=cols,
+                        frame=full[:, cols, :], scene_sha=sha(os.path.join(SC, "c2_world.yml")),
+                        camera_sha=sha(os.path.join(SC, "c2_camera.yml")), seed=1, source="rt_oracle.c")
+    print("c2 columns", cols.size, full[:, cols].mean(axis=(0, 1)))
+
+
 def main(only=None):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import make_scenes
@@ -111,6 +128,8 @@ def main(only=None):
                             world=world, camera=camera, overrides=repr(ov),
                             scene_sha=sha(os.path.join(SC, world)), seed=1)
         print(name, fb.shape, "errors", int((st != 0).sum()), "mean", fb.mean(axis=(0, 1)))
+    if not only or "c2_columns" in only:
+        c2_columns()
     if not only or "vectors" in only:
         np.savez_compressed(os.path.join(HERE, "vectors.npz"), **vectors())
         print("vectors")

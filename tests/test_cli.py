@@ -76,9 +76,10 @@ def test_cli_loader_matches_python_loader(cli, world, camera):
                     reason="reference checkout not present (GPU box)")
 def test_cli_loads_reference_config(cli):
     """The reference's own config/world.yml + camera.yml (duplicate keys, '-' on its
-    own line); its missing floor.jpg and RubyOnRails.png remapped to our textures."""
+    own line); its missing floor.jpg remapped to our checker, RubyOnRails.png to its
+    copy in scenes/textures."""
     remap = {"./textures/floor.jpg": os.path.join(SCENES, "textures", "checker.png"),
-             "./textures/RubyOnRails.png": os.path.join(SCENES, "textures", "rails_synth.png")}
+             "./textures/RubyOnRails.png": os.path.join(SCENES, "textures", "RubyOnRails.png")}
     w, c = os.path.join(REFERENCE, "config", "world.yml"), os.path.join(REFERENCE, "config", "camera.yml")
     assert _cli_dump(cli, w, c, remap.items()) == _py_dump(w, c, remap)
 

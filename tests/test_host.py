@@ -52,9 +52,12 @@ def test_reference_world_yml_equals_restated_c0():
     ours = config.load_yaml(os.path.join(SCENES, "c0_world.yml"))
     for a, b in zip(ref["world_objects"], ours["world_objects"]):
         pa, pb = dict(a["properties"]), dict(b["properties"])
-        pa.pop("texture_file_path", None)
-        pb.pop("texture_file_path", None)
+        ta, tb = pa.pop("texture_file_path", None), pb.pop("texture_file_path", None)
         assert pa == pb and a["type"] == b["type"]
+        if ta == "./textures/RubyOnRails.png":      # the reference's texture, used as-is
+            assert tb == ta
+            assert open(os.path.join(REFERENCE, "textures", "RubyOnRails.png"), "rb").read() == \
+                open(os.path.join(SCENES, "textures", "RubyOnRails.png"), "rb").read()
     assert ref["lights"] == ours["lights"]
     assert ref["max_distance"] == ours["max_distance"]
     cam_ref = config.load_yaml(os.path.join(REFERENCE, "config", "camera.yml"))
@@ -117,9 +120,36 @@ def test_png_decoder_matches_pillow(tmp_path, mode, bits):
 
 def test_png_texture_fixture_matches_pillow():
     from PIL import Image
-    for name in ("rails_synth.png", "checker.png"):
+    for name in ("rails_synth.png", "checker.png", "RubyOnRails.png"):
         p = os.path.join(SCENES, "textures", name)
         assert np.array_equal(png.decode_rgb8(p), np.asarray(Image.open(p).convert("RGB")))
+
+
+def test_reference_texture_decode_is_high_byte():
+    """texture.rb:12-20: Vec3((pixel.red >> 8) / 256.0): the reference's own 16-bit
+    RubyOnRails.png decodes to the high byte of every 16-bit sample."""
+    import struct
+    import zlib
+    p = os.path.join(SCENES, "textures", "RubyOnRails.png")
+    data = open(p, "rb").read()
+    w, h, depth, ctype = struct.unpack(">IIBB", data[16:26])
+    assert (w, h, depth, ctype) == (122, 158, 16, 6)
+    got = png.decode_rgb8(p)
+    # independent decode of the first row (filter type + 16-bit big-endian RGBA)
+    pos, idat = 8, b""
+    while pos < len(data):
+        n, = struct.unpack(">I", data[pos:pos + 4])
+        if data[pos + 4:pos + 8] == b"IDAT":
+            idat += data[pos + 8:pos + 8 + n]
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    ftype, line = raw[0], bytearray(raw[1:1 + w * 8])
+    assert ftype in (0, 1)                           # row 0: None or Sub (no row above)
+    if ftype == 1:
+        for i in range(8, len(line)):                # Sub: + the byte one pixel (8 B) left
+            line[i] = (line[i] + line[i - 8]) & 0xFF
+    row0 = np.frombuffer(bytes(line), ">u2").reshape(w, 4)
+    assert np.array_equal(got[0], (row0[:, :3] >> 8).astype(np.uint8))
 
 
 # ------------------------------------------------------------------ C-ABI

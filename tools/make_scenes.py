@@ -4,11 +4,13 @@ synthetic textures.  Deterministic (numpy RandomState with fixed seeds).
 
   scenes/c0_world.yml  default world of the reference (config/world.yml restated),
                        the missing ./textures/floor.jpg replaced by a synthetic
-                       checker and RubyOnRails.png by a synthetic texture of the
-                       same shape (122x158, 16-bit RGBA)
+                       checker; the front wall's texture is the reference's own
+                       textures/RubyOnRails.png (122x158, 16-bit RGBA), copied
+                       as data into scenes/textures/
   scenes/c1_world.yml  1 sphere + ground plane + point light
   scenes/c2_world.yml  64 spheres (jittered 8x8 grid) + ground + area light
-  scenes/c4_world.yml  4096 random spheres + textured ground + area light
+  scenes/c4_world.yml  4096 random spheres + ground textured with RubyOnRails.png
+                        + area light
   scenes/cN_camera.yml the reference camera (config/camera.yml) with the
                        config's size / samples / depth
 """
@@ -80,8 +82,8 @@ def camera(name, w, h, pre, mx, d):
 
 C0 = """# Default world of the reference (config/world.yml), restated.  The ground
 # texture ./textures/floor.jpg is missing from the reference repo and is
-# replaced by a synthetic checker; RubyOnRails.png by a synthetic texture of the
-# same shape.  The front wall keeps the duplicate keys (YAML: last wins).
+# replaced by a synthetic checker; RubyOnRails.png is the reference's own file.
+# The front wall keeps the duplicate keys (YAML: last wins).
 max_distance:           10000
 soft_shadow_exponent:   2
 lights:
@@ -126,7 +128,7 @@ world_objects:
       diffuse_rate:             [0.6, 0.6, 0.6]
       reflective_attenuation:   [0.39, 0.39, 0.39]
       ambient:                  [0.01, 0.01, 0.01]
-      texture_file_path:        ./textures/rails_synth.png
+      texture_file_path:        ./textures/RubyOnRails.png
       texture_horizontal_scale: 0.015
       texture_vertical_scale:   0.015
   - type: Sphere
@@ -223,9 +225,12 @@ def c2():
     return s
 
 
+C4_HEADER = "# C4: 4096 random spheres + ground textured with RubyOnRails.png + area light (SURVEY.md 8d)"
+
+
 def c4():
     rs = np.random.RandomState(4096)
-    s = ("# C4: 4096 random spheres + textured ground + area light (SURVEY.md 8d)\n"
+    s = (C4_HEADER + "\n"
          "max_distance:           10000\nsoft_shadow_exponent:   2\n")
     s += light([10.0, -6.0, 12.0], 1.0)
     s += "world_objects:\n"
@@ -236,16 +241,21 @@ def c4():
         s += sphere("s%04d" % i, c, r, material(rs, k[i]))
     s += GROUND.format(extra=("      u_unit:                 1\n"
                               "      v_unit:                 1\n"
-                              "      texture_file_path:      ./textures/rails_synth.png\n"
+                              "      texture_file_path:      ./textures/RubyOnRails.png\n"
                               "      texture_horizontal_scale: 0.015\n"
                               "      texture_vertical_scale: 0.015\n"))
     return s
 
 
 def ensure_c4():
-    """scenes/c4_world.yml is generated (2 MB, not committed): write it if missing."""
+    """scenes/c4_world.yml is generated (2 MB, not committed): write it if missing
+    or from an older generator (its first line)."""
     path = os.path.join(SC, "c4_world.yml")
-    if not os.path.exists(path):
+    current = False
+    if os.path.exists(path):
+        with open(path) as fh:
+            current = fh.readline().rstrip("\n") == C4_HEADER
+    if not current:
         tmp = path + ".%d.tmp" % os.getpid()
         with open(tmp, "w") as fh:
             fh.write(c4())
