@@ -822,7 +822,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const int rec_bytes = levels_rec_bytes(c->scene.n_light);
   const size_t maxch = (scap + 63) / 64;
   const size_t sz_ctl = al256(sizeof(LevelCtl)), sz_redo = al256(n0 * 4), sz_smp = al256(n0 * 32),
-               sz_stage = al256(scap * (persist ? RAY_BYTES_WT * std::max(1, nlev - 1) : RAY_BYTES)),
+               sz_stage = al256(scap * RAY_BYTES * (persist ? std::max(1, nlev - 1) : 1)),
                sz_rec = al256(lcap * (size_t)rec_bytes), sz_extra = al256((npx + 64) * 4),
                sz_ready = persist ? al256((size_t)nlev * maxch * 4) : 0;
   const size_t total = sz_ctl + 2 * sz_redo + sz_smp + (persist ? 1 : 2) * sz_stage + sz_rec + sz_extra + sz_ready;

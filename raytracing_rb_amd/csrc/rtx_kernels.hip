@@ -1521,54 +1521,9 @@ __device__ __forceinline__ void lv_redo(const KParams& p, int root) {
   }
 }
 
-// Persistent launch (PERSIST): ray records are handed from one CU to another
-// inside the launch.  Each record gets a 128-B line of its own (no two
-// records share a line, so no XCD's L2 can hold a stale copy of a record it
-// read a neighbour of), is stored write-through (`sc1`, 16 B per store) and
-// drained (`s_waitcnt vmcnt(0)`) before the lv_ready count; the consumer
-// reads it with `sc1` loads (L1 bypassed) after its poll of lv_ready matched
-// (MI355X_MICROARCH.md, "Valid forms" of the inter-workgroup hand-off).
-constexpr int RAY_DOUBLES_WT = 16;       // 128-B record line of the persistent launch
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st16_wt(double* dst, double a, double b) {
-  const u32x4 v = __builtin_bit_cast(u32x4, make_double2(a, b));
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(v) : "memory");
-}
-__device__ __forceinline__ void ld_ray_wt(const double* src, double2* o) {
-  u32x4 a, b, c, d, e, f;
-  asm volatile(
-      "global_load_dwordx4 %0, %6, off sc1\n\t"
-      "global_load_dwordx4 %1, %6, off offset:16 sc1\n\t"
-      "global_load_dwordx4 %2, %6, off offset:32 sc1\n\t"
-      "global_load_dwordx4 %3, %6, off offset:48 sc1\n\t"
-      "global_load_dwordx4 %4, %6, off offset:64 sc1\n\t"
-      "global_load_dwordx4 %5, %6, off offset:80 sc1\n\t"
-      "s_waitcnt vmcnt(0)"
-      : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d), "=&v"(e), "=&v"(f)
-      : "v"(src)
-      : "memory");
-  o[0] = __builtin_bit_cast(double2, a);
-  o[1] = __builtin_bit_cast(double2, b);
-  o[2] = __builtin_bit_cast(double2, c);
-  o[3] = __builtin_bit_cast(double2, d);
-  o[4] = __builtin_bit_cast(double2, e);
-  o[5] = __builtin_bit_cast(double2, f);
-}
-
 // root: the level-0 item of the ray's tree; (x, y, sample): its RNG key.
-template <bool WT>
 __device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, uint64_t path, int root, int x, int y,
                                              int sample) {
-  if (WT) {                                   // write-through (persistent launch)
-    st16_wt(dst, r.o.x, r.o.y);
-    st16_wt(dst + 2, r.o.z, r.d.x);
-    st16_wt(dst + 4, r.d.y, r.d.z);
-    st16_wt(dst + 6, att.x, att.y);
-    st16_wt(dst + 8, att.z, __builtin_bit_cast(double, path));
-    st16_wt(dst + 10, __builtin_bit_cast(double, (uint64_t)(uint32_t)root | (uint64_t)(uint32_t)sample << 32),
-            __builtin_bit_cast(double, (uint64_t)(uint32_t)x | (uint64_t)(uint32_t)y << 32));
-    return;
-  }
   double2* q = reinterpret_cast<double2*>(dst);
   q[0] = make_double2(r.o.x, r.o.y);
   q[1] = make_double2(r.o.z, r.d.x);
@@ -1586,8 +1541,7 @@ __device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, 
 //   * Tickets: a lane takes a ticket (atomicAdd on the level's claim counter,
 //     never a CAS) for a level >= 1 that has unclaimed rays.  A ticket is
 //     served once all records of its chunk are written (producers count them
-//     in lv_ready after their write-through stores drained) -- the deepest
-//     level first, so trees
+//     in lv_ready after a release fence) -- the deepest level first, so trees
 //     finish early.  A wave never blocks on a ticket: meanwhile it takes
 //     level-0 chunks, which are always ready, so no wait can deadlock.
 //   * Closure: level d's count is final once every level above it is done
@@ -1608,7 +1562,6 @@ __device__ bool lv_next_chunk(const KParams& p, int& pend, int& level, int& chun
   const unsigned long long full = nlev >= 64 ? ~0ull : ((1ull << nlev) - 1ull);
   const unsigned long long below = d >= 64 ? ~0ull : ((1ull << d) - 1ull);
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  int backoff = 1;                                           // idle polls back off: 1, 2, 4 .. 32 x s_sleep(8)
   while (true) {
     uint32_t cnt = 0, cl = 0, dn = 0, rdy = 0;
     if (lv) {
@@ -1640,7 +1593,8 @@ __device__ bool lv_next_chunk(const KParams& p, int& pend, int& level, int& chun
       chunk = __shfl(pend, dd);
       n = (uint32_t)__shfl((int)cnt, dd);
       if (d == dd) pend = -1;
-      return true;                                           // (the records are read with sc1 loads)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");     // the chunk's records, written by other CUs
+      return true;
     }
     if (lv && d >= 1 && pend < 0 && (unsigned long long)cl * 64u < cnt)
       pend = (int)atomicAdd(&ctl->claim[d], 1u);             // a ticket, served when written
@@ -1659,8 +1613,7 @@ __device__ bool lv_next_chunk(const KParams& p, int& pend, int& level, int& chun
       pend = -1;
       return false;
     }
-    for (int k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(8);
-    backoff = backoff < 32 ? 2 * backoff : 32;
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
@@ -1753,9 +1706,9 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
     }
     // this level's tree records, its rays (levels >= 1) and its children's slots
     const uint32_t base = PERSIST ? (uint32_t)level * p.lv_scap : base_fixed;
-    const double* __restrict__ in = PERSIST ? p.lv_stage[0] + (size_t)(level > 0 ? level - 1 : 0) * p.lv_scap * RAY_DOUBLES_WT
+    const double* __restrict__ in = PERSIST ? p.lv_stage[0] + (size_t)(level > 0 ? level - 1 : 0) * p.lv_scap * RAY_DOUBLES
                                             : p.lv_stage[level & 1];
-    double* __restrict__ outs = PERSIST ? p.lv_stage[0] + (size_t)level * p.lv_scap * RAY_DOUBLES_WT
+    double* __restrict__ outs = PERSIST ? p.lv_stage[0] + (size_t)level * p.lv_scap * RAY_DOUBLES
                                         : p.lv_stage[(level + 1) & 1];
     const int depth = cam.depth - level;      // trace_depth of this level's rays
     const uint32_t i = (uint32_t)chunk * 64u + (uint32_t)lane;
@@ -1769,15 +1722,8 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
       if (level == 0) {
         root = (int)i;
       } else {
-        double2 a, b, c, d, e, f;
-        if (PERSIST) {
-          double2 w[6];
-          ld_ray_wt(in + (size_t)i * RAY_DOUBLES_WT, w);
-          a = w[0], b = w[1], c = w[2], d = w[3], e = w[4], f = w[5];
-        } else {
-          const double2* q = reinterpret_cast<const double2*>(in + (size_t)i * RAY_DOUBLES);
-          a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
-        }
+        const double2* q = reinterpret_cast<const double2*>(in + (size_t)i * RAY_DOUBLES);
+        const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
         cur.ray.o = v3(a.x, a.y, b.x);
         cur.ray.d = v3(b.y, c.x, c.y);
         cur.att = v3(d.x, d.y, e.x);
@@ -1920,9 +1866,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
     if (shade) {
       uint32_t slot = child0;
       auto put = [&](const Ray& r, V3 att, uint64_t path) {
-        if (slot < p.lv_scap)
-          lv_store_ray<PERSIST>(outs + (size_t)slot * (PERSIST ? RAY_DOUBLES_WT : RAY_DOUBLES), r, att, path, root, x,
-                                y, sample);
+        if (slot < p.lv_scap) lv_store_ray(outs + (size_t)slot * RAY_DOUBLES, r, att, path, root, x, y, sample);
         else {
           lv_redo(p, root);
           atomicAdd(&p.lv_ctl->dropped, 1u);
@@ -1996,9 +1940,9 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
       *hdr = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8) | (mask << 16), child0);
     }
     if (PERSIST) {
-      // publish: the children's write-through records drained first, then
-      // how many of each next-level chunk this wave wrote, then this chunk as done
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // publish: the children's records first (release), then how many of
+      // each next-level chunk this wave wrote, then this chunk as done
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       const uint32_t lo = wbase, hi = min(wbase + (uint32_t)wtotal, p.lv_scap);
       if (wtotal > 0 && lo < hi) {
         const uint32_t c0 = lo / 64, c1 = (hi - 1) / 64;

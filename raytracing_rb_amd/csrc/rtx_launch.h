@@ -114,7 +114,6 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
 // Tree-record bytes for a scene with n_light lights (one leaf per fired light).
 int levels_rec_bytes(int n_light);
 constexpr size_t RAY_BYTES = 96;                // staged ray record of the bounce-level engine
-constexpr size_t RAY_BYTES_WT = 128;            // ... of its persistent launch: one 128-B line per record
 hipError_t launch_path_trace(KParams p, hipStream_t s);
 int resolve_mode(const SceneDev& S, int mode);
 // LDS bytes a hierarchy workgroup needs (nodes + leaf records + traversal
