@@ -811,7 +811,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const size_t n0 = std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, p.max_samples - p.pre));
   const size_t fl = (size_t)c->opt_lv_floor;
   const int nlev = std::max(1, c->cam.depth);
-  const bool persist = c->opt_lv_persist != 0 && nlev <= 64;
+  const bool persist = c->opt_lv_persist != 0;
   const size_t scap = std::max<size_t>(std::max<size_t>(std::max<size_t>(64, fl), n0 * (size_t)c->opt_lv_stage_pct / 100),
                                        persist ? n0 : 0);
   // persistent launch: one record region of scap per level (levels run concurrently)

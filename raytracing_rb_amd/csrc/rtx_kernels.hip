@@ -1535,86 +1535,65 @@ __device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, 
 }
 
 // One persistent launch for every level (PERSIST): the wave's next 64-ray
-// chunk.  The wave schedules with its lanes: lane d reads level d's count,
-// claims, done count and the written-records count of the chunk it holds a
-// ticket for, all in one round trip.
-//   * Tickets: a lane takes a ticket (atomicAdd on the level's claim counter,
-//     never a CAS) for a level >= 1 that has unclaimed rays.  A ticket is
-//     served once all records of its chunk are written (producers count them
-//     in lv_ready after a release fence) -- the deepest level first, so trees
-//     finish early.  A wave never blocks on a ticket: meanwhile it takes
-//     level-0 chunks, which are always ready, so no wait can deadlock.
-//   * Closure: level d's count is final once every level above it is done
-//     (done >= count over the prefix 0 .. d-1); a partial last chunk is served
-//     only then, and a ticket past the final count is dropped.
-// Returns false once every level is done.  A wave that waits 2 s (100 MHz
-// clock) without work gives up and flags the batch (RTX_EHIP).
+// chunk, from the deepest level that has a chunk whose records are all
+// written (producers count them in lv_ready after a release fence), so
+// trees finish early and no level waits for the previous one to drain.  A
+// level is closed (its count final) once the level above is closed and all
+// its rays are done; a partial last chunk is taken only then.  Returns false
+// when every level is closed and done.  Lane 0 schedules; the others wait.
+// A wave that waits longer than 2 s (100 MHz clock) for work that never
+// comes gives up and flags the batch (RTX_EHIP): every wait ends.
 __device__ __forceinline__ uint32_t lv_ld(const uint32_t* a) {
   return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ bool lv_next_chunk(const KParams& p, int& pend, int& level, int& chunk, uint32_t& n) {
+__device__ bool lv_next_chunk(const KParams& p, int& level, int& chunk, uint32_t& n) {
   LevelCtl* ctl = p.lv_ctl;
-  const int nlev = p.lv_nlev;                                // <= 64 (one lane per level)
-  const int d = (int)__lane_id();
-  const bool lv = d < nlev;
+  const int nlev = p.lv_nlev;
   const uint32_t maxch = (p.lv_scap + 63) / 64;
-  const unsigned long long full = nlev >= 64 ? ~0ull : ((1ull << nlev) - 1ull);
-  const unsigned long long below = d >= 64 ? ~0ull : ((1ull << d) - 1ull);
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  while (true) {
-    uint32_t cnt = 0, cl = 0, dn = 0, rdy = 0;
-    if (lv) {
-      dn = __hip_atomic_load(&ctl->done[d], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      cnt = d == 0 ? lv_ld(&ctl->count[0]) : min(lv_ld(&ctl->count[d]), p.lv_scap);
-      cl = lv_ld(&ctl->claim[d]);
-      if (pend >= 0) rdy = lv_ld(&p.lv_ready[(size_t)d * maxch + (uint32_t)pend]);
-    }
-    const unsigned long long doneb = __ballot(lv && dn >= cnt);
-    if ((doneb & full) == full) {                            // every level done
-      pend = -1;
-      return false;
-    }
-    const bool closed = (doneb & below) == below;            // levels 0 .. d-1 done: count[d] final
-    bool take = false;
-    if (lv && pend >= 0) {
-      const uint32_t c0 = (uint32_t)pend * 64u;
-      if (c0 < cnt) {
-        const uint32_t need = min(64u, cnt - c0);
-        take = (need == 64u || closed) && rdy >= need;
-      } else if (closed) {
-        pend = -1;                                           // past the final count: nothing to do
+  int lv = -1, ch = 0;
+  uint32_t cnt = 0;
+  if (__lane_id() == 0) {
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      // closed levels: bit d of `closed`
+      unsigned long long closed = 1ull;
+      for (int d = 0; d < nlev; d++) {
+        if (!(closed >> d & 1)) break;
+        const uint32_t dn = __hip_atomic_load(&ctl->done[d], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t c = d == 0 ? lv_ld(&ctl->count[0]) : min(lv_ld(&ctl->count[d]), p.lv_scap);
+        if (dn >= c) closed |= 1ull << (d + 1);
       }
+      if (closed >> nlev & 1) break;                        // every level closed and done
+      bool found = false;
+      for (int d = nlev - 1; d >= 0 && !found; d--) {
+        const uint32_t c = d == 0 ? lv_ld(&ctl->count[0]) : min(lv_ld(&ctl->count[d]), p.lv_scap);
+        const uint32_t cl = lv_ld(&ctl->claim[d]);
+        if ((unsigned long long)cl * 64 >= c) continue;
+        const uint32_t need = min(64u, c - cl * 64);
+        if (need < 64 && !(closed >> d & 1)) continue;      // the last chunk may still grow
+        if (d > 0 && lv_ld(&p.lv_ready[(size_t)d * maxch + cl]) < need) continue;   // not all written yet
+        if (atomicCAS(&ctl->claim[d], cl, cl + 1) == cl) {
+          lv = d;
+          ch = (int)cl;
+          cnt = c;
+          found = true;
+        }
+      }
+      if (found) break;
+      if (__builtin_amdgcn_s_memrealtime() - t_start > 200000000ull) {   // 2 s without work: give up
+        atomicOr(&ctl->hang, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
     }
-    const unsigned long long tb = __ballot(take);
-    if (tb) {
-      const int dd = 63 - __builtin_clzll(tb);               // the deepest ready level
-      level = dd;
-      chunk = __shfl(pend, dd);
-      n = (uint32_t)__shfl((int)cnt, dd);
-      if (d == dd) pend = -1;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");     // the chunk's records, written by other CUs
-      return true;
-    }
-    if (lv && d >= 1 && pend < 0 && (unsigned long long)cl * 64u < cnt)
-      pend = (int)atomicAdd(&ctl->claim[d], 1u);             // a ticket, served when written
-    int c0 = -1;
-    if (d == 0 && (unsigned long long)cl * 64u < cnt) c0 = (int)atomicAdd(&ctl->claim[0], 1u);
-    c0 = __shfl(c0, 0);
-    const uint32_t cnt0 = (uint32_t)__shfl((int)cnt, 0);
-    if (c0 >= 0 && (unsigned long long)c0 * 64u < cnt0) {   // level 0: camera samples, always ready
-      level = 0;
-      chunk = c0;
-      n = cnt0;
-      return true;
-    }
-    if (__builtin_amdgcn_s_memrealtime() - t_start > 200000000ull) {   // 2 s without work: give up
-      if (d == 0) atomicOr(&ctl->hang, 1u);
-      pend = -1;
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
   }
+  level = __shfl(lv, 0);
+  chunk = __shfl(ch, 0);
+  n = (uint32_t)__shfl((int)cnt, 0);
+  if (level < 0) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");        // the chunk's ray records, written by other CUs
+  return true;
 }
 
 // Launch `level_arg` (0 .. trace_depth-1) of one batch (PERSIST: every level
@@ -1682,7 +1661,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
   }
   // Chunk claims: one atomic per 64 rays (RTX_LV_CLAIM_AHEAD issues the next
   // claim when a chunk starts instead; measured no faster).
-  int next = 0, pend = -1;                    // pend: PERSIST, this lane's ticket for its level (lv_next_chunk)
+  int next = 0;
   if (!PERSIST && RTX_LV_CLAIM_AHEAD) {
     if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level_arg], 1u);
   }
@@ -1694,7 +1673,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
     int chunk = 0, level = level_arg;
     uint32_t n = n_fixed;
     if (PERSIST) {
-      if (!lv_next_chunk(p, pend, level, chunk, n)) break;
+      if (!lv_next_chunk(p, level, chunk, n)) break;
     } else if (RTX_LV_CLAIM_AHEAD) {
       chunk = __shfl(next, 0);
       if ((uint32_t)chunk * 64u >= n) break;
