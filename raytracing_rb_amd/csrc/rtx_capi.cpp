@@ -75,7 +75,6 @@ struct rtx_context {
   int64_t opt_lv_stage_pct = 300;    // bounce levels: ray records per staging buffer, % of the batch items
   int64_t opt_lv_rec_pct = 1600;      // bounce levels: tree records of a batch (all levels), % of the batch items
   int64_t opt_lv_floor = 1 << 20;    // bounce levels: at least this many staging and 4x this many tree records
-  int64_t opt_lv_persist = 0;        // bounce levels: 1 = every level in one persistent launch
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
@@ -388,8 +387,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"bvh_sah", c->opt_bvh_sah},     {"bvh_min", c->opt_bvh_min},         {"postpone", c->opt_postpone},
       {"lds_stack", c->opt_lds_stack}, {"tile_order", c->opt_tile_order},   {"sphere_src", c->opt_sphere_src},
       {"kernel_events", c->opt_kernel_events}, {"lv_batch", c->opt_lv_batch},
-      {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor},
-      {"lv_persist", c->opt_lv_persist}};
+      {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -446,10 +444,6 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_stage_pct") || !strcmp(key, "lv_rec_pct")) {   // bounce-level buffer capacities
     if (value < 1 || value > 10000) return fail(c, RTX_EINVAL, "%s must be in [1, 10000]", key);
     (!strcmp(key, "lv_stage_pct") ? c->opt_lv_stage_pct : c->opt_lv_rec_pct) = value;
-    return RTX_OK;
-  }
-  if (!strcmp(key, "lv_persist")) {        // bounce levels: every level in one persistent launch
-    c->opt_lv_persist = value != 0;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_floor")) {          // bounce levels: minimum buffer records (small frames, deep trees)
@@ -810,22 +804,15 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // level-0 items of one batch: pass 0 (tiles) or pass 1 (>= one pixel's extra samples)
   const size_t n0 = std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, p.max_samples - p.pre));
   const size_t fl = (size_t)c->opt_lv_floor;
-  const int nlev = std::max(1, c->cam.depth);
-  const bool persist = c->opt_lv_persist != 0;
-  const size_t scap = std::max<size_t>(std::max<size_t>(std::max<size_t>(64, fl), n0 * (size_t)c->opt_lv_stage_pct / 100),
-                                       persist ? n0 : 0);
-  // persistent launch: one record region of scap per level (levels run concurrently)
-  const size_t lcap = persist ? scap * nlev
-                              : std::max<size_t>(std::max(n0, 4 * fl), n0 * (size_t)c->opt_lv_rec_pct / 100);
+  const size_t scap = std::max<size_t>(std::max<size_t>(64, fl), n0 * (size_t)c->opt_lv_stage_pct / 100);
+  const size_t lcap = std::max<size_t>(std::max(n0, 4 * fl), n0 * (size_t)c->opt_lv_rec_pct / 100);
   if (scap > UINT32_MAX / 2 || lcap > UINT32_MAX / 2)
     return fail(c, RTX_EINVAL, "bounce-level buffers exceed 2^31 records: lower lv_batch");
   const int rec_bytes = levels_rec_bytes(c->scene.n_light);
-  const size_t maxch = (scap + 63) / 64;
   const size_t sz_ctl = al256(sizeof(LevelCtl)), sz_redo = al256(n0 * 4), sz_smp = al256(n0 * 32),
-               sz_stage = al256(scap * RAY_BYTES * (persist ? std::max(1, nlev - 1) : 1)),
-               sz_rec = al256(lcap * (size_t)rec_bytes), sz_extra = al256((npx + 64) * 4),
-               sz_ready = persist ? al256((size_t)nlev * maxch * 4) : 0;
-  const size_t total = sz_ctl + 2 * sz_redo + sz_smp + (persist ? 1 : 2) * sz_stage + sz_rec + sz_extra + sz_ready;
+               sz_stage = al256(scap * RAY_BYTES), sz_rec = al256(lcap * (size_t)rec_bytes),
+               sz_extra = al256((npx + 64) * 4);
+  const size_t total = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   HIPCHK(c, hipMemsetAsync(c->d_lvstats, 0, sizeof(unsigned long long) * (LV_MAXL + 3), stream));
   char* buf = nullptr;
@@ -836,12 +823,8 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_redo_list = (int32_t*)q;             q += sz_redo;
   p.lv_redo_smp = (double*)q;               q += sz_smp;
   p.lv_stage[0] = (double*)q;               q += sz_stage;
-  p.lv_stage[1] = persist ? p.lv_stage[0] : (double*)q;
-  if (!persist) q += sz_stage;
+  p.lv_stage[1] = (double*)q;               q += sz_stage;
   p.lv_rec = q;                             q += sz_rec;
-  p.lv_ready = (uint32_t*)q;                q += sz_ready;
-  p.lv_persist = persist;
-  p.lv_nlev = nlev;
   p.extra_count = (int32_t*)q;
   p.extra_list = p.extra_count + 64;
   p.lv_scap = (uint32_t)scap;
@@ -852,7 +835,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   KernelEvents kev{c->ev, 0, rtx_context::MAX_EV};
   if (c->opt_kernel_events && !c->ev[0])
     for (int k = 0; k < 2 * rtx_context::MAX_EV; k++) HIPCHK(c, hipEventCreate(&c->ev[k]));
-  const hipError_t e = launch_levels(p, sph_mode(c), maxs, nlev, batch_tiles, stream,
+  const hipError_t e = launch_levels(p, sph_mode(c), maxs, std::max(1, c->cam.depth), batch_tiles, stream,
                                      c->opt_kernel_events ? &kev : nullptr);
   if (c->opt_kernel_events) c->n_ev = kev.n;
   const hipError_t f = hipFreeAsync(buf, stream);
@@ -990,11 +973,9 @@ rtx_status rtx_sync(rtx_context* c, void* stream) {
   HIPCHK(c, hipDeviceSynchronize());
   if (!e.flags) return RTX_OK;
   // device ERR_ code -> rtx_status (index = ERR_ code, rtx_vec3.h)
-  static const rtx_status status_of[6] = {RTX_OK, RTX_EZERO_VEC, RTX_ECOLOR_GT1, RTX_EDOMAIN, RTX_ETYPE, RTX_EHIP};
+  static const rtx_status status_of[5] = {RTX_OK, RTX_EZERO_VEC, RTX_ECOLOR_GT1, RTX_EDOMAIN, RTX_ETYPE};
   rtx_status first = RTX_OK;
   unsigned long long pix = ~0ull;
-  if (e.flags >> ERR_HANG & 1)
-    return fail(c, RTX_EHIP, "bounce-level scheduler: a wave's wait guard fired (frame incomplete)");
   for (int code = 1; code < 5; code++)
     if ((e.flags >> code & 1) && e.first[code] < pix) {
       pix = e.first[code];

@@ -1534,79 +1534,16 @@ __device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, 
                       __builtin_bit_cast(double, (uint64_t)(uint32_t)x | (uint64_t)(uint32_t)y << 32));
 }
 
-// One persistent launch for every level (PERSIST): the wave's next 64-ray
-// chunk, from the deepest level that has a chunk whose records are all
-// written (producers count them in lv_ready after a release fence), so
-// trees finish early and no level waits for the previous one to drain.  A
-// level is closed (its count final) once the level above is closed and all
-// its rays are done; a partial last chunk is taken only then.  Returns false
-// when every level is closed and done.  Lane 0 schedules; the others wait.
-// A wave that waits longer than 2 s (100 MHz clock) for work that never
-// comes gives up and flags the batch (RTX_EHIP): every wait ends.
-__device__ __forceinline__ uint32_t lv_ld(const uint32_t* a) {
-  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ bool lv_next_chunk(const KParams& p, int& level, int& chunk, uint32_t& n) {
-  LevelCtl* ctl = p.lv_ctl;
-  const int nlev = p.lv_nlev;
-  const uint32_t maxch = (p.lv_scap + 63) / 64;
-  int lv = -1, ch = 0;
-  uint32_t cnt = 0;
-  if (__lane_id() == 0) {
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-    while (true) {
-      // closed levels: bit d of `closed`
-      unsigned long long closed = 1ull;
-      for (int d = 0; d < nlev; d++) {
-        if (!(closed >> d & 1)) break;
-        const uint32_t dn = __hip_atomic_load(&ctl->done[d], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t c = d == 0 ? lv_ld(&ctl->count[0]) : min(lv_ld(&ctl->count[d]), p.lv_scap);
-        if (dn >= c) closed |= 1ull << (d + 1);
-      }
-      if (closed >> nlev & 1) break;                        // every level closed and done
-      bool found = false;
-      for (int d = nlev - 1; d >= 0 && !found; d--) {
-        const uint32_t c = d == 0 ? lv_ld(&ctl->count[0]) : min(lv_ld(&ctl->count[d]), p.lv_scap);
-        const uint32_t cl = lv_ld(&ctl->claim[d]);
-        if ((unsigned long long)cl * 64 >= c) continue;
-        const uint32_t need = min(64u, c - cl * 64);
-        if (need < 64 && !(closed >> d & 1)) continue;      // the last chunk may still grow
-        if (d > 0 && lv_ld(&p.lv_ready[(size_t)d * maxch + cl]) < need) continue;   // not all written yet
-        if (atomicCAS(&ctl->claim[d], cl, cl + 1) == cl) {
-          lv = d;
-          ch = (int)cl;
-          cnt = c;
-          found = true;
-        }
-      }
-      if (found) break;
-      if (__builtin_amdgcn_s_memrealtime() - t_start > 200000000ull) {   // 2 s without work: give up
-        atomicOr(&ctl->hang, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  level = __shfl(lv, 0);
-  chunk = __shfl(ch, 0);
-  n = (uint32_t)__shfl((int)cnt, 0);
-  if (level < 0) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");        // the chunk's ray records, written by other CUs
-  return true;
-}
-
-// Launch `level_arg` (0 .. trace_depth-1) of one batch (PERSIST: every level
-// in one launch).  Persistent: every wave claims 64-ray chunks until the
-// work is exhausted.
-template <int SPH, int BS, bool PERSIST>
-__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_arg) {
+// Launch `level` (0 .. trace_depth-1) of one batch.  Persistent: every wave
+// claims 64-ray chunks until the level's count is exhausted.
+template <int SPH, int BS>
+__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level) {
   const SceneDev& S = p.scene;
   const CameraDev& cam = *p.cam;
   extern __shared__ float4 lds_sph[];
   char* lds = reinterpret_cast<char*>(lds_sph);
-  const uint32_t n_fixed = PERSIST ? 0u : lv_count(p, level_arg);
-  if (!PERSIST && n_fixed == 0) return;       // uniform: before any barrier
+  const uint32_t n = lv_count(p, level);
+  if (n == 0) return;                         // uniform: before any barrier
   if (SPH == SPH_LIN_LDS) {
     for (int i = threadIdx.x; i < S.n_sphere + 4; i += BS)
       lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
@@ -1624,9 +1561,11 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
   int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
   double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
 
-  uint32_t base_fixed = 0;                    // this level's first record in lv_rec
-  if (!PERSIST)
-    for (int e = 0; e < level_arg; e++) base_fixed += lv_count(p, e);
+  uint32_t base = 0;                          // this level's first record in lv_rec
+  for (int e = 0; e < level; e++) base += lv_count(p, e);
+  const double* __restrict__ in = p.lv_stage[level & 1];
+  double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
+  const int depth = cam.depth - level;        // trace_depth of this level's rays
   const int pt = cam.pt;
   const uint64_t R = (uint64_t)pt + 3;
   const int lane = (int)__lane_id();
@@ -1662,19 +1601,16 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
   // Chunk claims: one atomic per 64 rays (RTX_LV_CLAIM_AHEAD issues the next
   // claim when a chunk starts instead; measured no faster).
   int next = 0;
-  if (!PERSIST && RTX_LV_CLAIM_AHEAD) {
-    if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level_arg], 1u);
+  if (RTX_LV_CLAIM_AHEAD) {
+    if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
   }
   while (true) {
     if (RTX_STAMPS) {
       t0 = stamp();
       nchunks++;
     }
-    int chunk = 0, level = level_arg;
-    uint32_t n = n_fixed;
-    if (PERSIST) {
-      if (!lv_next_chunk(p, level, chunk, n)) break;
-    } else if (RTX_LV_CLAIM_AHEAD) {
+    int chunk = 0;
+    if (RTX_LV_CLAIM_AHEAD) {
       chunk = __shfl(next, 0);
       if ((uint32_t)chunk * 64u >= n) break;
       if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
@@ -1683,13 +1619,6 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
       chunk = __shfl(chunk, 0);
       if ((uint32_t)chunk * 64u >= n) break;
     }
-    // this level's tree records, its rays (levels >= 1) and its children's slots
-    const uint32_t base = PERSIST ? (uint32_t)level * p.lv_scap : base_fixed;
-    const double* __restrict__ in = PERSIST ? p.lv_stage[0] + (size_t)(level > 0 ? level - 1 : 0) * p.lv_scap * RAY_DOUBLES
-                                            : p.lv_stage[level & 1];
-    double* __restrict__ outs = PERSIST ? p.lv_stage[0] + (size_t)level * p.lv_scap * RAY_DOUBLES
-                                        : p.lv_stage[(level + 1) & 1];
-    const int depth = cam.depth - level;      // trace_depth of this level's rays
     const uint32_t i = (uint32_t)chunk * 64u + (uint32_t)lane;
     bool active = i < n;
 
@@ -1918,24 +1847,6 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level_
       uint2* hdr = reinterpret_cast<uint2*>(rec);
       *hdr = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8) | (mask << 16), child0);
     }
-    if (PERSIST) {
-      // publish: the children's records first (release), then how many of
-      // each next-level chunk this wave wrote, then this chunk as done
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      const uint32_t lo = wbase, hi = min(wbase + (uint32_t)wtotal, p.lv_scap);
-      if (wtotal > 0 && lo < hi) {
-        const uint32_t c0 = lo / 64, c1 = (hi - 1) / 64;
-        const uint32_t c = c0 + (uint32_t)lane;
-        if (c <= c1) {
-          const uint32_t a = max(lo, c * 64), b = min(hi, c * 64 + 64);
-          atomicAdd(&p.lv_ready[(size_t)(level + 1) * ((p.lv_scap + 63) / 64) + c], b - a);
-        }
-      }
-      if (lane == 0) {
-        const uint32_t m = n - (uint32_t)chunk * 64u;
-        __hip_atomic_fetch_add(&p.lv_ctl->done[level], m < 64u ? m : 64u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
@@ -1996,10 +1907,9 @@ __device__ __forceinline__ void lv_bases(const KParams& p, int nlev, uint32_t* b
   if (threadIdx.x == 0) {
     uint32_t b = 0;
     for (int d = 0; d <= nlev && d <= LV_MAXL; d++) {
-      base[d] = p.lv_persist ? (uint32_t)d * p.lv_scap : b;   // persistent launch: one region per level
+      base[d] = b;
       b += lv_count(p, d);
     }
-    if (p.lv_persist && blockIdx.x == 0 && p.lv_ctl->hang) record_error(p.err, ERR_HANG, 0ull);
   }
   __syncthreads();
 }
@@ -2147,7 +2057,7 @@ __global__ void k_level_acc(const LevelCtl* ctl, unsigned long long* acc) {
 // slot to -1.)
 __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max) {
   const int t = blockIdx.x * 256 + (int)threadIdx.x;
-  if (t < (int)(sizeof(LevelCtl) / 4)) {
+  if (t < 2 * (LV_MAXL + 1) + 2) {
     uint32_t v = 0;
     if (t == 0) {
       if (p.lv_pass == 0) {
@@ -2478,13 +2388,13 @@ hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t 
 
 
 // ----------------------------------------------------------------- bounce-level launchers
-template <int SPH, bool PERSIST>
+template <int SPH>
 static hipError_t launch_level(const KParams& p, int level, long cap_items, hipStream_t s, KernelEvents* kev) {
   constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
   KParams q = p;
   q.stk_slots_max = 0;                         // no ray stack in this engine
   const size_t lds = lds_layout(q, SPH, BS);
-  auto kern = k_level<SPH, BS, PERSIST>;
+  auto kern = k_level<SPH, BS>;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
@@ -2509,11 +2419,12 @@ static hipError_t launch_level(const KParams& p, int level, long cap_items, hipS
 
 static hipError_t launch_level_mode(const KParams& p, int mode, int level, long cap, hipStream_t s,
                                     KernelEvents* kev) {
-#define RTX_LVM(M)                                                                                 \
-  case M:                                                                                          \
-    return p.lv_persist ? launch_level<M, true>(p, level, cap, s, kev) : launch_level<M, false>(p, level, cap, s, kev);
-  switch (mode) { RTX_LVM(SPH_LIN_LDS) RTX_LVM(SPH_LIN_SCALAR) RTX_LVM(SPH_BVH_LDS) RTX_LVM(SPH_BVH_GLOBAL) }
-#undef RTX_LVM
+  switch (mode) {
+    case SPH_LIN_LDS: return launch_level<SPH_LIN_LDS>(p, level, cap, s, kev);
+    case SPH_LIN_SCALAR: return launch_level<SPH_LIN_SCALAR>(p, level, cap, s, kev);
+    case SPH_BVH_LDS: return launch_level<SPH_BVH_LDS>(p, level, cap, s, kev);
+    case SPH_BVH_GLOBAL: return launch_level<SPH_BVH_GLOBAL>(p, level, cap, s, kev);
+  }
   return hipErrorInvalidValue;
 }
 
@@ -2541,14 +2452,8 @@ static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_ma
                               KernelEvents* kev) {
   hipLaunchKernelGGL(k_level_begin, dim3(1), dim3(256), 0, s, q, n0_max);
   hipError_t e = hipGetLastError();
-  if (q.lv_persist) {                          // every level in one persistent launch
-    if (e == hipSuccess && nlev > 1)
-      e = hipMemsetAsync(q.lv_ready, 0, (size_t)nlev * ((q.lv_scap + 63) / 64) * sizeof(uint32_t), s);
-    if (e == hipSuccess) e = launch_level_mode(q, mode, 0, (long)n0_max * nlev, s, kev);
-  } else {
-    for (int d = 0; d < nlev && e == hipSuccess; d++)
-      e = launch_level_mode(q, mode, d, d == 0 ? (long)n0_max : (long)q.lv_scap, s, kev);
-  }
+  for (int d = 0; d < nlev && e == hipSuccess; d++)
+    e = launch_level_mode(q, mode, d, d == 0 ? (long)n0_max : (long)q.lv_scap, s, kev);
   if (e == hipSuccess) e = launch_src<SRC_LIST>(q, mode, false, maxs, n0_max, s);
   if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
   if (e == hipSuccess && q.lv_acc) {

@@ -13,7 +13,7 @@ namespace rtx {
 struct ErrState {
   unsigned int flags;              // bit (1 << code) for every code raised
   unsigned int pad;
-  unsigned long long first[6];     // per ERR_ code (rtx_vec3.h): min key (pixels: x*H + y, render_sync order; rays: index)
+  unsigned long long first[5];     // per ERR_ code (rtx_vec3.h): min key (pixels: x*H + y, render_sync order; rays: index)
 };
 
 // Bounce-level engine: one launch per tree level; the device
@@ -24,8 +24,6 @@ struct LevelCtl {
   uint32_t claim[LV_MAXL + 1];                  // 64-ray chunks claimed by the level-d launch
   uint32_t redo_n;                              // level-0 items handed to the lanes engine (capacity overflow)
   uint32_t dropped;                             // child rays that found no room (diagnostic)
-  uint32_t done[LV_MAXL + 1];                   // persistent launch: rays of level d processed
-  uint32_t hang;                                // persistent launch: a wave's wait guard fired (RTX_EHIP)
 };
 
 struct KParams {
@@ -75,11 +73,6 @@ struct KParams {
   int32_t* lv_redo_list;           // level-0 items re-rendered by the lanes engine (SRC_LIST)
   double* lv_redo_smp;             // their sample records {r, g, b, first raise}
   unsigned long long* lv_acc;      // per call: {redo_n, dropped, count[0..LV_MAXL]} summed over batches (or null)
-  // one persistent launch for every level (option "lv_persist"): level d's
-  // rays in lv_stage[0] region d-1 and records in region d (lv_scap each);
-  // per-chunk counts of written child records for the scheduler
-  int32_t lv_persist, lv_nlev;
-  uint32_t* lv_ready;              // [level][chunk] written ray records (levels >= 1)
 };
 
 // Where the sphere walk reads its records:

@@ -20,7 +20,7 @@
 
 namespace rtx {
 
-enum : uint32_t { ERR_NONE = 0, ERR_ZERO_VEC = 1, ERR_COLOR_GT1 = 2, ERR_DOMAIN = 3, ERR_TYPE = 4, ERR_HANG = 5, ERR_N = 6 };
+enum : uint32_t { ERR_NONE = 0, ERR_ZERO_VEC = 1, ERR_COLOR_GT1 = 2, ERR_DOMAIN = 3, ERR_TYPE = 4, ERR_N = 5 };
 
 struct V3 {
   double x, y, z;

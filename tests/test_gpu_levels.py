@@ -67,13 +67,12 @@ SCENES_SMALL = [
 ]
 
 
-@pytest.mark.parametrize("persist", [0, 1])
 @pytest.mark.parametrize("world,camera,ov", SCENES_SMALL)
-def test_levels_bit_identical_to_lanes_and_match_oracle(gpu, world, camera, ov, persist):
+def test_levels_bit_identical_to_lanes_and_match_oracle(gpu, world, camera, ov):
     from oracle.c_oracle import Oracle
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=3)
-    r = _renderer(sd, cd, 1, lv_persist=persist)
+    r = _renderer(sd, cd, 1)
     lv = r.render(seed=3)
     assert _same(lv, lanes)
     st = r.level_stats()
@@ -103,9 +102,6 @@ def test_levels_match_golden(gpu, name):
     dict(lv_stage_pct=5, lv_floor=0),                    # staging overflow: re-rendered by the lanes engine
     dict(lv_rec_pct=101, lv_floor=0),                    # tree-record overflow at level 1
     dict(lv_batch=1000, lv_stage_pct=20, lv_rec_pct=150, lv_floor=0),
-    dict(lv_persist=1, lv_batch=512),                    # one persistent launch per batch
-    dict(lv_persist=1, lv_stage_pct=40, lv_floor=0),     # ... with staging overflow
-    dict(lv_persist=1, lv_batch=1),
 ])
 def test_levels_batches_and_overflow_change_no_bit(gpu, opts):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
@@ -114,7 +110,7 @@ def test_levels_batches_and_overflow_change_no_bit(gpu, opts):
     lv = r.render(seed=5)
     assert _same(lv, lanes)
     st = r.level_stats()
-    if "lv_stage_pct" in opts or "lv_rec_pct" in opts:   # (persist: records have a region per level)
+    if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
         assert st["redo"] > 0, st                         # the overflow path ran
     assert sum(st["rays"]) > 0
 
@@ -124,26 +120,20 @@ def test_levels_adaptive_extras_batched(gpu):
     sd, cd = _scene("mix_world.yml", "mix_camera.yml", width=64, height=36, pre_sample_times=2,
                     max_sample_times=6, variant_threshold=1e-4)
     lanes = _renderer(sd, cd, 0).render(seed=9)
-    for opts in (dict(), dict(lv_batch=300), dict(lv_batch=64, lv_stage_pct=30, lv_floor=0),
-                 dict(lv_persist=1), dict(lv_persist=1, lv_batch=300)):
+    for opts in (dict(), dict(lv_batch=300), dict(lv_batch=64, lv_stage_pct=30, lv_floor=0)):
         assert _same(_renderer(sd, cd, 1, **opts).render(seed=9), lanes), opts
 
 
 def test_levels_c2_full_frame_identical_to_lanes(gpu):
     """C2 (the metric config) at full 1920x1080, 4xAA, depth 5: every pixel of
-    the bounce-level frame (per-level launches and the persistent launch)
-    equals the lanes engine's, no sample overflowed."""
+    the bounce-level frame equals the lanes engine's, no sample overflowed."""
     sd, cd = _scene("c2_world.yml", "c2_camera.yml")
     lanes = _renderer(sd, cd, 0).render()
-    rays = None
-    for persist in (0, 1):
-        r = _renderer(sd, cd, 1, lv_persist=persist)
-        lv = r.render()
-        assert _same(lv, lanes), persist
-        st = r.level_stats()
-        assert st["redo"] == 0 and st["rays"][0] == 32400 * 256, st
-        assert rays is None or st["rays"] == rays
-        rays = st["rays"]
+    r = _renderer(sd, cd, 1)
+    lv = r.render()
+    assert _same(lv, lanes)
+    st = r.level_stats()
+    assert st["redo"] == 0 and st["rays"][0] == 32400 * 256, st
 
 
 def test_levels_tiles_and_subregions(gpu):
