@@ -814,7 +814,6 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
                sz_extra = al256((npx + 64) * 4);
   const size_t total = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
-  HIPCHK(c, hipMemsetAsync(c->d_lvstats, 0, sizeof(unsigned long long) * (LV_MAXL + 3), stream));
   char* buf = nullptr;
   HIPCHK(c, hipMallocAsync((void**)&buf, total, stream));
   char* q = buf;

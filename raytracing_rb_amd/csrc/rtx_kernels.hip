@@ -1867,7 +1867,7 @@ __device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base
                                           uint32_t* lo, uint32_t* hi, int st, int sd, uint32_t& err_out) {
   int sp = 0;
   V3 sum = v3(0.0, 0.0, 0.0);
-  uint32_t err = 0;
+  uint32_t err = 0, pf = 0;
   bool gt1 = false;
   int lev = 0;
   uint32_t q = (uint32_t)root;
@@ -1892,6 +1892,12 @@ __device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base
       lo[sp * st] = hdr.y;
       hi[sp * st] = hdr.y + nch;
       sp++;
+      // the children's records (contiguous, slot order) are fetched now, all
+      // at once: the walk's dependent chain becomes the tree's depth, not
+      // its size (the loads' values are consumed only at the end)
+      const char* c0 = p.lv_rec + (size_t)(base[lev + 1] + hdr.y) * p.lv_rec_bytes;
+      pf += *reinterpret_cast<const uint32_t*>(c0) +
+            *reinterpret_cast<const uint32_t*>(c0 + (size_t)(nch - 1) * p.lv_rec_bytes);
     }
     // next: the last unvisited child of the deepest pending range (LIFO pop)
     while (sp > 0 && hi[(sp - 1) * st] == lo[(sp - 1) * st]) sp--;
@@ -1899,10 +1905,13 @@ __device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base
     q = --hi[(sp - 1) * st];
     lev = sp;
   }
+  asm volatile("" : : "v"(pf));               // the prefetches' values, consumed
   err_out = err ? err : (gt1 ? (uint32_t)ERR_COLOR_GT1 : 0u);
   return sum;
 }
 
+// Block 0 also adds the batch's level statistics to lv_acc (rtx_level_stats):
+// every level launch of the batch has ended.
 __device__ __forceinline__ void lv_bases(const KParams& p, int nlev, uint32_t* base) {
   if (threadIdx.x == 0) {
     uint32_t b = 0;
@@ -1910,6 +1919,12 @@ __device__ __forceinline__ void lv_bases(const KParams& p, int nlev, uint32_t* b
       base[d] = b;
       b += lv_count(p, d);
     }
+  }
+  if (blockIdx.x == 0 && p.lv_acc) {
+    const int t = (int)threadIdx.x;
+    if (t == 0) p.lv_acc[0] += p.lv_ctl->redo_n;
+    if (t == 1) p.lv_acc[1] += p.lv_ctl->dropped;
+    if (t < LV_MAXL + 1) p.lv_acc[2 + t] += p.lv_ctl->count[t];
   }
   __syncthreads();
 }
@@ -2043,20 +2058,17 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
   if (err) record_error(p.err, err, px_key(x, y, cam.height));
 }
 
-// Level statistics of a call: redo items, dropped children and rays per level,
-// summed over its batches (rtx_level_stats).
-__global__ void k_level_acc(const LevelCtl* ctl, unsigned long long* acc) {
-  const int t = (int)threadIdx.x;
-  if (t == 0) acc[0] += ctl->redo_n;
-  if (t == 1) acc[1] += ctl->dropped;
-  if (t < LV_MAXL + 1) acc[2 + t] += ctl->count[t];
-}
-
 // Per batch: the control block, count[0] = the batch's level-0 items (pass 1:
-// from the device-side extra count).  (Every level-0 lane sets its item's redo
-// slot to -1.)
-__global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max) {
+// from the device-side extra count), the lanes engine's work counter (the
+// re-render launch); the call's first batch also the extra-list count and the
+// level statistics.  (Every level-0 lane sets its item's redo slot to -1.)
+__global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int first) {
   const int t = blockIdx.x * 256 + (int)threadIdx.x;
+  if (t == 0) *p.work = 0;
+  if (first) {
+    if (t == 0) *p.extra_count = 0;
+    if (p.lv_acc && t < LV_MAXL + 3) p.lv_acc[t] = 0;
+  }
   if (t < 2 * (LV_MAXL + 1) + 2) {
     uint32_t v = 0;
     if (t == 0) {
@@ -2285,6 +2297,7 @@ static size_t lds_layout(KParams& p, int mode, int bs) {
 }
 
 static thread_local KernelEvents* g_kev = nullptr;   // set by launch_render for its launches
+static thread_local bool g_work_zeroed = false;      // launch_one: the work counter is already zero
 
 // Persistent launch: as many workgroups as can be resident at once (the
 // occupancy API; an over-estimate only leaves blocks that start after the
@@ -2307,7 +2320,7 @@ static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   long blocks = std::min<long>(need, (long)cus * per_cu);
   blocks = std::min<long>(blocks, (long)p.stk_glb_lanes / BS);   // lanes with a global ray-stack region
   if (blocks <= 0) return hipSuccess;
-  e = hipMemsetAsync(p.work, 0, sizeof(int), s);
+  if (!g_work_zeroed) e = hipMemsetAsync(p.work, 0, sizeof(int), s);
   if (e != hipSuccess) return e;
   KernelEvents* kev = g_kev && g_kev->n < g_kev->max ? g_kev : nullptr;
   if (kev) (void)hipEventRecord(kev->ev[2 * kev->n], s);
@@ -2449,17 +2462,16 @@ static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t
 // One batch: reset, the levels, the lanes-engine re-render of overflowed
 // samples (exits at once when there are none), the tree reduction.
 static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_max, int fin_threads, hipStream_t s,
-                              KernelEvents* kev) {
-  hipLaunchKernelGGL(k_level_begin, dim3(1), dim3(256), 0, s, q, n0_max);
+                              KernelEvents* kev, bool first) {
+  hipLaunchKernelGGL(k_level_begin, dim3(1), dim3(256), 0, s, q, n0_max, first ? 1 : 0);
   hipError_t e = hipGetLastError();
   for (int d = 0; d < nlev && e == hipSuccess; d++)
     e = launch_level_mode(q, mode, d, d == 0 ? (long)n0_max : (long)q.lv_scap, s, kev);
+  g_work_zeroed = true;                        // k_level_begin zeroed the re-render launch's counter
   if (e == hipSuccess) e = launch_src<SRC_LIST>(q, mode, false, maxs, n0_max, s);
+  g_work_zeroed = false;
   if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
-  if (e == hipSuccess && q.lv_acc) {
-    hipLaunchKernelGGL(k_level_acc, dim3(1), dim3(128), 0, s, q.lv_ctl, q.lv_acc);
-    e = hipGetLastError();
-  }
+
   return e;
 }
 
@@ -2471,14 +2483,14 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
   batch_tiles = std::max(1, std::min(batch_tiles, tiles));
   const int per_tile = 64 * p.pre;
   p.tile_order = nullptr;
-  hipError_t e = hipMemsetAsync(p.extra_count, 0, sizeof(int32_t), s);
+  hipError_t e = hipSuccess;                   // (the first batch's k_level_begin zeroes the extra count)
   for (int t0 = 0; t0 < tiles && e == hipSuccess; t0 += batch_tiles) {
     KParams q = p;
     q.lv_pass = 0;
     q.lv_t0 = t0;
     q.lv_tiles = std::min(batch_tiles, tiles - t0);
     q.lv_e0 = q.lv_entries = 0;
-    e = level_batch(q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles, s, kev);
+    e = level_batch(q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles, s, kev, t0 == 0);
   }
   if (e != hipSuccess || p.max_samples <= p.pre) return e;
   // extra samples of the pixels the variance test listed (count on the device)
@@ -2491,7 +2503,7 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
     q.lv_e0 = e0;
     q.lv_entries = std::min(entries, npx - e0);
     q.lv_t0 = q.lv_tiles = 0;
-    e = level_batch(q, mode, maxs, nlev, q.lv_entries * n_extra, q.lv_entries, s, kev);
+    e = level_batch(q, mode, maxs, nlev, q.lv_entries * n_extra, q.lv_entries, s, kev, false);
   }
   return e;
 }
