@@ -11,15 +11,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "librtx.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("rtx_kernels.hip", "rtx_capi.cpp")]
-HEADERS = [os.path.join(CSRC, f) for f in ("rtx_scene.h", "rtx_vec3.h", "rtx_launch.h")] + [
+SOURCES = [os.path.join(CSRC, f) for f in ("rtx_kernels.hip", "rtx_levels.hip", "rtx_capi.cpp")]
+HEADERS = [os.path.join(CSRC, f) for f in ("rtx_scene.h", "rtx_vec3.h", "rtx_launch.h", "rtx_device.h")] + [
     os.path.join(ROOT, "include", "rtx.h")]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: no FMA contraction anywhere — every binary64 operation rounds
 # exactly like the reference's Ruby + C-extension arithmetic.
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fno-fast-math", "-std=c++17", "-fPIC",
-         "-shared", "-Wall", "-Wno-unused-result", "-Wno-unused-value"]
+         "-Wall", "-Wno-unused-result", "-Wno-unused-value"]
 
 
 # RCCL for rtx_render_multi's gather over xGMI (librccl.so ships with ROCm).
@@ -54,11 +54,33 @@ def stale():
 
 
 def build(force=False, verbose=False, out=None, defines=()):
+    """Each translation unit compiled to an object in parallel (build/obj/), then linked."""
     out = out or OUT
     if not force and out == OUT and not stale():
         return OUT
     # `defines`: NAME[=VALUE] macros; entries starting with "-" are raw compiler flags
-    cmd = [HIPCC] + FLAGS + [d if d.startswith("-") else "-D" + d for d in defines] + ["-o", out + ".tmp"] + SOURCES + LIBS
+    dflags = [d if d.startswith("-") else "-D" + d for d in defines]
+    odir = os.path.join(ROOT, "build", "obj", os.path.basename(out))
+    os.makedirs(odir, exist_ok=True)
+    objs, procs = [], []
+    tag = os.path.join(odir, "flags")                # objects are reused only under the same flags
+    same = os.path.exists(tag) and open(tag).read() == " ".join(FLAGS + dflags)
+    with open(tag, "w") as f:
+        f.write(" ".join(FLAGS + dflags))
+    newest_dep = max(os.path.getmtime(p) for p in HEADERS + [__file__])
+    for src in SOURCES:
+        obj = os.path.join(odir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if same and os.path.exists(obj) and os.path.getmtime(obj) > max(newest_dep, os.path.getmtime(src)):
+            continue
+        cmd = [HIPCC] + FLAGS + dflags + ["-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((subprocess.Popen(cmd), cmd))
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out + ".tmp"] + objs + LIBS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

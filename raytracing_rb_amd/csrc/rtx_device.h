@@ -1,0 +1,1034 @@
+// rtx_device.h — device code shared by the two kernel translation units:
+// rtx_kernels.hip (lanes engine, finalize, tile order, quantize) and
+// rtx_levels.hip (bounce-level engine).  Scene walks, shading, Vec3, RNG,
+// the work-item decoding, and the LDS layout of a walk workgroup.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "rtx_launch.h"
+#include "rtx_scene.h"
+#include "rtx_vec3.h"
+
+namespace rtx {
+
+constexpr double PI = 3.141592653589793;   // Math::PI == M_PI
+constexpr double EPS = 1e-5;               // Alex::EPSILON (src/libs/algebra.rb:2)
+constexpr float CULL_M = 2e-5f;            // pre-test margin (exact culls)
+
+struct Ray {
+  V3 o, d;                          // Alex::Ray#position, #front
+};
+
+struct Item {                       // one queue entry of RayTracer (ray_tracer.rb:21-30)
+  Ray ray;
+  V3 att;
+  uint64_t path;                    // RNG ray-path id (DESIGN.md "RNG")
+  int32_t depth;
+  int32_t pad;
+};
+
+enum { C_RAYS = 0, C_SPHERE_TESTS, C_SPHERE_HITS, C_PLANE_TESTS, C_BOX_TESTS, C_SHADE_HITS,
+       C_COVER_SPHERE, C_COVER_PLANE, C_COVER_BOX, C_HIGHLIGHT_TESTS, C_PRIMARY, C_N };
+
+enum { M_NEED = 0, M_EXTEND = 1, M_SHADOW = 2, M_DONE = 3, M_FETCH = 4 };
+
+// Out-of-line the rarely-executed shading blocks (1) or inline everything (0).
+#ifndef RTX_OUTLINE_SHADING
+#define RTX_OUTLINE_SHADING 0
+#endif
+#if RTX_OUTLINE_SHADING
+#define RTX_SHADE_FN __device__ __noinline__
+#else
+#define RTX_SHADE_FN __device__ __forceinline__
+#endif
+
+// The scene is read-only for the whole launch: reading it through the constant
+// address space (4) lets wave-uniform indices become scalar loads (s_load) into
+// SGPRs instead of per-lane vector loads.
+#define RTX_CONST __attribute__((address_space(4)))
+template <typename T>
+__device__ __forceinline__ const RTX_CONST T* cptr(const T* p) {
+  return (const RTX_CONST T*)(p);
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2, SRC_LIST = 3 };
+#ifndef RTX_CLAIM_MAX
+#define RTX_CLAIM_MAX 64     // cap on the items a wave claims beyond its lanes' need (with expensive tiles first + Morton items: 32: C2 8.68 ms, 64: 8.30 ms, 96: 9.13 ms, 128: 9.58 ms — expensive tiles pile up in one wave)
+#endif
+
+// Diagnostic build only (-DRTX_STAMPS=1): per-wave shader-clock time spent in
+// each phase of the lane state machine, summed into rtx_stamps[] (read with
+// rtxdbg_read_stamps).  The shipped library is built without it.
+#ifndef RTX_CLAIM_DIV
+#define RTX_CLAIM_DIV 2      // a claim's extra items: at most remaining / (RTX_CLAIM_DIV x waves) (C2: 2: 8.27 ms, 4: 8.35-8.48 ms, 8: 8.37 ms)
+#endif
+#ifndef RTX_CLAIM_ALIGN
+#define RTX_CLAIM_ALIGN 1    // claims rounded up to a multiple of this (every claimed range then starts aligned; 64: C2 9.2 ms, worse)
+#endif
+#ifndef RTX_PROBE_W
+#define RTX_PROBE_W 0        // k_tile_cost hit weights: 0 (1, +1 reflective, +3 refractive), 1 (1, +1/+2 by reflectance, +6 refractive)
+#endif
+#ifndef RTX_ITEM_ORDER
+#define RTX_ITEM_ORDER 1     // SRC_PIXELS items within a tile: 1 (pixel Morton, sample; C2 8.75 -> 8.65 ms, C4 505 -> 495 ms), 0 (sample, pixel row-major)
+#endif
+#ifndef RTX_DIAG_NOEXACT
+#define RTX_DIAG_NOEXACT 0
+#endif
+#ifndef RTX_STAMPS
+#define RTX_STAMPS 0
+#endif
+#ifndef RTX_LVL_WPS
+#define RTX_LVL_WPS 2        // waves per SIMD k_level is compiled for
+#endif
+#ifndef RTX_LV_CLAIM_AHEAD
+#define RTX_LV_CLAIM_AHEAD 0 // k_level claims its next 64-ray chunk while working on the current one (C2 6.26 vs 6.22 ms: off)
+#endif
+static __device__ unsigned long long rtx_stamps[16];   // one per translation unit (no -fgpu-rdc)
+__device__ __forceinline__ unsigned long long wall() {   // 100 MHz constant clock, same on every XCD
+#if RTX_STAMPS
+  return __builtin_amdgcn_s_memrealtime();
+#else
+  return 0;
+#endif
+}
+__device__ __forceinline__ unsigned long long stamp() {
+#if RTX_STAMPS
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+#else
+  return 0;
+#endif
+}
+
+// sin and cos of one angle: separate ocml calls (measured 4 % faster on C2 than
+// ocml's sincos; both give the same bits).  -DRTX_SEPARATE_SINCOS=0 for sincos.
+#ifndef RTX_SEPARATE_SINCOS
+#define RTX_SEPARATE_SINCOS 1
+#endif
+// Transcendentals are real calls by default: inlined into the state machine,
+// their 64-bit polynomial coefficients are hoisted to the kernel entry and
+// spilled, and every sin/cos/acos then waits on a chain of serialized scratch
+// reloads (seen in the gfx950 ISA).  -DRTX_INLINE_MATH=1 inlines them again.
+#ifndef RTX_INLINE_MATH
+#define RTX_INLINE_MATH 0
+#endif
+#if RTX_INLINE_MATH
+#define RTX_MATH_FN __device__ __forceinline__
+#else
+#define RTX_MATH_FN __device__ __noinline__
+#endif
+RTX_MATH_FN double rx_sin(double x) { return sin(x); }
+RTX_MATH_FN double rx_cos(double x) { return cos(x); }
+RTX_MATH_FN double rx_asin(double x) { return asin(x); }
+RTX_MATH_FN double rx_acos(double x) { return acos(x); }
+RTX_MATH_FN double rx_pow(double x, double y) { return pow(x, y); }
+RTX_MATH_FN void rx_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+
+#if RTX_SEPARATE_SINCOS
+#define RTX_SINCOS(x, s, c) (*(s) = rx_sin(x), *(c) = rx_cos(x))
+#else
+#define RTX_SINCOS(x, s, c) rx_sincos((x), (s), (c))
+#endif
+
+// A lane's first raise (low byte) plus GT1_PENDING: rt_reduce's "color greater
+// than 1" is raised by the FIFO drain after the whole tree (ray_tracer.rb:39-45),
+// so it is held back and applies only if no rt_map of the tree raised (end_tree).
+constexpr uint32_t GT1_PENDING = 0x80000000u;
+__device__ __forceinline__ void seterr(uint32_t& err, uint32_t code) {
+  if (!(err & 0xffu)) err = (err & GT1_PENDING) | code;
+}
+__device__ __forceinline__ uint32_t end_tree(uint32_t err) {
+  const uint32_t code = err & 0xffu;
+  return code ? code : ((err & GT1_PENDING) ? (uint32_t)ERR_COLOR_GT1 : 0u);
+}
+
+// ----------------------------------------------------------------- spheres
+// Exact Sphere#intersect (sphere.rb:60-85); r2 = front.r2, dn = front.normalize.
+__device__ __forceinline__ bool sphere_exact(V3 C, double R, V3 o, V3 d, V3 dn, double r2, V3& hit, bool& in) {
+  const V3 oc = vsub(C, o);                       // center - ray.position
+  const double q = vdot(oc, d);
+  const double t = q / r2;
+  const double s = vsq(oc);                       // |position - center|^2 (same bits)
+  // The reference returns nil when the origin is outside and t < 0 (sphere.rb:80).
+  // s > R*R*(1 + 1e-12) proves |o - C|.r > R without the sqrt, so
+  // this exit is taken only where the full evaluation below would return nil.
+  if (t < 0 && s > R * R * (1.0 + 1e-12)) return false;
+  const V3 np = vadd(o, vsc(d, t));
+  const double nd = vr(vsub(np, C));
+  if (!(nd <= R)) return false;                   // inner?(nearest_point)
+  const double h = sqrt(R * R - nd * nd);         // radius**2 - nearest_dis**2
+  const V3 vec = vsc(dn, h);
+  const bool from_inner = sqrt(s) <= R;           // inner?(ray.position)
+  in = !from_inner;
+  hit = in ? vsub(np, vec) : vadd(np, vec);
+  if (!from_inner && t < 0) return false;
+  return true;
+}
+
+// ----------------------------------------------------------------- planes
+// Plane#intersect (plane.rb:38-51).  p = plane record (PLANE_GEO doubles).
+template <typename P>
+__device__ __forceinline__ bool plane_hit(P p, V3 o, V3 d, V3& hit) {
+  const V3 F = v3(p[3], p[4], p[5]);
+  const double den = vdot(F, d);
+  if (den == 0) return false;
+  const double t = vdot(vsub(v3(p[0], p[1], p[2]), o), F) / den;
+  hit = vadd(o, vsc(d, t));
+  if (t < 0) return false;
+  return true;
+}
+
+template <typename P>
+__device__ __forceinline__ void plane_uv(P p, V3 pos, double& u, double& v) {
+  const V3 a = vsub(pos, v3(p[0], p[1], p[2]));   // plane.rb:81-85
+  u = vdot(a, v3(p[6], p[7], p[8])) / p[12];
+  v = vdot(a, v3(p[9], p[10], p[11])) / p[13];
+}
+
+// Box#intersect (box.rb:79-97): nearest face hit inside its u,v square.
+template <typename P>
+__device__ __forceinline__ bool box_hit(P b, V3 o, V3 d, V3& hit, int& face) {
+  double nearest = __builtin_inf();
+  bool found = false;
+  for (int i = 0; i < 6; i++) {
+    const P p = b + i * PLANE_GEO;
+    V3 h;
+    if (plane_hit(p, o, d, h)) {
+      double u, v;
+      plane_uv(p, h, u, v);
+      if (-0.5 <= u && u <= 0.5 && -0.5 <= v && v <= 0.5) {
+        const double dd = vr(vsub(h, o));
+        if (dd < nearest) {
+          nearest = dd;
+          hit = h;
+          face = i;
+          found = true;
+        }
+      }
+    }
+  }
+  return found;
+}
+
+// Sphere#cover_area's penumbra (sphere.rb:31-56) once the binary factor is 1.
+RTX_SHADE_FN double penumbra(V3 C, double R, V3 T, V3 lt, double radius, uint32_t& err) {
+  const double t = vdot(vsub(C, T), lt) / vr2(lt);
+  const V3 x1 = vadd(T, vsc(lt, t));
+  const double r1 = radius * (vr(vsub(x1, T)) / vr(lt));
+  const double d = vr(vsub(x1, C));
+  if (d >= r1 + R) return 0.0;
+  const double s1 = PI * r1 * r1;
+  if (d > fabs(R - r1)) {
+    double c1 = (r1 * r1 + d * d - R * R) / (2.0 * r1 * d);
+    double c2 = (R * R + d * d - r1 * r1) / (2.0 * R * d);
+    if (c1 > 1.0) c1 = 1.0;
+    if (c2 > 1.0) c2 = 1.0;
+    if (c1 < -1.0 || c2 < -1.0) seterr(err, ERR_DOMAIN);     // Math::DomainError
+    const double th1 = rx_acos(c1), th2 = rx_acos(c2);
+    const double ds = ((th1 - rx_sin(th1)) * r1 * r1 + (th2 - rx_sin(th2)) * R * R) / 2.0;
+    return 1.0 * ds / s1;
+  }
+  if (r1 > R) return 1.0 * PI * R * R / s1;
+  return 1.0;
+}
+
+// ----------------------------------------------------------------- the query
+// One ordered walk over every object with ray (o, d), for every active lane.
+//   EXTEND: World#intersect — nearest hit (strict <, YAML order) -> best/besti.
+//   SHADOW: World#lit_area for light L (o = target T, d = L - T) -> total
+//           (1 - ordered sum of cover areas; zero covers skipped: exact).
+template <bool COUNT, typename SPH>
+__device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o, V3 d,
+                                      V3 L, double radius, double& best, int& besti, V3& bhit, bool& bin,
+                                      double& total, uint32_t& err, unsigned long long* cnt) {
+  const double r = vr(d);
+  const double r2 = r * r;                        // front.r2
+  // front.normalize is needed only by a sphere that passes the pre-test:
+  // computed on first use (same bits wherever it is computed).
+#ifndef RTX_LAZY_DN
+#define RTX_LAZY_DN 0
+#endif
+  V3 dn = d;
+  bool have_dn = false;
+  if (!RTX_LAZY_DN) {
+    if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r);
+    have_dn = true;
+  }
+  // float32 pre-test constants (exact culls)
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float dd = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+  const float Sx = fabsf(ox) + fabsf(oy) + fabsf(oz) + S.sph_scale;
+  const float ms2 = CULL_M * Sx * Sx;
+  const float kline = dd * ms2;
+  const float qneg = -CULL_M * Sx * sqrtf(dd);
+  if (COUNT) {
+    if (ext) {
+      cnt[C_SPHERE_TESTS] += S.n_sphere;
+      cnt[C_PLANE_TESTS] += S.n_plane;
+      cnt[C_BOX_TESTS] += S.n_box;
+    } else {
+      cnt[C_COVER_SPHERE] += S.n_sphere;
+      cnt[C_COVER_PLANE] += S.n_plane;
+      cnt[C_COVER_BOX] += S.n_box;
+    }
+  }
+  const RTX_CONST Run* runs = cptr(S.runs);
+  const RTX_CONST Sphere64* sph64 = cptr(S.sph64);
+  const int n_runs = uni(S.n_runs);
+  for (int ri = 0; ri < n_runs; ri++) {
+    Run run;
+    run.type = uni(runs[ri].type);
+    run.obj0 = uni(runs[ri].obj0);
+    run.count = uni(runs[ri].count);
+    run.rec0 = uni(runs[ri].rec0);
+    if (run.type == OBJ_SPHERE) {
+      // Pre-test 4 spheres at a time (4 LDS reads in flight), then run the
+      // exact test, in order, for those this lane cannot rule out.
+      for (int k0 = 0; k0 < run.count; k0 += 4) {
+        // The record table is padded to a multiple of 4 (rtx_capi.cpp), so
+        // the group loads are unconditional; records past the run are masked.
+        float4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {                // {cx, cy, cz, R^2}, wave-uniform
+          const int b = 4 * (run.rec0 + k0 + u);
+          c[u].x = sph[b];
+          c[u].y = sph[b + 1];
+          c[u].z = sph[b + 2];
+          c[u].w = sph[b + 3];
+        }
+        uint32_t keep = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const float ocx = c[u].x - ox, ocy = c[u].y - oy, ocz = c[u].z - oz;
+          const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+          const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
+          const bool miss_line = __builtin_fmaf(s, dd, -q * q) > __builtin_fmaf(dd, c[u].w, kline);
+          const bool behind = q < qneg && s > c[u].w + ms2;
+          keep |= (miss_line || behind) ? 0u : (1u << u);
+        }
+        if (k0 + 4 > run.count) keep &= (1u << (run.count - k0)) - 1u;
+#if RTX_STAMPS == 2
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
+          for (int u = 0; u < 4; u++) atomicAdd(&rtx_stamps[6], __ballot(keep >> u & 1) ? 1ull : 0ull);
+        }
+        atomicAdd(&rtx_stamps[7], (unsigned long long)__builtin_popcount(keep));
+#endif
+#if RTX_DIAG_NOEXACT
+        keep = 0;                                    // diagnostic only: wrong results
+#endif
+        if (!keep) continue;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (!(keep >> u & 1)) continue;
+          const int k = k0 + u;
+          const RTX_CONST Sphere64& sp = sph64[run.rec0 + k];
+          const V3 C = v3(sp.c[0], sp.c[1], sp.c[2]);
+          const double sr = sp.r;
+          if (!have_dn) {
+            if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r);
+            have_dn = true;
+          }
+          V3 hit;
+          bool in;
+          if (!sphere_exact(C, sr, o, d, dn, r2, hit, in)) continue;
+          if (ext) {
+            if (COUNT) cnt[C_SPHERE_HITS]++;
+            const double dist = vr(vsub(o, hit));    // Ray#distance
+            if (dist < best) {
+              best = dist;
+              besti = run.obj0 + k;
+              bhit = hit;                              // kept for shading (same bits as a re-evaluation)
+              bin = in;
+            }
+          } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
+            total -= penumbra(C, sr, o, d, radius, err);
+          }
+        }
+      }
+    } else if (run.type == OBJ_PLANE) {
+      for (int k = 0; k < run.count; k++) {
+        V3 hit;
+        if (!plane_hit(cptr(S.planes) + (size_t)(run.rec0 + k) * PLANE_GEO, o, d, hit)) continue;
+        if (ext) {
+          const double dist = vr(vsub(o, hit));
+          if (dist < best) {
+            best = dist;
+            besti = run.obj0 + k;
+            bhit = hit;
+            bin = true;
+          }
+        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {
+          total -= 1.0;
+        }
+      }
+    } else {
+      for (int k = 0; k < run.count; k++) {
+        V3 hit;
+        int face;
+        if (!box_hit(cptr(S.boxes) + (size_t)(run.rec0 + k) * BOX_GEO, o, d, hit, face)) continue;
+        if (ext) {
+          const double dist = vr(vsub(o, hit));
+          if (dist < best) {
+            best = dist;
+            besti = run.obj0 + k;
+          }
+        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {
+          total -= 1.0;
+        }
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------- the query, hierarchical
+// The same query answered through the four-wide box hierarchy (rtx_scene.h).
+// Every lane traverses on its own (per-lane stack in LDS, nearest child first,
+// "while-while": lanes descend through inner nodes together, then process
+// their leaves together).  A lane skips a child box when a float32 slab test
+// of the box dilated by m*S (the margin of DESIGN.md §2.1) proves that every
+// sphere below it
+//   * misses the ray's line, or lies wholly behind the origin (nil), or
+//   * EXTEND: is farther than the lane's current best hit (loses the strict <
+//     of world.rb:48-50 even on a tie), or
+//   * SHADOW: lies wholly beyond the light (cover factor 0, sphere.rb:30).
+// Order independence makes the result bit-identical to the ordered walk:
+//   * EXTEND keeps the lexicographic minimum of (distance, object index) below
+//     max_distance, which is exactly what the ordered strict-< scan returns;
+//   * SHADOW collects the non-zero covers in a per-lane list sorted by object
+//     index and subtracts them in that order (world.rb:64-67).  A lane whose
+//     list overflows COVER_K repeats the ordered linear walk.
+// Planes and boxes are few: they are walked first (tightening `best`).
+//
+// Slab-test rounding: each computed slab bound errs by a few float32 ulps of
+// (|box coordinate| + |o| + m*S) / |d_axis| <= 1e-6 * S / |d_axis|, far inside
+// the dilation m*S / |d_axis| (m = 2e-5), so the computed interval contains
+// the exact interval of the undilated box; direction components below
+// 1e-20 |d|_1 are replaced by that value (a deviation of < 1e-15 over any
+// distance the scene spans) so every reciprocal is finite.
+__device__ __forceinline__ bool lex_better(double dist, int obj, double best, int besti) {
+  return dist < best || (dist == best && besti >= 0 && obj < besti);
+}
+
+template <int BS>
+__device__ __forceinline__ void push_cover(int* ci, double* cv, int& n, bool& ovf, int obj, double val) {
+  if (n >= COVER_K) {
+    ovf = true;
+    return;
+  }
+  int k = n;                                        // insertion sort by object index
+  while (k > 0) {
+    const int pi = ci[(k - 1) * BS];
+    if (pi < obj) break;
+    ci[k * BS] = pi;
+    cv[k * BS] = cv[(k - 1) * BS];
+    k--;
+  }
+  ci[k * BS] = obj;
+  cv[k * BS] = val;
+  n++;
+}
+
+// Resumable: a lane whose walk is still running when fewer than `postpone`
+// lanes of its wave are is postponed (returns false) with its walk in
+// ref / sp (+ the LDS stack) / ncov / ovf (+ the LDS cover list) and best /
+// besti / bhit / bin, and continues where it stopped at the next call with
+// resume = true; meanwhile the wave's other lanes shade and start new
+// queries instead of idling.  Every lane visits the same nodes and leaves in
+// the same order either way, so the result is unchanged.
+template <int BS, bool PP, typename NP, typename LP>
+__device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4, int* stk, int* ci, double* cv,
+                                          bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
+                                          V3& bhit, bool& bin, double& total, uint32_t& err, int& ref, int& sp,
+                                          int& ncov, bool& ovf, bool resume, int postpone) {
+  const double r = vr(d);
+  const double r2 = r * r;                        // front.r2
+  V3 dn = d;
+  if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r); // front.normalize (same bits as the walk)
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float dd = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+  const float Sx = fabsf(ox) + fabsf(oy) + fabsf(oz) + S.sph_scale;
+  const float ms2 = CULL_M * Sx * Sx;
+  const float mS = CULL_M * Sx;
+  const float kline = dd * ms2;
+  const float qneg = -CULL_M * Sx * sqrtf(dd);
+  // slab set-up: reciprocal direction and the dilated origin terms
+  const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
+  const float tiny = 1e-20f * l1;
+  const float ex = fabsf(dx) < tiny ? copysignf(tiny, dx) : dx;
+  const float ey = fabsf(dy) < tiny ? copysignf(tiny, dy) : dy;
+  const float ez = fabsf(dz) < tiny ? copysignf(tiny, dz) : dz;
+  const float ix = 1.0f / ex, iy = 1.0f / ey, iz = 1.0f / ez;
+  const float ax = (ox + mS) * ix, ay = (oy + mS) * iy, az = (oz + mS) * iz;   // lo - mS side
+  const float bx = (ox - mS) * ix, by = (oy - mS) * iy, bz = (oz - mS) * iz;   // hi + mS side
+  // A non-finite or zero ray makes no cull (comparisons would be unordered).
+  const bool fin = __builtin_isfinite(dd) && __builtin_isfinite(Sx) && l1 > 0.0f && __builtin_isfinite(ix) &&
+                   __builtin_isfinite(iy) && __builtin_isfinite(iz);
+  if (!fin) {
+    // no float32 cull is valid for this ray: the ordered linear walk (same result)
+    if (!ext) total = 1.0;
+    query<false>(S, cptr(S.sph32), ext, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
+    return true;
+  }
+  const float rf = (float)r;
+  // far bound on the ray parameter: EXTEND the current best hit, SHADOW the light
+  float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + mS / rf;
+  if (!resume) {
+    ncov = 0;
+    ovf = false;
+    ref = S.bvh_root;
+    sp = 0;
+  }
+
+  // planes and boxes first, in run order (their order does not matter either)
+  const RTX_CONST Run* runs = cptr(S.runs);
+  const int n_runs = resume ? 0 : uni(S.n_runs);
+  for (int ri = 0; ri < n_runs; ri++) {
+    const int type = uni(runs[ri].type);
+    if (type == OBJ_SPHERE) continue;
+    const int obj0 = uni(runs[ri].obj0), count = uni(runs[ri].count), rec0 = uni(runs[ri].rec0);
+    for (int k = 0; k < count; k++) {
+      V3 hit;
+      bool h;
+      if (type == OBJ_PLANE) {
+        h = plane_hit(cptr(S.planes) + (size_t)(rec0 + k) * PLANE_GEO, o, d, hit);
+      } else {
+        int face;
+        h = box_hit(cptr(S.boxes) + (size_t)(rec0 + k) * BOX_GEO, o, d, hit, face);
+      }
+      if (!h) continue;
+      if (ext) {
+        const double dist = vr(vsub(o, hit));
+        if (lex_better(dist, obj0 + k, best, besti)) {
+          best = dist;
+          besti = obj0 + k;
+          bhit = hit;
+          bin = true;
+          thi = (float)(best / r * (1.0 + 1e-6));
+        }
+      } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {
+        push_cover<BS>(ci, cv, ncov, ovf, obj0 + k, 1.0);
+      }
+    }
+  }
+
+  while (ref != BVH_NONE) {
+    // ---- inner nodes: slab-test the four child boxes, descend into the nearest
+    while (ref >= 0 && ref != BVH_NONE) {
+      float key[4];
+      int ch[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        ch[k] = nodes[ref].child[k];
+        const float t0x = __builtin_fmaf(nodes[ref].lo[0][k], ix, -ax);
+        const float t1x = __builtin_fmaf(nodes[ref].hi[0][k], ix, -bx);
+        const float t0y = __builtin_fmaf(nodes[ref].lo[1][k], iy, -ay);
+        const float t1y = __builtin_fmaf(nodes[ref].hi[1][k], iy, -by);
+        const float t0z = __builtin_fmaf(nodes[ref].lo[2][k], iz, -az);
+        const float t1z = __builtin_fmaf(nodes[ref].hi[2][k], iz, -bz);
+        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+        // empty slots hold a box at (3e38, 3e38, 3e38): never wanted by a finite ray
+        key[k] = (tn <= tf && tf >= 0.0f && tn <= thi) ? tn : __builtin_inff();
+      }
+#define RTX_CS(a, b)         \
+  if (key[b] < key[a]) {     \
+    const float tk = key[a]; \
+    key[a] = key[b];         \
+    key[b] = tk;             \
+    const int tc = ch[a];    \
+    ch[a] = ch[b];           \
+    ch[b] = tc;              \
+  }
+      RTX_CS(0, 1) RTX_CS(2, 3) RTX_CS(0, 2) RTX_CS(1, 3) RTX_CS(1, 2)
+#undef RTX_CS
+#pragma unroll
+      for (int k = 3; k >= 1; k--)
+        if (key[k] < __builtin_inff()) stk[(sp++) * BS] = ch[k];
+      if (key[0] < __builtin_inff()) ref = ch[0];
+      else ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
+    }
+    if (ref == BVH_NONE) break;
+    // ---- leaf: pre-test its spheres, exact test for those not ruled out
+    {
+      const int v = ~ref;
+      const int slot0 = (v >> 2) * BVH_LEAF;
+      const int cnt = (v & 3) + 1;
+      float4 c[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) c[u] = leaf4[slot0 + u];
+      uint32_t keep = 0;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const float ocx = c[u].x - ox, ocy = c[u].y - oy, ocz = c[u].z - oz;
+        const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+        const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
+        const bool miss_line = __builtin_fmaf(s, dd, -q * q) > __builtin_fmaf(dd, c[u].w, kline);
+        const bool behind = q < qneg && s > c[u].w + ms2;
+        keep |= (miss_line || behind) ? 0u : (1u << u);
+      }
+      keep &= (1u << cnt) - 1u;
+      while (keep) {
+        const int u = __builtin_ctz(keep);
+        keep &= keep - 1;
+        const Sphere64 sp64 = S.bvh_sph64[slot0 + u];
+        const V3 C = v3(sp64.c[0], sp64.c[1], sp64.c[2]);
+        V3 hit;
+        bool in;
+        if (!sphere_exact(C, sp64.r, o, d, dn, r2, hit, in)) continue;
+        const int obj = S.bvh_obj[slot0 + u];
+        if (ext) {
+          const double dist = vr(vsub(o, hit));      // Ray#distance
+          if (lex_better(dist, obj, best, besti)) {
+            best = dist;
+            besti = obj;
+            bhit = hit;
+            bin = in;
+            thi = (float)(best / r * (1.0 + 1e-6));
+          }
+        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
+          const double cov = penumbra(C, sp64.r, o, d, radius, err);
+          if (cov != 0.0) push_cover<BS>(ci, cv, ncov, ovf, obj, cov);
+        }
+      }
+    }
+    ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
+    if (PP && __popcll(__ballot(ref != BVH_NONE)) < postpone && ref != BVH_NONE) return false;
+  }
+  if (!ext) {
+    total = 1.0;
+    if (ovf) {
+      // more than COVER_K non-zero covers: the ordered linear walk (rare)
+      query<false>(S, cptr(S.sph32), false, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
+    } else {
+      for (int k = 0; k < ncov; k++) total -= cv[k * BS];
+    }
+  }
+  return true;
+}
+
+// ----------------------------------------------------------------- shading
+// WorldObject#get_reflection_by_ray_and_n (world_object.rb:121-125).
+// nn = n.normalize, c = ray.front.cos(-n) (== ray.front.cos(n): |cos| of a
+// negated vector has the same bits), both computed once per hit.
+__device__ __forceinline__ Ray reflection(const Ray& ray, V3 nn, double c, V3 hit, V3 delta, uint32_t& err) {
+  Ray r;
+  r.d = vnorm(vadd(vsc(nn, 2.0 * c * vr(ray.d)), ray.d), err);
+  r.o = vadd(hit, delta);
+  return r;
+}
+
+// WorldObject#get_refraction_by_ray_and_n (world_object.rb:127-137).
+__device__ __forceinline__ bool refraction(const Ray& ray, V3 nn, double c, V3 hit, V3 refl, double rate,
+                                           Ray& out, uint32_t& err) {
+  const double sin_i = sqrt(1.0 - c * c);        // 1 - cos**2
+  const double sin_r = sin_i / rate;
+  if (sin_r >= 1) return false;                  // total internal reflection
+  const double r = rx_asin(sin_r);
+  out.d = vadd(vsc(nn, -rx_cos(r)), vsc(vnorm(vadd(refl, ray.d), err), sin_r));
+  out.o = vsub(hit, vsc(nn, EPS));
+  return true;
+}
+
+__device__ __forceinline__ V3 texcolor(const SceneDev& S, int tex, double hs, double vs, double uo,
+                                       double vo, double uu, double vv, uint32_t& err) {
+  // Texture#color (texture.rb:23-28): trunc, then Ruby's floor-mod.
+  const TexDev t = S.tex[tex];
+  const double qu = (uu + uo) / hs, qv = (vv + vo) / vs;
+  if (!isfinite(qu) || !isfinite(qv)) {
+    seterr(err, ERR_DOMAIN);                     // FloatDomainError in Float#to_i
+    return v3(0.0, 0.0, 0.0);
+  }
+  long iu = (long)fmod(trunc(qu), (double)t.w);
+  long iv = (long)fmod(trunc(qv), (double)t.h);
+  if (iu < 0) iu += t.w;
+  if (iv < 0) iv += t.h;
+  const uint8_t* p = S.texels + t.off + ((size_t)iv * t.w + iu) * 3;
+  return v3(p[0] / 256.0, p[1] / 256.0, p[2] / 256.0);
+}
+
+__device__ __forceinline__ V3 vertical_vector(V3 n, uint32_t& err) {   // world_object.rb:105-120
+  if (vr(n) == 0) {
+    seterr(err, ERR_ZERO_VEC);
+    return v3(1.0, 0.0, 0.0);
+  }
+  if (n.x == 0) {
+    if (n.y == 0) return v3(1.0, 0.0, 0.0);
+    return v3(0.0, -n.z / n.y, 1.0);
+  }
+  return v3(-(n.y + n.z) / n.x, 1.0, 1.0);
+}
+
+// Geometry of the winning hit: position, delta, normal n and the :in flag of
+// intersect_parameters (sphere.rb:60-101, plane.rb:38-67, box.rb:100-105).
+// Re-evaluated with the same operations as in the walk, hence the same bits.
+// Geometry of the winning hit: delta, normal n and the :in flag of
+// intersect_parameters (sphere.rb:60-101, plane.rb:38-67, box.rb:100-105).
+// Spheres and planes: `hit` and `in` are the walk's own evaluation of the
+// winner (kept when it became the nearest; same bits a re-evaluation gives).
+// Boxes re-evaluate to find the face.
+RTX_SHADE_FN void hit_info(const SceneDev& S, int obj, const Ray& ray, V3& hit, V3& delta, V3& n, bool& in) {
+  const Material& m = S.mat[obj];
+  if (m.type == OBJ_SPHERE) {
+    const Sphere64 sp = S.sph64[m.rec];
+    const V3 C = v3p(sp.c);
+    delta = vsc(vsc(vsub(hit, C), EPS), in ? 1.0 : -1.0);
+    n = in ? vsub(hit, C) : vsub(C, hit);
+    return;
+  }
+  in = true;
+  const double* plane;
+  if (m.type == OBJ_PLANE) {
+    plane = S.planes + (size_t)m.rec * PLANE_GEO;
+  } else {
+    int face = 0;
+    box_hit(S.boxes + (size_t)m.rec * BOX_GEO, ray.o, ray.d, hit, face);
+    plane = S.boxes + (size_t)m.rec * BOX_GEO + face * PLANE_GEO;
+  }
+  const V3 F = v3(plane[3], plane[4], plane[5]);
+  const double fd = vdot(F, ray.d);
+  const double nfd = -fd;
+  delta = vsc(vsc(F, EPS), nfd > 0 ? 1.0 : (nfd < 0 ? -1.0 : 0.0));   // (-f.d <=> 0).to_f
+  n = fd > 0 ? vneg(F) : F;
+}
+
+// Per-lane LIFO of pending rays (RayTracer#trace_sync's Array, ray_tracer.rb:21-30).
+// The bottom `slots` entries live in LDS (11 eight-byte words per entry, laid
+// out word-major across the workgroup's lanes so a wave's accesses are
+// conflict-free); deeper entries go to the lane's own contiguous region of a
+// global buffer (12 doubles per entry: one push or pop touches two 64-B lines,
+// where a private-array entry, swizzled across the wave, touched 21).
+constexpr int ITEM_WORDS = 11;
+constexpr int GITEM_DOUBLES = 12;
+template <int MAXS>
+struct Stack {
+  int n;
+  double* lds;     // this lane's word 0 of entry 0; word w of entry e at lds[(e * ITEM_WORDS + w) * bs]
+  double* g;       // this lane's global region: entry e at g[e * GITEM_DOUBLES]
+  int bs;
+  int slots;
+
+  __device__ __forceinline__ void push(const Item& it) {
+    if (n < slots) {
+      double* q = lds + (size_t)n * ITEM_WORDS * bs;
+      q[0] = it.ray.o.x;
+      q[bs] = it.ray.o.y;
+      q[2 * bs] = it.ray.o.z;
+      q[3 * bs] = it.ray.d.x;
+      q[4 * bs] = it.ray.d.y;
+      q[5 * bs] = it.ray.d.z;
+      q[6 * bs] = it.att.x;
+      q[7 * bs] = it.att.y;
+      q[8 * bs] = it.att.z;
+      q[9 * bs] = __builtin_bit_cast(double, it.path);
+      q[10 * bs] = __builtin_bit_cast(double, (int64_t)it.depth);
+    } else {
+      double2* q = reinterpret_cast<double2*>(g + (size_t)(n - slots) * GITEM_DOUBLES);
+      q[0] = make_double2(it.ray.o.x, it.ray.o.y);
+      q[1] = make_double2(it.ray.o.z, it.ray.d.x);
+      q[2] = make_double2(it.ray.d.y, it.ray.d.z);
+      q[3] = make_double2(it.att.x, it.att.y);
+      q[4] = make_double2(it.att.z, __builtin_bit_cast(double, it.path));
+      q[5] = make_double2(__builtin_bit_cast(double, (int64_t)it.depth), 0.0);
+    }
+    n++;
+  }
+  __device__ __forceinline__ void pop(Item& it) {
+    n--;
+    if (n < slots) {
+      const double* q = lds + (size_t)n * ITEM_WORDS * bs;
+      it.ray.o = v3(q[0], q[bs], q[2 * bs]);
+      it.ray.d = v3(q[3 * bs], q[4 * bs], q[5 * bs]);
+      it.att = v3(q[6 * bs], q[7 * bs], q[8 * bs]);
+      it.path = __builtin_bit_cast(uint64_t, q[9 * bs]);
+      it.depth = (int32_t)__builtin_bit_cast(int64_t, q[10 * bs]);
+    } else {
+      const double2* q = reinterpret_cast<const double2*>(g + (size_t)(n - slots) * GITEM_DOUBLES);
+      const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
+      it.ray.o = v3(a.x, a.y, b.x);
+      it.ray.d = v3(b.y, c.x, c.y);
+      it.att = v3(d.x, d.y, e.x);
+      it.path = __builtin_bit_cast(uint64_t, e.y);
+      it.depth = (int32_t)__builtin_bit_cast(int64_t, f.x);
+    }
+  }
+};
+
+__device__ __forceinline__ void add_leaf(V3& sum, V3 c, uint32_t& err) {   // ray_tracer.rb:292-298
+  sum = vadd(sum, c);
+  if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) err |= GT1_PENDING;
+}
+
+// Children are generated in the reference's push order; the most recent live
+// one is held in `pend` (it is what Array#pop returns next) and only older
+// siblings are written to the stack.  A child rt_map would discard on pop
+// (ray_tracer.rb:52) is dropped here: no leaf, no RNG draw, no effect.
+template <int MAXS>
+__device__ __forceinline__ void emit(Stack<MAXS>& st, Item& pend, bool& has, uint32_t& err, const Ray& r,
+                                     V3 att, uint64_t path, int depth) {
+  if (depth <= 0 || vr(att) < 0.0001) return;
+  if (has) {
+    if (st.n < MAXS) st.push(pend);
+    else seterr(err, ERR_DOMAIN);                // cannot happen: stack sized on the host
+  }
+  pend.ray = r;
+  pend.att = att;
+  pend.path = path;
+  pend.depth = depth;
+  has = true;
+}
+
+// The rest of rt_map once every light's lit area is known (ray_tracer.rb:80-158):
+// reflection / refraction children, then path-tracing children (no lit light)
+// or the local-lighting leaf.  Returns true with the next ray in `cur`.
+template <int MAXS>
+RTX_SHADE_FN bool shade_finish(const SceneDev& S, const CameraDev& cam, uint64_t seed, int x, int y,
+                                          int sample, int obj, bool in, V3 hit, V3 delta, V3 n, V3 nn, V3 lc,
+                                          int nl,
+                                          Item& cur, Stack<MAXS>& st, V3& sum, uint32_t& err) {
+  const Material& m = S.mat[obj];
+  Item pend;
+  bool has = false;
+  const uint64_t R = (uint64_t)cam.pt + 3;
+  const double c = vcos(cur.ray.d, n, err);
+  const Ray refl = reflection(cur.ray, nn, c, hit, delta, err);
+  emit<MAXS>(st, pend, has, err, refl, vmul(cur.att, v3p(m.refl_att)), cur.path * R + 1, cur.depth - 1);
+  Ray refr;
+  bool has_refr = false;
+  if (m.type == OBJ_SPHERE)                                  // sphere.rb:92-94: rate inverted leaving
+    has_refr = refraction(cur.ray, nn, c, hit, refl.d, in ? m.rr : 1.0 / m.rr, refr, err);
+  else if (m.has_rr)                                         // plane.rb:57-61: same rate both ways
+    has_refr = refraction(cur.ray, nn, c, hit, refl.d, m.rr, refr, err);
+  if (has_refr)
+    emit<MAXS>(st, pend, has, err, refr, vmul(cur.att, v3p(m.refr_att)), cur.path * R + 2, cur.depth - 1);
+  if (nl == 0) {
+    // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
+    const int pt = cam.pt;
+    const V3 att = vmul(cur.att, vdiv(v3p(m.diffuse), (double)pt));
+    const V3 front = nn;
+    const V3 left = vnorm(vertical_vector(n, err), err);
+    const V3 up = vcross(front, left);
+    Ray r;
+    r.o = vadd(hit, delta);
+    for (int k = 0; k < pt; k++) {
+      const double theta = rand01(seed, x, y, sample, cur.path, 2 * k) * PI / 2.0;
+      const double phi = rand01(seed, x, y, sample, cur.path, 2 * k + 1) * PI * 2.0;
+      double sth, cth, sph, cph;
+      RTX_SINCOS(theta, &sth, &cth);
+      RTX_SINCOS(phi, &sph, &cph);
+      r.d = vadd(vsc(front, sth), vsc(vadd(vsc(left, cph), vsc(up, sph)), cth));
+      emit<MAXS>(st, pend, has, err, r, att, cur.path * R + 3 + (uint64_t)k, cur.depth - 1);
+    }
+  } else {
+    lc = vdiv(lc, (double)nl);
+    V3 color;
+    if (m.type == OBJ_BOX) {
+      color = vadd(vmul(lc, v3p(m.diffuse)), v3p(m.ambient));
+    } else {
+      V3 filter = v3(1.0, 1.0, 1.0);
+      if (m.tex >= 0) {
+        if (m.type == OBJ_SPHERE) {                   // Sphere#get_uv (sphere.rb:111-120)
+          const Sphere64 sp = S.sph64[m.rec];
+          const V3 vec = vsub(hit, v3p(sp.c));
+          const double x0 = vdot(vec, v3p(m.gw_n)) / sp.r;
+          const double y0 = vdot(vec, v3p(m.east_n)) / sp.r;
+          const double z0 = vdot(vec, v3p(m.north_n)) / sp.r;
+          const double mm2 = x0 * x0 + y0 * y0 + z0 * z0 + 2.0 * x0 + 1.0;
+          if (mm2 < 0) seterr(err, ERR_DOMAIN);
+          const double mm = sqrt(mm2);
+          filter = vmul(texcolor(S, m.tex, m.hs, m.vs, m.u_off, m.v_off, (y0 / mm + 1.0) / 2.0,
+                                 (-z0 / mm + 1.0) / 2.0, err), filter);
+        } else {
+          double u, v;
+          plane_uv(S.planes + (size_t)m.rec * PLANE_GEO, hit, u, v);
+          filter = vmul(texcolor(S, m.tex, m.hs, m.vs, 0.0, 0.0, u, v, err), filter);
+        }
+      }
+      color = vadd(vmul(vmul(lc, v3p(m.diffuse)), filter), v3p(m.ambient));
+    }
+    add_leaf(sum, vmul(cur.att, color), err);
+  }
+  if (has) cur = pend;
+  return has;
+}
+
+// Camera#lens_func (camera.rb:129-151).  Everything but the aperture point is
+// independent of the sample: the focal-plane target of pixel (x, y) is
+// computed once per pixel (lens_target), the sample's ray per draw (lens_ray).
+__device__ __forceinline__ V3 lens_target(const CameraDev& c, int x, int y) {
+  const V3 rp = vadd(vadd(v3p(c.retina_center), vsc(v3p(c.left), 2.0 * ((double)x / c.width - 0.5) * c.retina_width)),
+                     vsc(v3p(c.up_n), 2.0 * ((double)y / c.height - 0.5) * c.retina_height));
+  const V3 rd = vsub(v3p(c.pos), rp);                           // Ray(position - retina, retina)
+  const double t = vdot(vsub(v3p(c.pofp), rp), v3p(c.front)) / vdot(v3p(c.front), rd);
+  return vadd(rp, vsc(rd, t));                                  // intersect_plane (:123-127)
+}
+
+__device__ __forceinline__ Ray lens_ray(const CameraDev& c, V3 target, int x, int y, int j, uint64_t seed) {
+  const double theta = rand01(seed, x, y, j, 0, 0);
+  double st, ct;
+  RTX_SINCOS(theta, &st, &ct);
+  const V3 rv = vsc(vadd(vsc(v3p(c.left_n), ct), vsc(v3p(c.up_n), st)), c.aperture_radius);
+  Ray r;
+  r.o = vadd(v3p(c.pos), rv);
+  r.d = vsub(target, r.o);
+  return r;
+}
+
+// World#high_lights (world.rb:83-98) for `ray`: every fired light's leaf goes
+// to `leaf(V3)` in light order.  Returns true if any light fired (the ray then
+// stops, ray_tracer.rb:77).  The `&& lit_area(...)` is always truthy in Ruby and
+// is not evaluated.
+template <typename Leaf>
+__device__ __forceinline__ bool highlight_leaves(const SceneDev& S, const Item& it, Leaf&& leaf, uint32_t& err) {
+  uint32_t fired = 0;
+  int nfired = 0;
+  const RTX_CONST LightDev* lights = cptr(S.light);
+  for (int l = 0; l < S.n_light; l++) {
+    const RTX_CONST LightDev& L = lights[l];
+    const V3 a = vsub(v3(L.pos[0], L.pos[1], L.pos[2]), it.ray.o);
+    const double dot = vdot(it.ray.d, a);
+    const double r1 = vsq(it.ray.d), r2 = vsq(a);
+    if (r1 == 0 || r2 == 0) {
+      seterr(err, ERR_ZERO_VEC);
+      continue;
+    }
+    bool fire;
+    const double g = dot * dot, h = r1 * r2;
+    if (L.hl_mode == 2) {
+      fire = false;
+    } else if (L.hl_mode == 0 && g > L.cos_hi2 * h) {
+      fire = true;                                  // |cos| surely above cos(angle)
+    } else if (L.hl_mode == 0 && g < L.cos_lo2 * h) {
+      fire = false;                                 // |cos| surely below cos(angle)
+    } else {
+      double c = sqrt(g / r1 / r2);                 // Vec3#cos exactly
+      if (c > 1) c = 1;
+      if (c < -1) c = -1;
+      fire = rx_acos(c) < L.hl_angle_rad;
+    }
+    if (fire) {
+      fired |= 1u << l;
+      nfired++;
+    }
+  }
+  if (!nfired) return false;
+  for (int l = 0; l < S.n_light; l++) {
+    if (!(fired >> l & 1)) continue;
+    const RTX_CONST LightDev& L = lights[l];
+    leaf(vdiv(vmul(it.att, vsc(v3(L.color[0], L.color[1], L.color[2]), L.hl_rate)), (double)nfired));
+  }
+  return true;
+}
+
+// The same into a running sum.  REDUCE: leaves go through rt_reduce
+// (trace_sync); path_trace adds them with a plain `ret +=` (ray_tracer.rb:210),
+// no "color greater than 1" check.
+template <bool REDUCE = true>
+__device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3& sum, uint32_t& err) {
+  return highlight_leaves(S, it, [&](V3 c) {
+    if (REDUCE) add_leaf(sum, c, err);
+    else sum = vadd(sum, c);
+  }, err);
+}
+
+// `key` orders the raise sites as the reference meets them: x * height + y for
+// pixels (render_sync runs x in the outer loop, y in the inner one,
+// camera.rb:102-103), the ray index for rtx_trace.
+__device__ __forceinline__ void record_error(ErrState* e, uint32_t code, unsigned long long key) {
+  atomicOr(&e->flags, 1u << code);
+  atomicMin(&e->first[code], key);
+}
+__device__ __forceinline__ unsigned long long px_key(int x, int y, int H) {
+  return (unsigned long long)x * (unsigned long long)H + (unsigned long long)y;
+}
+
+__device__ __forceinline__ int row_to_y(const KParams& p, int row) {
+  if (p.tile_rows == 0) return p.y0 + row;
+  const int k = row / p.tile_rows;
+  return (k * p.nranks + p.rank) * p.tile_rows + (row - k * p.tile_rows);
+}
+
+// Level-0 item k of a bounce-level batch (KParams lv_*): pass 0, the pre
+// samples of the batch's tiles in (tile, pixel in Morton order, sample) order;
+// pass 1, the extra samples of the batch's extra-list entries.
+struct ItemPos {
+  int px, row, sample;
+  bool valid;                      // inside the region (8x8 tiles are padded)
+};
+__device__ __forceinline__ ItemPos decode_item(const KParams& p, int k) {
+  ItemPos ip;
+  if (p.lv_pass == 0) {
+    const int tiles_x = (p.nx + 7) >> 3;
+    const int per = 64 * p.pre;
+    const int slot = k / per, r = k - slot * per;
+    const int tile = p.lv_t0 + slot;
+    const int l = r / p.pre;
+    ip.sample = r - l * p.pre;
+    ip.px = (tile % tiles_x) * 8 + ((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));
+    ip.row = (tile / tiles_x) * 8 + (((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4));
+    ip.valid = ip.px < p.nx && ip.row < p.nrows && row_to_y(p, ip.row) < p.cam->height;
+  } else {
+    const int n_extra = p.max_samples - p.pre;
+    const int e = k / n_extra;
+    const int idx = p.extra_list[p.lv_e0 + e];
+    ip.sample = p.pre + (k - e * n_extra);
+    ip.px = idx % p.nx;
+    ip.row = idx / p.nx;
+    ip.valid = true;
+  }
+  return ip;
+}
+
+// LDS budgets.  Linear walk: 16 B per sphere in 256-thread workgroups, small
+// enough for several workgroups per CU.  Hierarchy: nodes + leaf records in
+// one 512-thread workgroup per CU (2 waves per SIMD, the register-limited
+// occupancy), next to its stacks and cover lists.
+constexpr size_t LDS_SPHERE_BYTES = 32 * 1024;
+constexpr size_t LDS_TOTAL_BYTES = 160 * 1024;
+constexpr size_t LDS_LIN_BLOCK_BYTES = 76 * 1024;   // two 256-thread workgroups per CU
+#ifndef RTX_BS_BVH
+#define RTX_BS_BVH 512
+#endif
+constexpr int BS_LIN = 256, BS_BVH = RTX_BS_BVH;
+#ifndef RTX_WPS
+#define RTX_WPS 2            // waves per SIMD the kernels are compiled for (256 VGPRs)
+#endif
+
+// Fills the LDS layout of `p` for `mode` and returns the dynamic LDS bytes.
+inline size_t lds_layout(KParams& p, int mode, int bs) {
+  const SceneDev& S = p.scene;
+  size_t off = 0;
+  if (mode == SPH_LIN_LDS) off = (size_t)(S.n_sphere + 4) * 16;
+  if (mode == SPH_BVH_LDS) {
+    off = (size_t)S.n_nodes * sizeof(Bvh4Node);
+    p.lds_leaf = (int32_t)off;
+    off += (size_t)S.n_slots * 16;
+  }
+  off = (off + 15) & ~(size_t)15;
+  p.lds_stack = (int32_t)off;
+  p.lds_cov = (int32_t)off;
+  if (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL) {
+    off += (size_t)S.bvh_stack * bs * 4;
+    off = (off + 15) & ~(size_t)15;
+    p.lds_cov = (int32_t)off;
+    off += (size_t)COVER_K * bs * 12;
+  }
+  // the bottom of every lane's ray stack, as many entries as fit the budget
+  off = (off + 15) & ~(size_t)15;
+  p.lds_items = (int32_t)off;
+  const size_t budget = (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL) ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
+  const size_t per = (size_t)ITEM_WORDS * 8 * bs;
+  int slots = budget > off ? (int)((budget - off) / per) : 0;
+  if (slots > p.stk_slots_max) slots = p.stk_slots_max;
+  p.stk_slots = slots;
+  off += (size_t)slots * per;
+  return off;
+}
+
+}  // namespace rtx

@@ -108,6 +108,10 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
 int levels_rec_bytes(int n_light);
 constexpr size_t RAY_BYTES = 96;                // staged ray record of the bounce-level engine
 hipError_t launch_path_trace(KParams p, hipStream_t s);
+// The lanes engine's re-render of the level-0 items listed in lv_redo_list
+// (SRC_LIST; exits at once when the list is empty).
+hipError_t launch_redo(const KParams& q, int mode, int maxs, int n, hipStream_t s);
+int read_level_stamps(unsigned long long* out, int reset);   // diagnostic builds
 int resolve_mode(const SceneDev& S, int mode);
 // LDS bytes a hierarchy workgroup needs (nodes + leaf records + traversal
 // stacks + cover lists) and the budget SPH_BVH_LDS has.

@@ -1,0 +1,735 @@
+// rtx_levels.hip — the bounce-level engine on gfx950:
+// RayTracer#trace_sync (src/ray_tracer.rb:16-46) breadth-first, one launch per
+// ray-tree level, and Camera#render_at's reduction over the stored trees.
+#include "rtx_device.h"
+
+namespace rtx {
+
+// ================================================================= bounce levels
+// The bounce-level engine (option "engine" = 1).  Instead of
+// one lane walking one sample's whole ray tree (the lanes engine above), every
+// ray of tree level d is one work item of the level-d launch: the camera
+// samples at level 0, their live children at level 1, and so on.  A wave's 64
+// lanes therefore run the same step of rt_map (ray_tracer.rb:50-164) on 64
+// rays at once, and no sample's tree can hold a launch open: a launch's
+// longest item is one ray.
+//
+// Order.  trace_sync pops rays LIFO and drains the leaves FIFO afterwards
+// (ray_tracer.rb:31-45): leaves are summed in pre-order of the tree, children
+// visited in reverse push order (refraction after its pt siblings, reflection
+// last).  Each ray writes a tree record {first raise, leaf count, child mask,
+// first child, leaves} at its level; its live children go, contiguous and in
+// slot order, to the next level at an offset found by a wave prefix count
+// (ballot / mbcnt / shfl) plus one atomic per wave.  k_tree_finalize walks each
+// sample's tree in the reference's order and sums the leaves in it: the same
+// additions in the same order as the sequential program, so the same bits.
+//
+// Raises.  rt_map's raises happen while the tree is walked, the "color greater
+// than 1" of rt_reduce only in the drain after it (:39-45): a record keeps the
+// first raise of its ray in rt_map's order (highlights; reflection and
+// refraction; local_lights' lit_area; path tracing / local_lighting), the walk
+// takes the first in tree order, and a >1 partial sum counts only without one.
+//
+// Capacity.  Children beyond the staging buffer or tree records beyond the
+// record arena are not written; their camera sample is listed (lv_redo_list)
+// and re-rendered whole by the lanes engine (SRC_LIST), exact either way.
+constexpr int RAY_DOUBLES = 12;          // staging ray record: o, d, att, path, root item, pad (96 B)
+
+int levels_rec_bytes(int n_light) {
+  const int nl = n_light > 1 ? n_light : 1;
+  return (8 + 24 * nl + 15) & ~15;       // {meta, first child} + one leaf per fired light
+}
+
+__device__ __forceinline__ uint32_t lv_count(const KParams& p, int d) {
+  const uint32_t c = p.lv_ctl->count[d];
+  return d == 0 ? c : (c < p.lv_scap ? c : p.lv_scap);
+}
+
+__device__ __forceinline__ void lv_redo(const KParams& p, int root) {
+  if (atomicCAS(&p.lv_redo_of[root], -1, -2) == -1) {
+    const uint32_t e = atomicAdd(&p.lv_ctl->redo_n, 1u);
+    p.lv_redo_list[e] = root;
+    p.lv_redo_of[root] = (int)e;
+  }
+}
+
+// root: the level-0 item of the ray's tree; (x, y, sample): its RNG key.
+__device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, uint64_t path, int root, int x, int y,
+                                             int sample) {
+  double2* q = reinterpret_cast<double2*>(dst);
+  q[0] = make_double2(r.o.x, r.o.y);
+  q[1] = make_double2(r.o.z, r.d.x);
+  q[2] = make_double2(r.d.y, r.d.z);
+  q[3] = make_double2(att.x, att.y);
+  q[4] = make_double2(att.z, __builtin_bit_cast(double, path));
+  q[5] = make_double2(__builtin_bit_cast(double, (uint64_t)(uint32_t)root | (uint64_t)(uint32_t)sample << 32),
+                      __builtin_bit_cast(double, (uint64_t)(uint32_t)x | (uint64_t)(uint32_t)y << 32));
+}
+
+// Launch `level` (0 .. trace_depth-1) of one batch.  Persistent: every wave
+// claims 64-ray chunks until the level's count is exhausted.
+template <int SPH, int BS>
+__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level) {
+  const SceneDev& S = p.scene;
+  const CameraDev& cam = *p.cam;
+  extern __shared__ float4 lds_sph[];
+  char* lds = reinterpret_cast<char*>(lds_sph);
+  const uint32_t n = lv_count(p, level);
+  if (n == 0) return;                         // uniform: before any barrier
+  if (SPH == SPH_LIN_LDS) {
+    for (int i = threadIdx.x; i < S.n_sphere + 4; i += BS)
+      lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
+    __syncthreads();
+  } else if (SPH == SPH_BVH_LDS) {
+    const int nn = S.n_nodes * (int)(sizeof(Bvh4Node) / 16);
+    for (int i = threadIdx.x; i < nn; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.bvh)[i];
+    float4* leaf = reinterpret_cast<float4*>(lds + p.lds_leaf);
+    for (int i = threadIdx.x; i < S.n_slots; i += BS) leaf[i] = reinterpret_cast<const float4*>(S.bvh_sph32)[i];
+    __syncthreads();
+  }
+  const float* sph_lds = reinterpret_cast<const float*>(lds_sph);
+  const RTX_CONST float* sph_k = cptr(S.sph32);
+  int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
+  int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
+  double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
+
+  uint32_t base = 0;                          // this level's first record in lv_rec
+  for (int e = 0; e < level; e++) base += lv_count(p, e);
+  const double* __restrict__ in = p.lv_stage[level & 1];
+  double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
+  const int depth = cam.depth - level;        // trace_depth of this level's rays
+  const int pt = cam.pt;
+  const uint64_t R = (uint64_t)pt + 3;
+  const int lane = (int)__lane_id();
+
+  // walk dispatch (the same query code as the lanes engine; every lane of a
+  // level launch runs the same query kind at the same time)
+  auto walk = [&](bool ext, V3 o, V3 d, V3 L, double rad, double& best, int& besti, V3& hit, bool& hin,
+                  double& total, uint32_t& err) {
+    if (SPH == SPH_LIN_LDS)
+      query<false>(S, sph_lds, ext, o, d, L, rad, best, besti, hit, hin, total, err, nullptr);
+    else if (SPH == SPH_LIN_SCALAR)
+      query<false>(S, sph_k, ext, o, d, L, rad, best, besti, hit, hin, total, err, nullptr);
+    else {
+      int q_ref = BVH_NONE, q_sp = 0, q_ncov = 0;
+      bool q_ovf = false;
+      if (SPH == SPH_BVH_LDS)
+        query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
+                             stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp,
+                             q_ncov, q_ovf, false, 0);
+      else
+        query_bvh<BS, false>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), stk, cov_i, cov_v, ext, o, d, L,
+                             rad, best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
+    }
+  };
+
+  unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
+#define RTX_LV_STAMP(k)  \
+  if (RTX_STAMPS) {      \
+    t1 = stamp();        \
+    tS[k] += t1 - t0;    \
+    t0 = t1;             \
+  }
+  // Chunk claims: one atomic per 64 rays (RTX_LV_CLAIM_AHEAD issues the next
+  // claim when a chunk starts instead; measured no faster).
+  int next = 0;
+  if (RTX_LV_CLAIM_AHEAD) {
+    if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
+  }
+  while (true) {
+    if (RTX_STAMPS) {
+      t0 = stamp();
+      nchunks++;
+    }
+    int chunk = 0;
+    if (RTX_LV_CLAIM_AHEAD) {
+      chunk = __shfl(next, 0);
+      if ((uint32_t)chunk * 64u >= n) break;
+      if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
+    } else {
+      if (lane == 0) chunk = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
+      chunk = __shfl(chunk, 0);
+      if ((uint32_t)chunk * 64u >= n) break;
+    }
+    const uint32_t i = (uint32_t)chunk * 64u + (uint32_t)lane;
+    bool active = i < n;
+
+    // ---- the ray: a camera sample (level 0) or a staged child
+    Item cur;
+    int root = 0, x = 0, y = 0, sample = 0;
+    bool alive = false;
+    if (active) {
+      if (level == 0) {
+        root = (int)i;
+      } else {
+        const double2* q = reinterpret_cast<const double2*>(in + (size_t)i * RAY_DOUBLES);
+        const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
+        cur.ray.o = v3(a.x, a.y, b.x);
+        cur.ray.d = v3(b.y, c.x, c.y);
+        cur.att = v3(d.x, d.y, e.x);
+        cur.path = __builtin_bit_cast(uint64_t, e.y);
+        const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
+        root = (int)(uint32_t)rs;
+        sample = (int)(rs >> 32);
+        x = (int)(uint32_t)xy;
+        y = (int)(xy >> 32);
+      }
+      if (level == 0) {
+        p.lv_redo_of[i] = -1;                 // no overflow yet (lv_redo)
+        const ItemPos ip = decode_item(p, root);
+        x = p.x0 + ip.px;
+        y = row_to_y(p, ip.row);
+        sample = ip.sample;
+        if (ip.valid) {
+          cur.ray = lens_ray(cam, lens_target(cam, x, y), x, y, sample, p.seed);
+          cur.att = v3(1.0, 1.0, 1.0);
+          cur.path = 1;
+          alive = !(depth <= 0 || vr(cur.att) < 0.0001);   // rt_map's cutoff (ray_tracer.rb:52)
+        } else {
+          active = false;                     // padding of an 8x8 tile: no record
+        }
+      } else {
+        alive = true;                         // children are staged only past the cutoff
+      }
+      if (active && base + i >= p.lv_lcap) { // no room for this ray's record
+        lv_redo(p, root);
+        active = alive = false;
+      }
+    }
+    char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
+    double* leafp = reinterpret_cast<double*>(rec + 8);
+
+    // ---- rt_map: highlights (ray_tracer.rb:60-75), raises in rt_map's order:
+    // errA highlights, errS intersect_parameters (reflection / refraction),
+    // errL local_lights' lit_area, errP path_tracing / local_lighting
+    uint32_t errA = 0, errS = 0, errL = 0, errP = 0;
+    int nleaf = 0;
+    bool fired = false;
+    if (alive)
+      fired = highlight_leaves(S, cur, [&](V3 c) {
+        leafp[3 * nleaf] = c.x;
+        leafp[3 * nleaf + 1] = c.y;
+        leafp[3 * nleaf + 2] = c.z;
+        nleaf++;
+      }, errA);
+
+    RTX_LV_STAMP(0)
+    // ---- World#intersect (world.rb:37-59)
+    const bool ext = alive && !fired;
+    double best = S.max_distance, total = 0.0;
+    int besti = -1;
+    V3 hit = v3(0.0, 0.0, 0.0);
+    bool hin = true;
+    if (ext) walk(true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
+    const bool shade = ext && besti >= 0;
+    RTX_LV_STAMP(1)
+
+    V3 delta = hit, nrm = hit, nn = hit;
+    double c = 0.0;
+    if (shade) {
+      hit_info(S, besti, cur.ray, hit, delta, nrm, hin);
+      nn = vnorm(nrm, errS);                  // n.normalize (world_object.rb:123)
+      c = vcos(cur.ray.d, nrm, errS);         // ray.front.cos(-n): same bits as cos(n)
+    }
+    const V3 qo = vadd(hit, delta);           // the shadow rays' target point (world.rb:76)
+
+    RTX_LV_STAMP(2)
+    // ---- World#local_lights (world.rb:72-80) fused with local_lighting's
+    // light loop (world_object.rb:51-74): one SHADOW walk per light.  (Holding
+    // delta / n / n.normalize across the walks measured faster than
+    // recomputing them after: 6.22 vs 6.40 ms on C2.)
+    V3 lc = v3(0.0, 0.0, 0.0);
+    int nl = 0;
+    for (int li = 0; li < S.n_light; li++) {
+      if (!shade) continue;
+      const LightDev& L = S.light[li];
+      const V3 qL = v3p(L.pos);
+      double tot = 1.0;
+      double b2 = 0.0;
+      int bi2 = -1;
+      V3 h2 = qo;
+      bool in2 = true;
+      walk(false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL);
+      const double area = tot > 0 ? tot : 0.0;
+      if (area > 0) {
+        nl++;
+        const double pw = S.sse_is_two ? area * area : rx_pow(area, S.sse);
+        const V3 lcol = vsc(v3p(L.color), pw / (double)S.n_light);
+        const V3 ll = vnorm(vsub(v3p(L.pos), hit), errP);
+        double ldn = vdot(ll, nn);
+        if (ldn > 1) ldn = 1.0;
+        else if (ldn < 0) ldn = 0.0;
+        lc = vadd(lc, vsc(lcol, ldn));
+      }
+    }
+    RTX_LV_STAMP(3)
+    // ---- which children pass rt_map's cutoff (ray_tracer.rb:52) at depth - 1
+    uint32_t mask = 0;
+    double rate = 0.0;
+    bool may_refract = false;
+    const Material* m = shade ? &S.mat[besti] : S.mat;
+    if (shade) {
+      const int cd = depth - 1;
+      if (cd > 0 && !(vr(vmul(cur.att, v3p(m->refl_att))) < 0.0001)) mask |= 1u;
+      if (m->type == OBJ_SPHERE) {            // sphere.rb:92-94: rate inverted leaving
+        may_refract = true;
+        rate = hin ? m->rr : 1.0 / m->rr;
+      } else if (m->has_rr) {                 // plane.rb:57-61: the same rate both ways
+        may_refract = true;
+        rate = m->rr;
+      }
+      if (may_refract && !(sqrt(1.0 - c * c) / rate >= 1) && cd > 0 &&
+          !(vr(vmul(cur.att, v3p(m->refr_att))) < 0.0001))
+        mask |= 2u;                           // refraction exists (no TIR) and is alive
+      if (nl == 0 && cd > 0 && !(vr(vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt))) < 0.0001))
+        mask |= ((1u << pt) - 1u) << 2;       // every path-tracing child (same attenuation)
+    }
+
+    // ---- room in the next level: wave prefix count of the live children + one atomic
+    const int cnt = __popc(mask);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(incl, off);
+      if (lane >= off) incl += t;
+    }
+    const int wtotal = __shfl(incl, 63);
+    uint32_t wbase = 0;
+    if (wtotal > 0) {
+      if (lane == 0) wbase = atomicAdd(&p.lv_ctl->count[level + 1], (uint32_t)wtotal);
+      wbase = __shfl(wbase, 0);
+    }
+    const uint32_t child0 = wbase + (uint32_t)(incl - cnt);
+    RTX_LV_STAMP(4)
+
+    // ---- children in the reference's push order (ray_tracer.rb:84-143), then the leaf
+    if (shade) {
+      uint32_t slot = child0;
+      auto put = [&](const Ray& r, V3 att, uint64_t path) {
+        if (slot < p.lv_scap) lv_store_ray(outs + (size_t)slot * RAY_DOUBLES, r, att, path, root, x, y, sample);
+        else {
+          lv_redo(p, root);
+          atomicAdd(&p.lv_ctl->dropped, 1u);
+        }
+        slot++;
+      };
+      const Ray refl = reflection(cur.ray, nn, c, hit, delta, errS);
+      if (mask & 1u) put(refl, vmul(cur.att, v3p(m->refl_att)), cur.path * R + 1);
+      if (may_refract) {
+        Ray refr;
+        if (refraction(cur.ray, nn, c, hit, refl.d, rate, refr, errS) && (mask & 2u))
+          put(refr, vmul(cur.att, v3p(m->refr_att)), cur.path * R + 2);
+      }
+      if (nl == 0) {
+        // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
+        const V3 att = vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt));
+        const V3 left = vnorm(vertical_vector(nrm, errP), errP);
+        const V3 up = vcross(nn, left);
+        Ray r;
+        r.o = vadd(hit, delta);
+        for (int k = 0; k < pt; k++) {
+          const double theta = rand01(p.seed, x, y, sample, cur.path, 2 * k) * PI / 2.0;
+          const double phi = rand01(p.seed, x, y, sample, cur.path, 2 * k + 1) * PI * 2.0;
+          double sth, cth, sph, cph;
+          RTX_SINCOS(theta, &sth, &cth);
+          RTX_SINCOS(phi, &sph, &cph);
+          r.d = vadd(vsc(nn, sth), vsc(vadd(vsc(left, cph), vsc(up, sph)), cth));
+          if (mask >> (2 + k) & 1u) put(r, att, cur.path * R + 3 + (uint64_t)k);
+        }
+      } else {
+        // WorldObject#local_lighting's colour (world_object.rb:51-74), texture filter
+        lc = vdiv(lc, (double)nl);
+        V3 color;
+        if (m->type == OBJ_BOX) {
+          color = vadd(vmul(lc, v3p(m->diffuse)), v3p(m->ambient));
+        } else {
+          V3 filter = v3(1.0, 1.0, 1.0);
+          if (m->tex >= 0) {
+            if (m->type == OBJ_SPHERE) {             // Sphere#get_uv (sphere.rb:111-120)
+              const Sphere64 sp = S.sph64[m->rec];
+              const V3 vec = vsub(hit, v3p(sp.c));
+              const double x0 = vdot(vec, v3p(m->gw_n)) / sp.r;
+              const double y0 = vdot(vec, v3p(m->east_n)) / sp.r;
+              const double z0 = vdot(vec, v3p(m->north_n)) / sp.r;
+              const double mm2 = x0 * x0 + y0 * y0 + z0 * z0 + 2.0 * x0 + 1.0;
+              if (mm2 < 0) seterr(errP, ERR_DOMAIN);
+              const double mm = sqrt(mm2);
+              filter = vmul(texcolor(S, m->tex, m->hs, m->vs, m->u_off, m->v_off, (y0 / mm + 1.0) / 2.0,
+                                     (-z0 / mm + 1.0) / 2.0, errP), filter);
+            } else {
+              double u, v;
+              plane_uv(S.planes + (size_t)m->rec * PLANE_GEO, hit, u, v);
+              filter = vmul(texcolor(S, m->tex, m->hs, m->vs, 0.0, 0.0, u, v, errP), filter);
+            }
+          }
+          color = vadd(vmul(vmul(lc, v3p(m->diffuse)), filter), v3p(m->ambient));
+        }
+        const V3 leaf = vmul(cur.att, color);
+        leafp[0] = leaf.x;
+        leafp[1] = leaf.y;
+        leafp[2] = leaf.z;
+        nleaf = 1;
+      }
+    }
+    if (active) {
+      uint32_t err = errA;
+      if (!err) err = errS;
+      if (!err) err = errL;
+      if (!err) err = errP;
+      uint2* hdr = reinterpret_cast<uint2*>(rec);
+      *hdr = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8) | (mask << 16), child0);
+    }
+    RTX_LV_STAMP(5)
+  }
+#undef RTX_LV_STAMP
+  if (RTX_STAMPS && lane == 0) {
+    for (int k = 0; k < 6; k++) atomicAdd(&rtx_stamps[k], tS[k]);
+    atomicAdd(&rtx_stamps[6], nchunks);
+    atomicAdd(&rtx_stamps[7], 1ull);
+  }
+}
+
+// Sum of one camera sample's tree (level-0 item `root`) in trace_sync's
+// order: pre-order, children in reverse slot order; `base` = first record of
+// every level.  Returns the first raise (rt_map's first, else rt_reduce's).
+// The walk keeps one pending child range per level below the root in
+// lo[k * st] / hi[k * st], k < sd (LDS, word-major over the block's threads,
+// or a private array with st = 1).
+__device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base, int root, int nlev,
+                                          uint32_t* lo, uint32_t* hi, int st, int sd, uint32_t& err_out) {
+  int sp = 0;
+  V3 sum = v3(0.0, 0.0, 0.0);
+  uint32_t err = 0, pf = 0;
+  bool gt1 = false;
+  int lev = 0;
+  uint32_t q = (uint32_t)root;
+  while (true) {
+    const char* rec = p.lv_rec + (size_t)(base[lev] + q) * p.lv_rec_bytes;
+    const uint2 hdr = *reinterpret_cast<const uint2*>(rec);
+    const double* lf = reinterpret_cast<const double*>(rec + 8);
+    const double2 l01 = *reinterpret_cast<const double2*>(lf);   // the first leaf, with the header's sector
+    const double l2 = lf[2];
+    if (!err) err = hdr.x & 0xffu;
+    const int nleaf = (int)(hdr.x >> 8 & 0xffu);
+    if (nleaf > 0) {                           // rt_reduce (ray_tracer.rb:292-298), in emission order
+      sum = vadd(sum, v3(l01.x, l01.y, l2));
+      if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) gt1 = true;
+      for (int k = 1; k < nleaf; k++) {
+        sum = vadd(sum, v3(lf[3 * k], lf[3 * k + 1], lf[3 * k + 2]));
+        if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) gt1 = true;
+      }
+    }
+    const uint32_t nch = (uint32_t)__popc(hdr.x >> 16);
+    if (nch && lev + 1 < nlev && sp < sd) {
+      lo[sp * st] = hdr.y;
+      hi[sp * st] = hdr.y + nch;
+      sp++;
+      // the children's records (contiguous, slot order) are fetched now, all
+      // at once: the walk's dependent chain becomes the tree's depth, not
+      // its size (the loads' values are consumed only at the end)
+      const char* c0 = p.lv_rec + (size_t)(base[lev + 1] + hdr.y) * p.lv_rec_bytes;
+      pf += *reinterpret_cast<const uint32_t*>(c0) +
+            *reinterpret_cast<const uint32_t*>(c0 + (size_t)(nch - 1) * p.lv_rec_bytes);
+    }
+    // next: the last unvisited child of the deepest pending range (LIFO pop)
+    while (sp > 0 && hi[(sp - 1) * st] == lo[(sp - 1) * st]) sp--;
+    if (sp == 0) break;
+    q = --hi[(sp - 1) * st];
+    lev = sp;
+  }
+  asm volatile("" : : "v"(pf));               // the prefetches' values, consumed
+  err_out = err ? err : (gt1 ? (uint32_t)ERR_COLOR_GT1 : 0u);
+  return sum;
+}
+
+// Block 0 also adds the batch's level statistics to lv_acc (rtx_level_stats):
+// every level launch of the batch has ended.
+__device__ __forceinline__ void lv_bases(const KParams& p, int nlev, uint32_t* base) {
+  if (threadIdx.x == 0) {
+    uint32_t b = 0;
+    for (int d = 0; d <= nlev && d <= LV_MAXL; d++) {
+      base[d] = b;
+      b += lv_count(p, d);
+    }
+  }
+  if (blockIdx.x == 0 && p.lv_acc) {
+    const int t = (int)threadIdx.x;
+    if (t == 0) p.lv_acc[0] += p.lv_ctl->redo_n;
+    if (t == 1) p.lv_acc[1] += p.lv_ctl->dropped;
+    if (t < LV_MAXL + 1) p.lv_acc[2 + t] += p.lv_ctl->count[t];
+  }
+  __syncthreads();
+}
+
+// One camera sample's colour and first raise: its tree, or the lanes engine's
+// record when the sample overflowed the level buffers.
+__device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, int item, int nlev, uint32_t* lo,
+                                        uint32_t* hi, int st, int sd, uint32_t& e) {
+  const int r = p.lv_redo_of[item];
+  if (r >= 0) {
+    const double* q = p.lv_redo_smp + (size_t)r * 4;
+    e = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
+    return v3(q[0], q[1], q[2]);
+  }
+  return lv_tree_sum(p, base, item, nlev, lo, hi, st, sd, e);
+}
+
+// Camera#render_at's reduction (camera.rb:70-99) of pass 0: one 256-thread
+// block per 8x8 tile of the batch.  The block's threads sum the tile's
+// 64 x pre sample trees (item order (pixel, sample): a wave's trees are
+// neighbours), park colour and raise in LDS, then 64 threads do the pixels:
+// mean in sample order, the variance test, then the pixel or (max_sample_times
+// > pre) an extra-list entry with the pre mean parked in the output.
+// Dynamic LDS: SD * 2 words of walk stack per thread, then 64 * pre samples.
+template <int SD>
+__global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
+  extern __shared__ uint32_t lds_fin[];
+  lv_bases(p, nlev, base);
+  const int pre = p.pre;
+  const int slot = blockIdx.x;                 // tile of the batch
+  uint32_t* lo = lds_fin + threadIdx.x;
+  uint32_t* hi = lo + SD * 256;
+  double* scol = reinterpret_cast<double*>(lds_fin + 2 * SD * 256);   // 64 * pre * 3
+  uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
+  uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];  // deep trees: private stack
+  const int n_items = 64 * pre;
+  const int item0 = slot * n_items;
+  for (int it = (int)threadIdx.x; it < n_items; it += 256) {
+    const ItemPos ip = decode_item(p, item0 + it);
+    if (!ip.valid) continue;
+    uint32_t e = 0;
+    const V3 c = SD > 16 ? lv_sample(p, base, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
+                         : lv_sample(p, base, item0 + it, nlev, lo, hi, 256, SD, e);
+    scol[3 * it] = c.x;
+    scol[3 * it + 1] = c.y;
+    scol[3 * it + 2] = c.z;
+    serr[it] = e;
+  }
+  __syncthreads();
+  const int l = (int)threadIdx.x;
+  if (l >= 64) return;
+  const int tiles_x = (p.nx + 7) >> 3;
+  const int tile = p.lv_t0 + slot;
+  const int px_ = (tile % tiles_x) * 8 + ((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));
+  const int row = (tile / tiles_x) * 8 + (((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4));
+  if (px_ >= p.nx || row >= p.nrows) return;
+  const int y = row_to_y(p, row);
+  const CameraDev& cam = *p.cam;
+  if (y >= cam.height) return;
+  const int x = p.x0 + px_;
+  const double* sc = scol + 3 * l * pre;
+  uint32_t err = 0;
+  V3 avg = v3(0.0, 0.0, 0.0);
+  for (int j = 0; j < pre; j++) {
+    avg = vadd(avg, v3(sc[3 * j], sc[3 * j + 1], sc[3 * j + 2]));
+    if (!err) err = serr[l * pre + j];
+  }
+  avg = vdiv(avg, (double)pre);
+  double variance = 0.0;                       // camera.rb:80-85
+  for (int j = 0; j < pre; j++) {
+    const V3 dd = vsub(v3(sc[3 * j], sc[3 * j + 1], sc[3 * j + 2]), avg);
+    double mx = dd.x;
+    if (dd.y > mx) mx = dd.y;
+    if (dd.z > mx) mx = dd.z;
+    variance += mx * mx;                       // .max ** 2
+  }
+  variance /= (double)pre;
+  double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
+  if (variance >= cam.variant_threshold) {
+    if (p.max_samples > pre) {                 // extra samples: pass 1 finishes this pixel
+      p.extra_list[atomicAdd(p.extra_count, 1)] = row * p.nx + px_;
+      o[0] = avg.x;
+      o[1] = avg.y;
+      o[2] = avg.z;
+      if (err) record_error(p.err, err, px_key(x, y, cam.height));
+      return;
+    }
+    avg = vdiv(vadd(vsc(avg, (double)pre), v3(0.0, 0.0, 0.0)), (double)p.max_samples);
+  }
+  o[0] = avg.x;
+  o[1] = avg.y;
+  o[2] = avg.z;
+  if (err) record_error(p.err, err, px_key(x, y, cam.height));
+}
+
+// Pass 1: one thread per extra-list entry of the batch: (pre mean * pre +
+// the extra samples in order) / max_sample_times.
+template <int SD>
+__global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
+  extern __shared__ uint32_t lds_fin[];
+  lv_bases(p, nlev, base);
+  uint32_t* lo = lds_fin + threadIdx.x;
+  uint32_t* hi = lo + SD * 256;
+  uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];
+  const int t = blockIdx.x * 256 + (int)threadIdx.x;
+  if (t >= p.lv_entries || p.lv_e0 + t >= *p.extra_count) return;
+  const int idx = p.extra_list[p.lv_e0 + t];
+  const int px_ = idx % p.nx, row = idx / p.nx;
+  const int y = row_to_y(p, row);
+  const CameraDev& cam = *p.cam;
+  if (y >= cam.height) return;
+  const int x = p.x0 + px_;
+  const int pre = p.pre, n_extra = p.max_samples - pre;
+  double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
+  const V3 avg = v3(o[0], o[1], o[2]);         // the pre mean parked by pass 0
+  V3 cv = v3(0.0, 0.0, 0.0);
+  uint32_t err = 0;
+  for (int j = 0; j < n_extra; j++) {
+    uint32_t e = 0;
+    const int item = t * n_extra + j;
+    cv = vadd(cv, SD > 16 ? lv_sample(p, base, item, nlev, lo_p, hi_p, 1, LV_MAXL, e)
+                          : lv_sample(p, base, item, nlev, lo, hi, 256, SD, e));
+    if (!err) err = e;
+  }
+  const V3 r = vdiv(vadd(vsc(avg, (double)pre), cv), (double)p.max_samples);
+  o[0] = r.x;
+  o[1] = r.y;
+  o[2] = r.z;
+  if (err) record_error(p.err, err, px_key(x, y, cam.height));
+}
+
+// Per batch: the control block, count[0] = the batch's level-0 items (pass 1:
+// from the device-side extra count), the lanes engine's work counter (the
+// re-render launch); the call's first batch also the extra-list count and the
+// level statistics.  (Every level-0 lane sets its item's redo slot to -1.)
+__global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int first) {
+  const int t = blockIdx.x * 256 + (int)threadIdx.x;
+  if (t == 0) *p.work = 0;
+  if (first) {
+    if (t == 0) *p.extra_count = 0;
+    if (p.lv_acc && t < LV_MAXL + 3) p.lv_acc[t] = 0;
+  }
+  if (t < 2 * (LV_MAXL + 1) + 2) {
+    uint32_t v = 0;
+    if (t == 0) {
+      if (p.lv_pass == 0) {
+        v = (uint32_t)n0_max;
+      } else {
+        const int left = *p.extra_count - p.lv_e0;
+        const int ent = left < 0 ? 0 : (left < p.lv_entries ? left : p.lv_entries);
+        v = (uint32_t)(ent * (p.max_samples - p.pre));
+      }
+    }
+    reinterpret_cast<uint32_t*>(p.lv_ctl)[t] = v;
+  }
+}
+
+// Diagnostic builds: this unit's stamps (k_level), added by rtxdbg_read_stamps.
+int read_level_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtx_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtx_stamps), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+
+// ----------------------------------------------------------------- bounce-level launchers
+template <int SPH>
+static hipError_t launch_level(const KParams& p, int level, long cap_items, hipStream_t s, KernelEvents* kev) {
+  constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
+  KParams q = p;
+  q.stk_slots_max = 0;                         // no ray stack in this engine
+  const size_t lds = lds_layout(q, SPH, BS);
+  auto kern = k_level<SPH, BS>;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  int dev = 0, cus = 0, per_cu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BS, lds);
+  if (e != hipSuccess) return e;
+  if (per_cu < 1) per_cu = 1;
+  long blocks = std::min<long>((cap_items + BS - 1) / BS, (long)cus * per_cu);
+  if (blocks < 1) blocks = 1;
+  const bool ev = kev && kev->n < kev->max;
+  if (ev) (void)hipEventRecord(kev->ev[2 * kev->n], s);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BS), lds, s, q, level);
+  e = hipGetLastError();
+  if (ev) {
+    (void)hipEventRecord(kev->ev[2 * kev->n + 1], s);
+    kev->n++;
+  }
+  return e;
+}
+
+static hipError_t launch_level_mode(const KParams& p, int mode, int level, long cap, hipStream_t s,
+                                    KernelEvents* kev) {
+  switch (mode) {
+    case SPH_LIN_LDS: return launch_level<SPH_LIN_LDS>(p, level, cap, s, kev);
+    case SPH_LIN_SCALAR: return launch_level<SPH_LIN_SCALAR>(p, level, cap, s, kev);
+    case SPH_BVH_LDS: return launch_level<SPH_BVH_LDS>(p, level, cap, s, kev);
+    case SPH_BVH_GLOBAL: return launch_level<SPH_BVH_GLOBAL>(p, level, cap, s, kev);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int SD>
+static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStream_t s) {
+  const size_t stack = SD > 16 ? 0 : (size_t)SD * 2 * 256 * 4;
+  if (q.lv_pass == 0) {                        // n = tiles of the batch
+    const size_t lds = stack + (size_t)64 * q.pre * 28;
+    hipLaunchKernelGGL(k_tree_finalize<SD>, dim3((unsigned)n), dim3(256), lds, s, q, nlev);
+  } else {                                     // n = extra-list entries of the batch
+    hipLaunchKernelGGL(k_tree_finalize_extra<SD>, dim3((unsigned)((n + 255) / 256)), dim3(256), stack, s, q, nlev);
+  }
+  return hipGetLastError();
+}
+
+static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t s) {
+  if (nlev <= 8) return launch_finalize_sd<8>(q, nlev, n, s);
+  if (nlev <= 16) return launch_finalize_sd<16>(q, nlev, n, s);
+  return launch_finalize_sd<64>(q, nlev, n, s);
+}
+
+// One batch: reset, the levels, the lanes-engine re-render of overflowed
+// samples (exits at once when there are none), the tree reduction.
+static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_max, int fin_threads, hipStream_t s,
+                              KernelEvents* kev, bool first) {
+  hipLaunchKernelGGL(k_level_begin, dim3(1), dim3(256), 0, s, q, n0_max, first ? 1 : 0);
+  hipError_t e = hipGetLastError();
+  for (int d = 0; d < nlev && e == hipSuccess; d++)
+    e = launch_level_mode(q, mode, d, d == 0 ? (long)n0_max : (long)q.lv_scap, s, kev);
+  if (e == hipSuccess) e = launch_redo(q, mode, maxs, n0_max, s);
+  if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
+
+  return e;
+}
+
+hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tiles, hipStream_t s,
+                         KernelEvents* kev) {
+  const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
+  if (tiles == 0) return hipSuccess;
+  mode = resolve_mode(p.scene, mode);
+  batch_tiles = std::max(1, std::min(batch_tiles, tiles));
+  const int per_tile = 64 * p.pre;
+  p.tile_order = nullptr;
+  hipError_t e = hipSuccess;                   // (the first batch's k_level_begin zeroes the extra count)
+  for (int t0 = 0; t0 < tiles && e == hipSuccess; t0 += batch_tiles) {
+    KParams q = p;
+    q.lv_pass = 0;
+    q.lv_t0 = t0;
+    q.lv_tiles = std::min(batch_tiles, tiles - t0);
+    q.lv_e0 = q.lv_entries = 0;
+    e = level_batch(q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles, s, kev, t0 == 0);
+  }
+  if (e != hipSuccess || p.max_samples <= p.pre) return e;
+  // extra samples of the pixels the variance test listed (count on the device)
+  const int n_extra = p.max_samples - p.pre;
+  const int entries = std::max(1, batch_tiles * per_tile / n_extra);
+  const int npx = p.nx * p.nrows;
+  for (int e0 = 0; e0 < npx && e == hipSuccess; e0 += entries) {
+    KParams q = p;
+    q.lv_pass = 1;
+    q.lv_e0 = e0;
+    q.lv_entries = std::min(entries, npx - e0);
+    q.lv_t0 = q.lv_tiles = 0;
+    e = level_batch(q, mode, maxs, nlev, q.lv_entries * n_extra, q.lv_entries, s, kev, false);
+  }
+  return e;
+}
+
+}  // namespace rtx
