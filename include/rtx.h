@@ -271,7 +271,10 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          per tree level, one ray per lane; same bits), "lv_batch" (bounce levels: camera samples per batch,
          2^23), "lv_stage_pct" / "lv_rec_pct" (bounce-level buffer capacities in % of a batch's samples,
          300 / 1600, and at least "lv_floor" staging / 4 x "lv_floor" tree records, 2^20; samples that
-         overflow them are re-rendered by the lanes engine, same bits). */
+         overflow them are re-rendered by the lanes engine, same bits), "lv_split" (bounce levels: 0 one fused
+         launch per level, 1 three launches per level over dense queues: trace, shadow, shade; same bits; used up
+         to 16 lights), "lv_static" (bounce levels: % of a level launch's 64-ray chunks scheduled statically, the
+         rest claimed from sharded counters; -1 [default] = 100 up to 512 spheres, else 50; same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

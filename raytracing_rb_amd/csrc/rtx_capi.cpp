@@ -75,6 +75,8 @@ struct rtx_context {
   int64_t opt_lv_stage_pct = 300;    // bounce levels: ray records per staging buffer, % of the batch items
   int64_t opt_lv_rec_pct = 1600;      // bounce levels: tree records of a batch (all levels), % of the batch items
   int64_t opt_lv_floor = 1 << 20;    // bounce levels: at least this many staging and 4x this many tree records
+  int64_t opt_lv_split = 0;          // bounce levels: 1 = three phase launches per level (trace / shadow / shade)
+  int64_t opt_lv_static = -1;        // bounce levels: % of a launch's chunks scheduled statically (-1 auto)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
@@ -387,7 +389,8 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"bvh_sah", c->opt_bvh_sah},     {"bvh_min", c->opt_bvh_min},         {"postpone", c->opt_postpone},
       {"lds_stack", c->opt_lds_stack}, {"tile_order", c->opt_tile_order},   {"sphere_src", c->opt_sphere_src},
       {"kernel_events", c->opt_kernel_events}, {"lv_batch", c->opt_lv_batch},
-      {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor}};
+      {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor},
+      {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -449,6 +452,16 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_floor")) {          // bounce levels: minimum buffer records (small frames, deep trees)
     if (value < 0 || value > (1 << 26)) return fail(c, RTX_EINVAL, "lv_floor must be in [0, 2^26]");
     c->opt_lv_floor = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_split")) {          // bounce levels: 0 one fused launch per level, 1 trace / shadow / shade
+    if (value < 0 || value > 1) return fail(c, RTX_EINVAL, "lv_split must be 0 or 1");
+    c->opt_lv_split = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_static")) {         // bounce levels: % of chunks scheduled statically, -1 auto
+    if (value < -1 || value > 100) return fail(c, RTX_EINVAL, "lv_static must be in [-1, 100]");
+    c->opt_lv_static = value;
     return RTX_OK;
   }
   if (!strcmp(key, "kernel_events")) {     // 1: HIP events around the ray-tree launches (rtx_kernel_time)
@@ -804,15 +817,26 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // level-0 items of one batch: pass 0 (tiles) or pass 1 (>= one pixel's extra samples)
   const size_t n0 = std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, p.max_samples - p.pre));
   const size_t fl = (size_t)c->opt_lv_floor;
-  const size_t scap = std::max<size_t>(std::max<size_t>(64, fl), n0 * (size_t)c->opt_lv_stage_pct / 100);
+  const size_t want = std::max<size_t>(std::max<size_t>(64, fl), n0 * (size_t)c->opt_lv_stage_pct / 100);
   const size_t lcap = std::max<size_t>(std::max(n0, 4 * fl), n0 * (size_t)c->opt_lv_rec_pct / 100);
+  // queues of levels >= 1: LV_SLICES slices of 2^k slots (k rounded up)
+  int slog2 = 0;
+  while (((size_t)LV_SLICES << slog2) < want) slog2++;
+  const size_t scap = (size_t)LV_SLICES << slog2;
   if (scap > UINT32_MAX / 2 || lcap > UINT32_MAX / 2)
     return fail(c, RTX_EINVAL, "bounce-level buffers exceed 2^31 records: lower lv_batch");
   const int rec_bytes = levels_rec_bytes(c->scene.n_light);
   const size_t sz_ctl = al256(sizeof(LevelCtl)), sz_redo = al256(n0 * 4), sz_smp = al256(n0 * 32),
                sz_stage = al256(scap * RAY_BYTES), sz_rec = al256(lcap * (size_t)rec_bytes),
                sz_extra = al256((npx + 64) * 4);
-  const size_t total = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_extra;
+  // split phases: the hit queue of a level (at most its rays) and its shadow results
+  const bool split = c->opt_lv_split != 0 && c->scene.n_light <= LV_SPLIT_MAX_LIGHTS;
+  int hlog2 = 0;
+  while (((size_t)LV_SLICES << hlog2) < std::max(n0, scap)) hlog2++;
+  const size_t hcap = (size_t)LV_SLICES << hlog2;
+  const size_t sz_hit = split ? al256(hcap * LV_HIT_BYTES) : 0,
+               sz_area = split ? al256(hcap * (size_t)std::max(1, c->scene.n_light) * 16) : 0;
+  const size_t total = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_extra + sz_hit + sz_area;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
   HIPCHK(c, hipMallocAsync((void**)&buf, total, stream));
@@ -824,9 +848,19 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_stage[0] = (double*)q;               q += sz_stage;
   p.lv_stage[1] = (double*)q;               q += sz_stage;
   p.lv_rec = q;                             q += sz_rec;
+  p.lv_hit = split ? (double*)q : nullptr;  q += sz_hit;
+  p.lv_area = split ? (double*)q : nullptr; q += sz_area;
+  p.lv_split = split ? 1 : 0;
+  // Static chunks cost no atomics; dynamic claims balance rays of very
+  // different cost.  Auto: all static while the sphere records fit one walk
+  // workgroup's LDS with room to spare (C2: 5.35 vs 5.9 ms at 50 %), half
+  // static for large hierarchies (C4: 437 vs 518 ms all static).
+  p.lv_static_pct = c->opt_lv_static >= 0 ? (int32_t)c->opt_lv_static : (c->scene.n_sphere <= 512 ? 100 : 50);
   p.extra_count = (int32_t*)q;
   p.extra_list = p.extra_count + 64;
   p.lv_scap = (uint32_t)scap;
+  p.lv_slice_log2 = slog2;
+  p.lv_hslice_log2 = hlog2;
   p.lv_lcap = (uint32_t)lcap;
   p.lv_rec_bytes = rec_bytes;
   p.lv_acc = c->d_lvstats;

@@ -82,9 +82,6 @@ enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2, SRC_LIST = 3 };
 #ifndef RTX_LVL_WPS
 #define RTX_LVL_WPS 2        // waves per SIMD k_level is compiled for
 #endif
-#ifndef RTX_LV_CLAIM_AHEAD
-#define RTX_LV_CLAIM_AHEAD 0 // k_level claims its next 64-ray chunk while working on the current one (C2 6.26 vs 6.22 ms: off)
-#endif
 static __device__ unsigned long long rtx_stamps[16];   // one per translation unit (no -fgpu-rdc)
 __device__ __forceinline__ unsigned long long wall() {   // 100 MHz constant clock, same on every XCD
 #if RTX_STAMPS

@@ -16,14 +16,21 @@ struct ErrState {
   unsigned long long first[5];     // per ERR_ code (rtx_vec3.h): min key (pixels: x*H + y, render_sync order; rays: index)
 };
 
-// Bounce-level engine: one launch per tree level; the device
-// counts of every level and the work claims of each launch.
+// Bounce-level engine: one launch per tree level (or three,
+// option lv_split).  The ray queue of every level >= 1 (and the hit queue of
+// the split phases) is cut into LV_SLICES slices of 2^k slots, each with its
+// own allocation counter on its own 128-B line (no contended device atomics).
 constexpr int LV_MAXL = 64;                     // levels (= trace_depth) the engine supports
+constexpr int LV_SLICES = 64;                   // slices per queue (one per lane of a consumer wave)
+constexpr int LV_CLAIMS = 16;                   // sharded chunk-claim counters per launch
 struct LevelCtl {
-  uint32_t count[LV_MAXL + 1];                  // rays of level d (count[0]: level-0 items of the batch)
-  uint32_t claim[LV_MAXL + 1];                  // 64-ray chunks claimed by the level-d launch
+  uint32_t count0;                              // level-0 items of the batch
   uint32_t redo_n;                              // level-0 items handed to the lanes engine (capacity overflow)
   uint32_t dropped;                             // child rays that found no room (diagnostic)
+  uint32_t pad[29];
+  uint32_t sc[LV_MAXL + 1][LV_SLICES * 32];     // rays allocated in slice s of level d: sc[d][32 s]
+  uint32_t sh[LV_MAXL + 1][LV_SLICES * 32];     // split phases: hits of level d in slice s
+  uint32_t claim[3][LV_MAXL + 1][LV_CLAIMS * 32]; // chunk claims: [launch kind: fused/trace, shadow, shade][level][j * 32]
 };
 
 struct KParams {
@@ -63,7 +70,9 @@ struct KParams {
   // entries [lv_e0, lv_e0 + lv_entries)); level-0 item k of the batch is
   // decode_item(k); trees are stored per level in lv_rec (lv_rec_bytes each).
   int32_t lv_pass, lv_t0, lv_tiles, lv_e0, lv_entries;
-  uint32_t lv_scap;                // ray records per staging buffer (levels >= 1)
+  uint32_t lv_scap;                // ray records per staging buffer (levels >= 1): LV_SLICES << lv_slice_log2
+  int32_t lv_slice_log2;           // slots per slice of a level's ray queue (log2)
+  int32_t lv_hslice_log2;          // split phases: slots per slice of a level's hit queue (log2)
   uint32_t lv_lcap;                // tree records in lv_rec
   int32_t lv_rec_bytes;
   LevelCtl* lv_ctl;
@@ -73,6 +82,10 @@ struct KParams {
   int32_t* lv_redo_list;           // level-0 items re-rendered by the lanes engine (SRC_LIST)
   double* lv_redo_smp;             // their sample records {r, g, b, first raise}
   unsigned long long* lv_acc;      // per call: {redo_n, dropped, count[0..LV_MAXL]} summed over batches (or null)
+  int32_t lv_split;                // 1: three phase launches per level (k_lv_trace / k_lv_shadow / k_lv_shade)
+  int32_t lv_static_pct;           // % of a level launch's chunks scheduled statically (the rest: sharded claims)
+  double* lv_hit;                  // split: hit queue, LV_HIT_BYTES per hit, LV_SLICES << lv_hslice_log2 slots
+  double* lv_area;                 // split: {1 - covers, raise} per (hit, light)
 };
 
 // Where the sphere walk reads its records:
@@ -107,6 +120,8 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
 // Tree-record bytes for a scene with n_light lights (one leaf per fired light).
 int levels_rec_bytes(int n_light);
 constexpr size_t RAY_BYTES = 96;                // staged ray record of the bounce-level engine
+constexpr size_t LV_HIT_BYTES = 64;             // split phases: hit-queue record
+constexpr int LV_SPLIT_MAX_LIGHTS = 16;         // split phases only up to this many lights (shadow results per hit)
 hipError_t launch_path_trace(KParams p, hipStream_t s);
 // The lanes engine's re-render of the level-0 items listed in lv_redo_list
 // (SRC_LIST; exits at once when the list is empty).

@@ -1,28 +1,41 @@
 // rtx_levels.hip — the bounce-level engine on gfx950:
 // RayTracer#trace_sync (src/ray_tracer.rb:16-46) breadth-first, one launch per
-// ray-tree level, and Camera#render_at's reduction over the stored trees.
+// ray-tree level (or three: trace / shadow / shade), and Camera#render_at's
+// reduction over the stored trees.
 #include "rtx_device.h"
 
 namespace rtx {
 
 // ================================================================= bounce levels
 // The bounce-level engine (option "engine" = 1).  Instead of
-// one lane walking one sample's whole ray tree (the lanes engine above), every
-// ray of tree level d is one work item of the level-d launch: the camera
-// samples at level 0, their live children at level 1, and so on.  A wave's 64
-// lanes therefore run the same step of rt_map (ray_tracer.rb:50-164) on 64
-// rays at once, and no sample's tree can hold a launch open: a launch's
-// longest item is one ray.
+// one lane walking one sample's whole ray tree (the lanes engine), every ray
+// of tree level d is one work item of the level-d launch: the camera samples
+// at level 0, their live children at level 1, and so on.  A wave's 64 lanes
+// therefore run the same step of rt_map (ray_tracer.rb:50-164) on 64 rays at
+// once, and no sample's tree can hold a launch open: a launch's longest item
+// is one ray.
 //
 // Order.  trace_sync pops rays LIFO and drains the leaves FIFO afterwards
 // (ray_tracer.rb:31-45): leaves are summed in pre-order of the tree, children
 // visited in reverse push order (refraction after its pt siblings, reflection
 // last).  Each ray writes a tree record {first raise, leaf count, child mask,
-// first child, leaves} at its level; its live children go, contiguous and in
-// slot order, to the next level at an offset found by a wave prefix count
-// (ballot / mbcnt / shfl) plus one atomic per wave.  k_tree_finalize walks each
-// sample's tree in the reference's order and sums the leaves in it: the same
-// additions in the same order as the sequential program, so the same bits.
+// first child, leaves}; its live children go, contiguous and in slot order,
+// to the next level's queue.  k_tree_finalize walks each sample's tree in the
+// reference's order and sums the leaves in it: the same additions in the same
+// order as the sequential program, so the same bits.
+//
+// Queues without contended atomics.  One device-scope counter
+// word saturates at ~88 atomics/us on MI355X (MI355X_MICROARCH.md, "dequeue"),
+// below what one chunk claim plus one child allocation per 64 rays needs.  So
+//   * chunks are scheduled statically: wave w of W takes chunks w, w + W, ...;
+//   * a level's queue (levels >= 1) is cut into LV_SLICES slices of 2^k slots,
+//     each with its own counter on its own 128-B line; a wave allocates its
+//     children in slice (wave id mod LV_SLICES) with one atomicAdd (wave prefix
+//     count: ballot / mbcnt / shfl).  A consumer wave reads the 64 slice
+//     counts (one per lane), scans them, and maps its chunk to (slice, offset)
+//     with one ballot; dense ray indices (the record arena) are the slice
+//     prefix plus the offset, and k_tree_finalize translates a parent's child
+//     slot to the dense index the same way.
 //
 // Raises.  rt_map's raises happen while the tree is walked, the "color greater
 // than 1" of rt_reduce only in the drain after it (:39-45): a record keeps the
@@ -30,20 +43,20 @@ namespace rtx {
 // refraction; local_lights' lit_area; path tracing / local_lighting), the walk
 // takes the first in tree order, and a >1 partial sum counts only without one.
 //
-// Capacity.  Children beyond the staging buffer or tree records beyond the
-// record arena are not written; their camera sample is listed (lv_redo_list)
-// and re-rendered whole by the lanes engine (SRC_LIST), exact either way.
-constexpr int RAY_DOUBLES = 12;          // staging ray record: o, d, att, path, root item, pad (96 B)
+// Capacity.  Children beyond their slice or tree records beyond the record
+// arena are not written; their camera sample is listed (lv_redo_list) and
+// re-rendered whole by the lanes engine (SRC_LIST), exact either way.
+constexpr int RAY_DOUBLES = 12;          // staging ray record: o, d, att, path, root item, sample, x, y (96 B)
+constexpr int HIT_DOUBLES = 8;           // split hit record: hit, hit + delta, {ray, object | in}, {slot, raises}
+static_assert(RAY_DOUBLES * 8 == (int)RAY_BYTES && HIT_DOUBLES * 8 == (int)LV_HIT_BYTES, "record sizes");
 
 int levels_rec_bytes(int n_light) {
   const int nl = n_light > 1 ? n_light : 1;
   return (8 + 24 * nl + 15) & ~15;       // {meta, first child} + one leaf per fired light
 }
 
-__device__ __forceinline__ uint32_t lv_count(const KParams& p, int d) {
-  const uint32_t c = p.lv_ctl->count[d];
-  return d == 0 ? c : (c < p.lv_scap ? c : p.lv_scap);
-}
+// slice counter of slice s of a level (own 128-B line)
+__device__ __forceinline__ uint32_t* lv_slice_ctr(uint32_t* level_ctrs, int s) { return level_ctrs + s * 32; }
 
 __device__ __forceinline__ void lv_redo(const KParams& p, int root) {
   if (atomicCAS(&p.lv_redo_of[root], -1, -2) == -1) {
@@ -66,19 +79,137 @@ __device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, 
                       __builtin_bit_cast(double, (uint64_t)(uint32_t)x | (uint64_t)(uint32_t)y << 32));
 }
 
-// Launch `level` (0 .. trace_depth-1) of one batch.  Persistent: every wave
-// claims 64-ray chunks until the level's count is exhausted.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
+  const int lane = (int)__lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)v, off);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
+
+// One wave's view of a queue: lane s holds slice s (count clamped to the
+// slice capacity, exclusive item prefix, inclusive chunk prefix).  Level 0 is
+// one dense slice.  `mult` items per queue entry (the shadow launch: lights).
+struct LvQueue {
+  uint32_t cnt, pex, cin;      // per lane = per slice
+  uint32_t total, chunks;      // wave-uniform
+  __device__ __forceinline__ void dense(uint32_t n) {
+    const int lane = (int)__lane_id();
+    cnt = lane == 0 ? n : 0u;
+    pex = lane == 0 ? 0u : n;
+    cin = (n + 63u) >> 6;
+    total = n;
+    chunks = cin;
+  }
+  __device__ __forceinline__ void sliced(const uint32_t* ctrs, uint32_t cap, uint32_t mult) {
+    const int lane = (int)__lane_id();
+    uint32_t c = ctrs[lane * 32];
+    c = (c < cap ? c : cap) * mult;
+    const uint32_t incl = wave_scan_incl(c);
+    cnt = c;
+    pex = incl - c;
+    total = (uint32_t)__shfl((int)incl, 63);
+    cin = wave_scan_incl((c + 63u) >> 6);
+    chunks = (uint32_t)__shfl((int)cin, 63);
+  }
+  // chunk c (< chunks) -> this lane's slice s, offset within the slice, dense
+  // index; valid false past the slice's count.  All lanes must call it.
+  __device__ __forceinline__ bool item(uint32_t c, uint32_t& s, uint32_t& off, uint32_t& dense_i) const {
+    s = (uint32_t)__popcll(__ballot(cin <= c));
+    const uint32_t first = s ? (uint32_t)__shfl((int)cin, (int)s - 1) : 0u;
+    off = (c - first) * 64u + __lane_id();
+    dense_i = (uint32_t)__shfl((int)pex, (int)s) + off;
+    return off < (uint32_t)__shfl((int)cnt, (int)s);
+  }
+};
+
+// Dense ray count of level e (>= 1) of the batch (a wave reduction of its slices).
+__device__ __forceinline__ uint32_t lv_level_total(const KParams& p, int e) {
+  const int lane = (int)__lane_id();
+  const uint32_t cap = 1u << p.lv_slice_log2;
+  uint32_t c = p.lv_ctl->sc[e][lane * 32];
+  c = c < cap ? c : cap;
+  return (uint32_t)__shfl((int)wave_scan_incl(c), 63);
+}
+
+// Level d's first record in the arena: the dense counts of levels < d.
+__device__ __forceinline__ uint32_t lv_base(const KParams& p, int level) {
+  uint32_t base = level > 0 ? p.lv_ctl->count0 : 0u;
+  for (int e = 1; e < level; e++) base += lv_level_total(p, e);
+  return base;
+}
+
+__device__ __forceinline__ void lv_in_queue(const KParams& p, int level, LvQueue& q) {
+  if (level == 0) q.dense(p.lv_ctl->count0);
+  else q.sliced(p.lv_ctl->sc[level], 1u << p.lv_slice_log2, 1u);
+}
+
+// Chunk schedule of a launch: the first p.lv_static_pct % of the chunks
+// static (wave w of the grid's W waves takes chunks w, w + W, ...: no
+// atomics, but imbalanced when ray costs vary a lot, C4), the rest dynamic
+// over LV_CLAIMS sharded counters, counter j handing out chunks
+// S + j, S + j + LV_CLAIMS, ...; a wave starts at its home counter (wave id
+// mod LV_CLAIMS) and, once that is exhausted, reads all counters (one load
+// per lane, no atomic) and moves to one that is not.
+struct LvSched {
+  uint32_t* ctrs;              // this launch's claim counters (ctrs[j * 32])
+  uint32_t next, step, j, pct;
+  __device__ __forceinline__ LvSched(uint32_t* claim_ctrs, int static_pct) : ctrs(claim_ctrs), pct((uint32_t)static_pct) {
+    next = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    step = gridDim.x * (blockDim.x >> 6);
+    j = next & (LV_CLAIMS - 1);
+  }
+  __device__ __forceinline__ int wave_id() const { return (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); }
+  __device__ __forceinline__ bool claim(uint32_t chunks, uint32_t& c) {
+    const uint32_t S = (uint32_t)(((uint64_t)chunks * pct) / 100);
+    if (next < S) {
+      c = next;
+      next += step;
+      return true;
+    }
+    if (S == chunks) return false;
+    const int lane = (int)__lane_id();
+    while (true) {
+      uint32_t k = 0;
+      if (lane == 0) k = atomicAdd(&ctrs[j * 32], 1u);
+      c = S + j + LV_CLAIMS * (uint32_t)__shfl((int)k, 0);
+      if (c < chunks) return true;
+      // counter j is exhausted: look at all of them (plain loads past L1)
+      bool open = false;
+      if (lane < LV_CLAIMS) {
+        const uint32_t v = __hip_atomic_load(&ctrs[lane * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        open = S + (uint32_t)lane + LV_CLAIMS * v < chunks;
+      }
+      const uint64_t m = __ballot(open);
+      if (!m) return false;
+      const uint64_t rot = (m >> j) | (m << ((64 - j) & 63));   // the next open counter after j
+      j = (j + (uint32_t)__builtin_ctzll(rot)) & (LV_CLAIMS - 1);
+    }
+  }
+};
+
+// Exclusive wave prefix of `cnt` plus one atomicAdd of the wave's total on
+// `ctr` (skipped when the total is 0): the lane's first offset.
+__device__ __forceinline__ uint32_t lv_wave_alloc(uint32_t* ctr, int cnt) {
+  const int incl = (int)wave_scan_incl((uint32_t)cnt);
+  const int wtotal = __shfl(incl, 63);
+  uint32_t wbase = 0;
+  if (wtotal > 0) {
+    if (__lane_id() == 0) wbase = atomicAdd(ctr, (uint32_t)wtotal);
+    wbase = (uint32_t)__shfl((int)wbase, 0);
+  }
+  return wbase + (uint32_t)(incl - cnt);
+}
+
+// LDS staging of the sphere records / hierarchy of a walk workgroup.
 template <int SPH, int BS>
-__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level) {
+__device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph) {
   const SceneDev& S = p.scene;
-  const CameraDev& cam = *p.cam;
-  extern __shared__ float4 lds_sph[];
   char* lds = reinterpret_cast<char*>(lds_sph);
-  const uint32_t n = lv_count(p, level);
-  if (n == 0) return;                         // uniform: before any barrier
   if (SPH == SPH_LIN_LDS) {
-    for (int i = threadIdx.x; i < S.n_sphere + 4; i += BS)
-      lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
+    for (int i = threadIdx.x; i < S.n_sphere + 4; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
     __syncthreads();
   } else if (SPH == SPH_BVH_LDS) {
     const int nn = S.n_nodes * (int)(sizeof(Bvh4Node) / 16);
@@ -87,41 +218,202 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     for (int i = threadIdx.x; i < S.n_slots; i += BS) leaf[i] = reinterpret_cast<const float4*>(S.bvh_sph32)[i];
     __syncthreads();
   }
-  const float* sph_lds = reinterpret_cast<const float*>(lds_sph);
-  const RTX_CONST float* sph_k = cptr(S.sph32);
-  int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
-  int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
-  double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
+}
 
-  uint32_t base = 0;                          // this level's first record in lv_rec
-  for (int e = 0; e < level; e++) base += lv_count(p, e);
-  const double* __restrict__ in = p.lv_stage[level & 1];
-  double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
-  const int depth = cam.depth - level;        // trace_depth of this level's rays
+// One walk (EXTEND or SHADOW) through the launch's sphere mode.
+template <int SPH, int BS>
+__device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V3 o, V3 d, V3 L, double rad,
+                                        double& best, int& besti, V3& hit, bool& hin, double& total, uint32_t& err) {
+  const SceneDev& S = p.scene;
+  if (SPH == SPH_LIN_LDS) {
+    query<false>(S, reinterpret_cast<const float*>(lds), ext, o, d, L, rad, best, besti, hit, hin, total, err,
+                 nullptr);
+  } else if (SPH == SPH_LIN_SCALAR) {
+    query<false>(S, cptr(S.sph32), ext, o, d, L, rad, best, besti, hit, hin, total, err, nullptr);
+  } else {
+    int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
+    int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
+    double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
+    int q_ref = BVH_NONE, q_sp = 0, q_ncov = 0;
+    bool q_ovf = false;
+    if (SPH == SPH_BVH_LDS)
+      query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
+                           stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp,
+                           q_ncov, q_ovf, false, 0);
+    else
+      query_bvh<BS, false>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), stk, cov_i, cov_v, ext, o, d, L,
+                           rad, best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
+  }
+}
+
+// The ray of a level's queue entry: a camera sample (level 0: `idx` = its
+// item, Camera#lens_func) or the staged child at slot `idx`.  `valid` false
+// for the padding of an 8x8 tile.
+__device__ __forceinline__ void lv_ray(const KParams& p, int level, uint32_t idx, Item& cur, int& root, int& x, int& y,
+                                       int& sample, bool& valid) {
+  valid = true;
+  if (level == 0) {
+    root = (int)idx;
+    const ItemPos ip = decode_item(p, root);
+    x = p.x0 + ip.px;
+    y = row_to_y(p, ip.row);
+    sample = ip.sample;
+    valid = ip.valid;
+    if (valid) {
+      const CameraDev& cam = *p.cam;
+      cur.ray = lens_ray(cam, lens_target(cam, x, y), x, y, sample, p.seed);
+      cur.att = v3(1.0, 1.0, 1.0);
+      cur.path = 1;
+    }
+    return;
+  }
+  const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)idx * RAY_DOUBLES);
+  const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
+  cur.ray.o = v3(a.x, a.y, b.x);
+  cur.ray.d = v3(b.y, c.x, c.y);
+  cur.att = v3(d.x, d.y, e.x);
+  cur.path = __builtin_bit_cast(uint64_t, e.y);
+  const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
+  root = (int)(uint32_t)rs;
+  sample = (int)(rs >> 32);
+  x = (int)(uint32_t)xy;
+  y = (int)(xy >> 32);
+}
+
+// rt_map's tail once the lit areas are known (ray_tracer.rb:80-158): which
+// children pass the cutoff (:52) at depth - 1, their slots in the next level
+// (slice of this wave), the children in the reference's push order, else the
+// local_lighting leaf; then the ray's tree record.  Shared by k_level and
+// k_lv_shade; every lane of the wave calls it (the slot allocation is a wave
+// operation).  errA/errS/errL/errP: the raises so far, in rt_map's order.
+__device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice, bool shade, bool active,
+                                          const Item& cur, int root, int x, int y, int sample, int besti, bool hin,
+                                          V3 hit, V3 delta, V3 nrm, V3 nn, double c, V3 lc, int nl, char* rec,
+                                          int nleaf, uint32_t errA, uint32_t errS, uint32_t errL, uint32_t errP) {
+  const SceneDev& S = p.scene;
+  const CameraDev& cam = *p.cam;
+  const int depth = cam.depth - level;
   const int pt = cam.pt;
   const uint64_t R = (uint64_t)pt + 3;
-  const int lane = (int)__lane_id();
-
-  // walk dispatch (the same query code as the lanes engine; every lane of a
-  // level launch runs the same query kind at the same time)
-  auto walk = [&](bool ext, V3 o, V3 d, V3 L, double rad, double& best, int& besti, V3& hit, bool& hin,
-                  double& total, uint32_t& err) {
-    if (SPH == SPH_LIN_LDS)
-      query<false>(S, sph_lds, ext, o, d, L, rad, best, besti, hit, hin, total, err, nullptr);
-    else if (SPH == SPH_LIN_SCALAR)
-      query<false>(S, sph_k, ext, o, d, L, rad, best, besti, hit, hin, total, err, nullptr);
-    else {
-      int q_ref = BVH_NONE, q_sp = 0, q_ncov = 0;
-      bool q_ovf = false;
-      if (SPH == SPH_BVH_LDS)
-        query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
-                             stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp,
-                             q_ncov, q_ovf, false, 0);
-      else
-        query_bvh<BS, false>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), stk, cov_i, cov_v, ext, o, d, L,
-                             rad, best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
+  uint32_t mask = 0;
+  double rate = 0.0;
+  bool may_refract = false;
+  const Material* m = shade ? &S.mat[besti] : S.mat;
+  if (shade) {
+    const int cd = depth - 1;
+    if (cd > 0 && !(vr(vmul(cur.att, v3p(m->refl_att))) < 0.0001)) mask |= 1u;
+    if (m->type == OBJ_SPHERE) {            // sphere.rb:92-94: rate inverted leaving
+      may_refract = true;
+      rate = hin ? m->rr : 1.0 / m->rr;
+    } else if (m->has_rr) {                 // plane.rb:57-61: the same rate both ways
+      may_refract = true;
+      rate = m->rr;
     }
-  };
+    if (may_refract && !(sqrt(1.0 - c * c) / rate >= 1) && cd > 0 &&
+        !(vr(vmul(cur.att, v3p(m->refr_att))) < 0.0001))
+      mask |= 2u;                           // refraction exists (no TIR) and is alive
+    if (nl == 0 && cd > 0 && !(vr(vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt))) < 0.0001))
+      mask |= ((1u << pt) - 1u) << 2;       // every path-tracing child (same attenuation)
+  }
+  // room in the next level: this wave's slice, wave prefix count + one atomic
+  const uint32_t log2cap = (uint32_t)p.lv_slice_log2, cap = 1u << log2cap;
+  const uint32_t off0 = lv_wave_alloc(lv_slice_ctr(p.lv_ctl->sc[level + 1], slice), __popc(mask));
+  const uint32_t child0 = ((uint32_t)slice << log2cap) + off0;   // slot of the first child (k_tree_finalize)
+  if (shade) {
+    double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
+    uint32_t off = off0;
+    auto put = [&](const Ray& r, V3 att, uint64_t path) {
+      if (off < cap) lv_store_ray(outs + (size_t)(((uint32_t)slice << log2cap) + off) * RAY_DOUBLES, r, att, path, root,
+                                  x, y, sample);
+      else {
+        lv_redo(p, root);
+        atomicAdd(&p.lv_ctl->dropped, 1u);
+      }
+      off++;
+    };
+    const Ray refl = reflection(cur.ray, nn, c, hit, delta, errS);
+    if (mask & 1u) put(refl, vmul(cur.att, v3p(m->refl_att)), cur.path * R + 1);
+    if (may_refract) {
+      Ray refr;
+      if (refraction(cur.ray, nn, c, hit, refl.d, rate, refr, errS) && (mask & 2u))
+        put(refr, vmul(cur.att, v3p(m->refr_att)), cur.path * R + 2);
+    }
+    if (nl == 0) {
+      // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
+      const V3 att = vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt));
+      const V3 left = vnorm(vertical_vector(nrm, errP), errP);
+      const V3 up = vcross(nn, left);
+      Ray r;
+      r.o = vadd(hit, delta);
+      for (int k = 0; k < pt; k++) {
+        const double theta = rand01(p.seed, x, y, sample, cur.path, 2 * k) * PI / 2.0;
+        const double phi = rand01(p.seed, x, y, sample, cur.path, 2 * k + 1) * PI * 2.0;
+        double sth, cth, sph, cph;
+        RTX_SINCOS(theta, &sth, &cth);
+        RTX_SINCOS(phi, &sph, &cph);
+        r.d = vadd(vsc(nn, sth), vsc(vadd(vsc(left, cph), vsc(up, sph)), cth));
+        if (mask >> (2 + k) & 1u) put(r, att, cur.path * R + 3 + (uint64_t)k);
+      }
+    } else {
+      // WorldObject#local_lighting's colour (world_object.rb:51-74), texture filter
+      lc = vdiv(lc, (double)nl);
+      V3 color;
+      if (m->type == OBJ_BOX) {
+        color = vadd(vmul(lc, v3p(m->diffuse)), v3p(m->ambient));
+      } else {
+        V3 filter = v3(1.0, 1.0, 1.0);
+        if (m->tex >= 0) {
+          if (m->type == OBJ_SPHERE) {             // Sphere#get_uv (sphere.rb:111-120)
+            const Sphere64 sp = S.sph64[m->rec];
+            const V3 vec = vsub(hit, v3p(sp.c));
+            const double x0 = vdot(vec, v3p(m->gw_n)) / sp.r;
+            const double y0 = vdot(vec, v3p(m->east_n)) / sp.r;
+            const double z0 = vdot(vec, v3p(m->north_n)) / sp.r;
+            const double mm2 = x0 * x0 + y0 * y0 + z0 * z0 + 2.0 * x0 + 1.0;
+            if (mm2 < 0) seterr(errP, ERR_DOMAIN);
+            const double mm = sqrt(mm2);
+            filter = vmul(texcolor(S, m->tex, m->hs, m->vs, m->u_off, m->v_off, (y0 / mm + 1.0) / 2.0,
+                                   (-z0 / mm + 1.0) / 2.0, errP), filter);
+          } else {
+            double u, v;
+            plane_uv(S.planes + (size_t)m->rec * PLANE_GEO, hit, u, v);
+            filter = vmul(texcolor(S, m->tex, m->hs, m->vs, 0.0, 0.0, u, v, errP), filter);
+          }
+        }
+        color = vadd(vmul(vmul(lc, v3p(m->diffuse)), filter), v3p(m->ambient));
+      }
+      const V3 leaf = vmul(cur.att, color);
+      double* leafp = reinterpret_cast<double*>(rec + 8);
+      leafp[0] = leaf.x;
+      leafp[1] = leaf.y;
+      leafp[2] = leaf.z;
+      nleaf = 1;
+    }
+  }
+  if (active) {
+    uint32_t err = errA;
+    if (!err) err = errS;
+    if (!err) err = errL;
+    if (!err) err = errP;
+    *reinterpret_cast<uint2*>(rec) = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8) | (mask << 16), child0);
+  }
+}
+
+// Level `level` (0 .. trace_depth-1) of one batch in one launch (option
+// lv_split = 0).  Persistent, static chunk schedule.
+template <int SPH, int BS>
+__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level) {
+  const SceneDev& S = p.scene;
+  extern __shared__ float4 lds_sph[];
+  char* lds = reinterpret_cast<char*>(lds_sph);
+  LvQueue in;
+  lv_in_queue(p, level, in);
+  if (in.chunks == 0) return;                 // uniform: before any barrier
+  lv_stage_scene<SPH, BS>(p, lds_sph);
+  const uint32_t base = lv_base(p, level);
+  const int depth = p.cam->depth - level;
+  LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
+  const int slice = sched.wave_id() & (LV_SLICES - 1);
 
   unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
 #define RTX_LV_STAMP(k)  \
@@ -130,68 +422,25 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     tS[k] += t1 - t0;    \
     t0 = t1;             \
   }
-  // Chunk claims: one atomic per 64 rays (RTX_LV_CLAIM_AHEAD issues the next
-  // claim when a chunk starts instead; measured no faster).
-  int next = 0;
-  if (RTX_LV_CLAIM_AHEAD) {
-    if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
-  }
-  while (true) {
+  uint32_t chunk;
+  while (sched.claim(in.chunks, chunk)) {
     if (RTX_STAMPS) {
       t0 = stamp();
       nchunks++;
     }
-    int chunk = 0;
-    if (RTX_LV_CLAIM_AHEAD) {
-      chunk = __shfl(next, 0);
-      if ((uint32_t)chunk * 64u >= n) break;
-      if (lane == 0) next = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
-    } else {
-      if (lane == 0) chunk = (int)atomicAdd(&p.lv_ctl->claim[level], 1u);
-      chunk = __shfl(chunk, 0);
-      if ((uint32_t)chunk * 64u >= n) break;
-    }
-    const uint32_t i = (uint32_t)chunk * 64u + (uint32_t)lane;
-    bool active = i < n;
-
+    uint32_t s, off, i;
+    bool active = in.item(chunk, s, off, i);  // i: the ray's dense index in the level
     // ---- the ray: a camera sample (level 0) or a staged child
     Item cur;
     int root = 0, x = 0, y = 0, sample = 0;
     bool alive = false;
     if (active) {
-      if (level == 0) {
-        root = (int)i;
-      } else {
-        const double2* q = reinterpret_cast<const double2*>(in + (size_t)i * RAY_DOUBLES);
-        const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
-        cur.ray.o = v3(a.x, a.y, b.x);
-        cur.ray.d = v3(b.y, c.x, c.y);
-        cur.att = v3(d.x, d.y, e.x);
-        cur.path = __builtin_bit_cast(uint64_t, e.y);
-        const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
-        root = (int)(uint32_t)rs;
-        sample = (int)(rs >> 32);
-        x = (int)(uint32_t)xy;
-        y = (int)(xy >> 32);
-      }
-      if (level == 0) {
-        p.lv_redo_of[i] = -1;                 // no overflow yet (lv_redo)
-        const ItemPos ip = decode_item(p, root);
-        x = p.x0 + ip.px;
-        y = row_to_y(p, ip.row);
-        sample = ip.sample;
-        if (ip.valid) {
-          cur.ray = lens_ray(cam, lens_target(cam, x, y), x, y, sample, p.seed);
-          cur.att = v3(1.0, 1.0, 1.0);
-          cur.path = 1;
-          alive = !(depth <= 0 || vr(cur.att) < 0.0001);   // rt_map's cutoff (ray_tracer.rb:52)
-        } else {
-          active = false;                     // padding of an 8x8 tile: no record
-        }
-      } else {
-        alive = true;                         // children are staged only past the cutoff
-      }
-      if (active && base + i >= p.lv_lcap) { // no room for this ray's record
+      bool valid;
+      lv_ray(p, level, level == 0 ? i : (s << p.lv_slice_log2) + off, cur, root, x, y, sample, valid);
+      if (level == 0) p.lv_redo_of[i] = -1;   // no overflow yet (lv_redo)
+      active = valid;                         // tile padding: no record
+      alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // rt_map's cutoff (ray_tracer.rb:52)
+      if (active && base + i >= p.lv_lcap) {  // no room for this ray's record
         lv_redo(p, root);
         active = alive = false;
       }
@@ -199,9 +448,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
     double* leafp = reinterpret_cast<double*>(rec + 8);
 
-    // ---- rt_map: highlights (ray_tracer.rb:60-75), raises in rt_map's order:
-    // errA highlights, errS intersect_parameters (reflection / refraction),
-    // errL local_lights' lit_area, errP path_tracing / local_lighting
+    // ---- rt_map: highlights (ray_tracer.rb:60-75)
     uint32_t errA = 0, errS = 0, errL = 0, errP = 0;
     int nleaf = 0;
     bool fired = false;
@@ -212,7 +459,6 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
       }, errA);
-
     RTX_LV_STAMP(0)
     // ---- World#intersect (world.rb:37-59)
     const bool ext = alive && !fired;
@@ -220,10 +466,9 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     int besti = -1;
     V3 hit = v3(0.0, 0.0, 0.0);
     bool hin = true;
-    if (ext) walk(true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
+    if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
     const bool shade = ext && besti >= 0;
     RTX_LV_STAMP(1)
-
     V3 delta = hit, nrm = hit, nn = hit;
     double c = 0.0;
     if (shade) {
@@ -232,12 +477,9 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
       c = vcos(cur.ray.d, nrm, errS);         // ray.front.cos(-n): same bits as cos(n)
     }
     const V3 qo = vadd(hit, delta);           // the shadow rays' target point (world.rb:76)
-
     RTX_LV_STAMP(2)
     // ---- World#local_lights (world.rb:72-80) fused with local_lighting's
-    // light loop (world_object.rb:51-74): one SHADOW walk per light.  (Holding
-    // delta / n / n.normalize across the walks measured faster than
-    // recomputing them after: 6.22 vs 6.40 ms on C2.)
+    // light loop (world_object.rb:51-74): one SHADOW walk per light.
     V3 lc = v3(0.0, 0.0, 0.0);
     int nl = 0;
     for (int li = 0; li < S.n_light; li++) {
@@ -249,7 +491,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
       int bi2 = -1;
       V3 h2 = qo;
       bool in2 = true;
-      walk(false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL);
+      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL);
       const double area = tot > 0 ? tot : 0.0;
       if (area > 0) {
         nl++;
@@ -263,146 +505,267 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
       }
     }
     RTX_LV_STAMP(3)
-    // ---- which children pass rt_map's cutoff (ray_tracer.rb:52) at depth - 1
-    uint32_t mask = 0;
-    double rate = 0.0;
-    bool may_refract = false;
-    const Material* m = shade ? &S.mat[besti] : S.mat;
-    if (shade) {
-      const int cd = depth - 1;
-      if (cd > 0 && !(vr(vmul(cur.att, v3p(m->refl_att))) < 0.0001)) mask |= 1u;
-      if (m->type == OBJ_SPHERE) {            // sphere.rb:92-94: rate inverted leaving
-        may_refract = true;
-        rate = hin ? m->rr : 1.0 / m->rr;
-      } else if (m->has_rr) {                 // plane.rb:57-61: the same rate both ways
-        may_refract = true;
-        rate = m->rr;
-      }
-      if (may_refract && !(sqrt(1.0 - c * c) / rate >= 1) && cd > 0 &&
-          !(vr(vmul(cur.att, v3p(m->refr_att))) < 0.0001))
-        mask |= 2u;                           // refraction exists (no TIR) and is alive
-      if (nl == 0 && cd > 0 && !(vr(vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt))) < 0.0001))
-        mask |= ((1u << pt) - 1u) << 2;       // every path-tracing child (same attenuation)
-    }
-
-    // ---- room in the next level: wave prefix count of the live children + one atomic
-    const int cnt = __popc(mask);
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int t = __shfl_up(incl, off);
-      if (lane >= off) incl += t;
-    }
-    const int wtotal = __shfl(incl, 63);
-    uint32_t wbase = 0;
-    if (wtotal > 0) {
-      if (lane == 0) wbase = atomicAdd(&p.lv_ctl->count[level + 1], (uint32_t)wtotal);
-      wbase = __shfl(wbase, 0);
-    }
-    const uint32_t child0 = wbase + (uint32_t)(incl - cnt);
-    RTX_LV_STAMP(4)
-
-    // ---- children in the reference's push order (ray_tracer.rb:84-143), then the leaf
-    if (shade) {
-      uint32_t slot = child0;
-      auto put = [&](const Ray& r, V3 att, uint64_t path) {
-        if (slot < p.lv_scap) lv_store_ray(outs + (size_t)slot * RAY_DOUBLES, r, att, path, root, x, y, sample);
-        else {
-          lv_redo(p, root);
-          atomicAdd(&p.lv_ctl->dropped, 1u);
-        }
-        slot++;
-      };
-      const Ray refl = reflection(cur.ray, nn, c, hit, delta, errS);
-      if (mask & 1u) put(refl, vmul(cur.att, v3p(m->refl_att)), cur.path * R + 1);
-      if (may_refract) {
-        Ray refr;
-        if (refraction(cur.ray, nn, c, hit, refl.d, rate, refr, errS) && (mask & 2u))
-          put(refr, vmul(cur.att, v3p(m->refr_att)), cur.path * R + 2);
-      }
-      if (nl == 0) {
-        // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
-        const V3 att = vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt));
-        const V3 left = vnorm(vertical_vector(nrm, errP), errP);
-        const V3 up = vcross(nn, left);
-        Ray r;
-        r.o = vadd(hit, delta);
-        for (int k = 0; k < pt; k++) {
-          const double theta = rand01(p.seed, x, y, sample, cur.path, 2 * k) * PI / 2.0;
-          const double phi = rand01(p.seed, x, y, sample, cur.path, 2 * k + 1) * PI * 2.0;
-          double sth, cth, sph, cph;
-          RTX_SINCOS(theta, &sth, &cth);
-          RTX_SINCOS(phi, &sph, &cph);
-          r.d = vadd(vsc(nn, sth), vsc(vadd(vsc(left, cph), vsc(up, sph)), cth));
-          if (mask >> (2 + k) & 1u) put(r, att, cur.path * R + 3 + (uint64_t)k);
-        }
-      } else {
-        // WorldObject#local_lighting's colour (world_object.rb:51-74), texture filter
-        lc = vdiv(lc, (double)nl);
-        V3 color;
-        if (m->type == OBJ_BOX) {
-          color = vadd(vmul(lc, v3p(m->diffuse)), v3p(m->ambient));
-        } else {
-          V3 filter = v3(1.0, 1.0, 1.0);
-          if (m->tex >= 0) {
-            if (m->type == OBJ_SPHERE) {             // Sphere#get_uv (sphere.rb:111-120)
-              const Sphere64 sp = S.sph64[m->rec];
-              const V3 vec = vsub(hit, v3p(sp.c));
-              const double x0 = vdot(vec, v3p(m->gw_n)) / sp.r;
-              const double y0 = vdot(vec, v3p(m->east_n)) / sp.r;
-              const double z0 = vdot(vec, v3p(m->north_n)) / sp.r;
-              const double mm2 = x0 * x0 + y0 * y0 + z0 * z0 + 2.0 * x0 + 1.0;
-              if (mm2 < 0) seterr(errP, ERR_DOMAIN);
-              const double mm = sqrt(mm2);
-              filter = vmul(texcolor(S, m->tex, m->hs, m->vs, m->u_off, m->v_off, (y0 / mm + 1.0) / 2.0,
-                                     (-z0 / mm + 1.0) / 2.0, errP), filter);
-            } else {
-              double u, v;
-              plane_uv(S.planes + (size_t)m->rec * PLANE_GEO, hit, u, v);
-              filter = vmul(texcolor(S, m->tex, m->hs, m->vs, 0.0, 0.0, u, v, errP), filter);
-            }
-          }
-          color = vadd(vmul(vmul(lc, v3p(m->diffuse)), filter), v3p(m->ambient));
-        }
-        const V3 leaf = vmul(cur.att, color);
-        leafp[0] = leaf.x;
-        leafp[1] = leaf.y;
-        leafp[2] = leaf.z;
-        nleaf = 1;
-      }
-    }
-    if (active) {
-      uint32_t err = errA;
-      if (!err) err = errS;
-      if (!err) err = errL;
-      if (!err) err = errP;
-      uint2* hdr = reinterpret_cast<uint2*>(rec);
-      *hdr = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8) | (mask << 16), child0);
-    }
+    lv_finish(p, level, slice, shade, active, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec,
+              nleaf, errA, errS, errL, errP);
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
-  if (RTX_STAMPS && lane == 0) {
+  if (RTX_STAMPS && __lane_id() == 0) {
     for (int k = 0; k < 6; k++) atomicAdd(&rtx_stamps[k], tS[k]);
     atomicAdd(&rtx_stamps[6], nchunks);
     atomicAdd(&rtx_stamps[7], 1ull);
   }
 }
 
+// ----------------------------------------------------------------- split phases
+// Option lv_split = 1: every level runs as three launches,
+// each over a dense queue, so a wave's 64 lanes do the same phase of rt_map:
+//   k_lv_trace   every ray of the level: highlights (world.rb:83-98) and the
+//                nearest-hit walk (World#intersect, world.rb:37-59).  A ray
+//                that stops here (dead, fired, miss) writes its tree record;
+//                a hit goes to the level's hit queue (sliced like the ray
+//                queues): {hit, hit + delta, ray, object, :in, slot, raises}.
+//   k_lv_shadow  every (hit, light) pair: World#lit_area's walk (world.rb:62-80)
+//                from hit + delta towards the light -> {1 - covers, raise}.
+//   k_lv_shade   every hit: intersect_parameters, local_lights' colour,
+//                the children (reflection, refraction, path tracing) into the
+//                next level and the local_lighting leaf; the tree record.
+// The phases evaluate the same operations on the same values as k_level
+// (hit_info re-evaluated from the stored hit gives its bits again), so the
+// trees, hence the frames, are bit-identical to the fused kernel's.
+#ifndef RTX_LV_WALK_WPS
+#define RTX_LV_WALK_WPS 3                 // waves per SIMD k_lv_trace / k_lv_shadow are compiled for
+#endif
+#ifndef RTX_LV_SHADE_WPS
+#define RTX_LV_SHADE_WPS 3                // k_lv_shade (no walk)
+#endif
+constexpr int BS_SHADE = 256;
+
+template <int SPH, int BS>
+__global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int level) {
+  const SceneDev& S = p.scene;
+  extern __shared__ float4 lds_sph[];
+  char* lds = reinterpret_cast<char*>(lds_sph);
+  LvQueue in;
+  lv_in_queue(p, level, in);
+  if (in.chunks == 0) return;                 // uniform: before any barrier
+  lv_stage_scene<SPH, BS>(p, lds_sph);
+  const uint32_t base = lv_base(p, level);
+  const int depth = p.cam->depth - level;
+  LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
+  const int slice = sched.wave_id() & (LV_SLICES - 1);
+  const uint32_t hlog2 = (uint32_t)p.lv_hslice_log2, hcap = 1u << hlog2;
+  uint32_t chunk;
+  while (sched.claim(in.chunks, chunk)) {
+    uint32_t s, off, i;
+    bool active = in.item(chunk, s, off, i);
+    const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
+    bool alive = false;
+    Item cur;
+    int root = 0, x = 0, y = 0, sample = 0;
+    if (active) {
+      bool valid;
+      lv_ray(p, level, slot, cur, root, x, y, sample, valid);
+      if (level == 0) p.lv_redo_of[i] = -1;   // no overflow yet (lv_redo)
+      active = valid;                         // tile padding: no record
+      alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // rt_map's cutoff (ray_tracer.rb:52)
+      if (active && base + i >= p.lv_lcap) {  // no room for this ray's record
+        lv_redo(p, root);
+        active = alive = false;
+      }
+    }
+    char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
+    double* leafp = reinterpret_cast<double*>(rec + 8);
+    uint32_t errA = 0, errL = 0;
+    int nleaf = 0;
+    bool fired = false;
+    if (alive)
+      fired = highlight_leaves(S, cur, [&](V3 c) {
+        leafp[3 * nleaf] = c.x;
+        leafp[3 * nleaf + 1] = c.y;
+        leafp[3 * nleaf + 2] = c.z;
+        nleaf++;
+      }, errA);
+    const bool ext = alive && !fired;
+    double best = S.max_distance, total = 0.0;
+    int besti = -1;
+    V3 hit = v3(0.0, 0.0, 0.0);
+    bool hin = true;
+    if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
+    bool shade = ext && besti >= 0;
+    V3 delta = hit, nrm = hit;
+    if (shade) hit_info(S, besti, cur.ray, hit, delta, nrm, hin);
+    const uint32_t h = lv_wave_alloc(lv_slice_ctr(p.lv_ctl->sh[level], slice), shade ? 1 : 0);
+    if (shade && h >= hcap) {                 // the hit queue's slice is full
+      lv_redo(p, root);
+      shade = false;
+    }
+    if (shade) {
+      const V3 qo = vadd(hit, delta);         // the shadow rays' target point (world.rb:76)
+      double2* q = reinterpret_cast<double2*>(p.lv_hit + (size_t)(((uint32_t)slice << hlog2) + h) * HIT_DOUBLES);
+      q[0] = make_double2(hit.x, hit.y);
+      q[1] = make_double2(hit.z, qo.x);
+      q[2] = make_double2(qo.y, qo.z);
+      q[3] = make_double2(
+          __builtin_bit_cast(double, (uint64_t)i | (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) << 32),
+          __builtin_bit_cast(double, (uint64_t)slot | (uint64_t)((errA & 0xffu) | (errL & 0xffu) << 8) << 32));
+    } else if (active) {
+      uint32_t err = errA;
+      if (!err) err = errL;
+      *reinterpret_cast<uint2*>(rec) = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8), 0u);
+    }
+  }
+}
+
+template <int SPH, int BS>
+__global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_shadow(KParams p, int level) {
+  const SceneDev& S = p.scene;
+  extern __shared__ float4 lds_sph[];
+  char* lds = reinterpret_cast<char*>(lds_sph);
+  const uint32_t nL = (uint32_t)S.n_light;
+  const uint32_t hlog2 = (uint32_t)p.lv_hslice_log2;
+  LvQueue in;
+  in.sliced(p.lv_ctl->sh[level], 1u << hlog2, nL);
+  if (in.chunks == 0) return;
+  lv_stage_scene<SPH, BS>(p, lds_sph);
+  LvSched sched(p.lv_ctl->claim[1][level], p.lv_static_pct);
+  uint32_t chunk;
+  while (sched.claim(in.chunks, chunk)) {
+    uint32_t s, off, t;
+    if (in.item(chunk, s, off, t)) {          // (lanes past their slice idle until the next chunk)
+      const uint32_t hs = (s << hlog2) + off / nL, li = off % nL;   // hit slot, light
+      const double* q = p.lv_hit + (size_t)hs * HIT_DOUBLES;
+      const double2 a = *reinterpret_cast<const double2*>(q + 2), b = *reinterpret_cast<const double2*>(q + 4);
+      const V3 qo = v3(a.y, b.x, b.y);
+      const LightDev& L = S.light[li];
+      const V3 qL = v3p(L.pos);
+      double tot = 1.0, b2 = 0.0;
+      int bi2 = -1;
+      V3 h2 = qo;
+      bool in2 = true;
+      uint32_t err = 0;
+      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, err);
+      reinterpret_cast<double2*>(p.lv_area)[(size_t)hs * nL + li] =
+          make_double2(tot, __builtin_bit_cast(double, (uint64_t)err));
+    }
+  }
+}
+
+__global__ __launch_bounds__(BS_SHADE, RTX_LV_SHADE_WPS) void k_lv_shade(KParams p, int level) {
+  const SceneDev& S = p.scene;
+  const uint32_t hlog2 = (uint32_t)p.lv_hslice_log2;
+  LvQueue in;
+  in.sliced(p.lv_ctl->sh[level], 1u << hlog2, 1u);
+  if (in.chunks == 0) return;
+  const uint32_t base = lv_base(p, level);
+  const int nL = S.n_light;
+  LvSched sched(p.lv_ctl->claim[2][level], p.lv_static_pct);
+  const int slice = sched.wave_id() & (LV_SLICES - 1);
+  uint32_t chunk;
+  while (sched.claim(in.chunks, chunk)) {
+    uint32_t s, off, t;
+    const bool shade = in.item(chunk, s, off, t);
+    const uint32_t hs = (s << hlog2) + off;   // hit slot
+    V3 hit = v3(0.0, 0.0, 0.0);
+    uint32_t i = 0, errA = 0, errL = 0, errS = 0, errP = 0;
+    int besti = 0;
+    bool hin = true;
+    Item cur;
+    int root = 0, x = 0, y = 0, sample = 0;
+    if (shade) {
+      const double2* q = reinterpret_cast<const double2*>(p.lv_hit + (size_t)hs * HIT_DOUBLES);
+      const double2 a = q[0], b = q[1], d = q[3];
+      hit = v3(a.x, a.y, b.x);
+      const uint64_t ib = __builtin_bit_cast(uint64_t, d.x), se = __builtin_bit_cast(uint64_t, d.y);
+      i = (uint32_t)ib;
+      besti = (int)((uint32_t)(ib >> 32) & 0x7fffffffu);
+      hin = (ib >> 63) != 0;
+      errA = (uint32_t)(se >> 32) & 0xffu;
+      errL = (uint32_t)(se >> 40) & 0xffu;
+      bool valid;
+      lv_ray(p, level, (uint32_t)se, cur, root, x, y, sample, valid);
+    }
+    char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
+    V3 delta = hit, nrm = hit, nn = hit;
+    double c = 0.0;
+    if (shade) {
+      hit_info(S, besti, cur.ray, hit, delta, nrm, hin);   // the bits k_lv_trace computed
+      nn = vnorm(nrm, errS);                  // n.normalize (world_object.rb:123)
+      c = vcos(cur.ray.d, nrm, errS);         // ray.front.cos(-n): same bits as cos(n)
+    }
+    // World#local_lights' areas (k_lv_shadow) into local_lighting's light loop
+    V3 lc = v3(0.0, 0.0, 0.0);
+    int nl = 0;
+    for (int li = 0; li < nL; li++) {
+      if (!shade) continue;
+      const double2 ar = reinterpret_cast<const double2*>(p.lv_area)[(size_t)hs * nL + li];
+      seterr(errL, (uint32_t)__builtin_bit_cast(uint64_t, ar.y));
+      const double tot = ar.x;
+      const double area = tot > 0 ? tot : 0.0;
+      if (area > 0) {
+        const LightDev& L = S.light[li];
+        nl++;
+        const double pw = S.sse_is_two ? area * area : rx_pow(area, S.sse);
+        const V3 lcol = vsc(v3p(L.color), pw / (double)nL);
+        const V3 ll = vnorm(vsub(v3p(L.pos), hit), errP);
+        double ldn = vdot(ll, nn);
+        if (ldn > 1) ldn = 1.0;
+        else if (ldn < 0) ldn = 0.0;
+        lc = vadd(lc, vsc(lcol, ldn));
+      }
+    }
+    lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec,
+              0, errA, errS, errL, errP);
+  }
+}
+
+// ----------------------------------------------------------------- tree reduction
+// The batch's level layout for the reductions: base[d] = first record of level
+// d, pex[d * 64 + s] = dense index of slice s's first ray at level d (d >= 1).
+// Block 0 also adds the batch's level statistics to lv_acc (rtx_level_stats):
+// every level launch of the batch has ended.
+__device__ __forceinline__ void lv_layout(const KParams& p, int nlev, uint32_t* base, uint32_t* pex) {
+  __shared__ uint32_t tot[LV_MAXL + 1];
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)__lane_id();
+  const uint32_t cap = 1u << p.lv_slice_log2;
+  for (int e = 1 + wave; e < nlev; e += (int)(blockDim.x >> 6)) {
+    uint32_t c = p.lv_ctl->sc[e][lane * 32];
+    c = c < cap ? c : cap;
+    const uint32_t incl = wave_scan_incl(c);
+    pex[e * 64 + lane] = incl - c;
+    if (lane == 63) tot[e] = incl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t b = 0;
+    for (int d = 0; d <= nlev && d <= LV_MAXL; d++) {
+      base[d] = b;
+      if (d < nlev) b += d == 0 ? p.lv_ctl->count0 : tot[d];
+    }
+  }
+  if (blockIdx.x == 0 && p.lv_acc) {
+    const int t = (int)threadIdx.x;
+    if (t == 0) p.lv_acc[0] += p.lv_ctl->redo_n;
+    if (t == 1) p.lv_acc[1] += p.lv_ctl->dropped;
+    if (t < nlev) p.lv_acc[2 + t] += t == 0 ? p.lv_ctl->count0 : tot[t];
+  }
+  __syncthreads();
+}
+
 // Sum of one camera sample's tree (level-0 item `root`) in trace_sync's
-// order: pre-order, children in reverse slot order; `base` = first record of
-// every level.  Returns the first raise (rt_map's first, else rt_reduce's).
-// The walk keeps one pending child range per level below the root in
-// lo[k * st] / hi[k * st], k < sd (LDS, word-major over the block's threads,
-// or a private array with st = 1).
-__device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base, int root, int nlev,
-                                          uint32_t* lo, uint32_t* hi, int st, int sd, uint32_t& err_out) {
+// order: pre-order, children in reverse slot order.  Returns the first raise
+// (rt_map's first, else rt_reduce's).  The walk keeps one pending child range
+// per level below the root in lo[k * st] / hi[k * st], k < sd (LDS, word-major
+// over the block's threads, or a private array with st = 1).
+__device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base, const uint32_t* pex, int root,
+                                          int nlev, uint32_t* lo, uint32_t* hi, int st, int sd, uint32_t& err_out) {
   int sp = 0;
   V3 sum = v3(0.0, 0.0, 0.0);
   uint32_t err = 0, pf = 0;
   bool gt1 = false;
   int lev = 0;
   uint32_t q = (uint32_t)root;
+  const uint32_t log2cap = (uint32_t)p.lv_slice_log2;
   while (true) {
     const char* rec = p.lv_rec + (size_t)(base[lev] + q) * p.lv_rec_bytes;
     const uint2 hdr = *reinterpret_cast<const uint2*>(rec);
@@ -421,15 +784,17 @@ __device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base
     }
     const uint32_t nch = (uint32_t)__popc(hdr.x >> 16);
     if (nch && lev + 1 < nlev && sp < sd) {
-      lo[sp * st] = hdr.y;
-      hi[sp * st] = hdr.y + nch;
+      // the children's slot -> their dense index at level lev + 1
+      const uint32_t c0 = pex[(lev + 1) * 64 + (hdr.y >> log2cap)] + (hdr.y & ((1u << log2cap) - 1u));
+      lo[sp * st] = c0;
+      hi[sp * st] = c0 + nch;
       sp++;
       // the children's records (contiguous, slot order) are fetched now, all
       // at once: the walk's dependent chain becomes the tree's depth, not
       // its size (the loads' values are consumed only at the end)
-      const char* c0 = p.lv_rec + (size_t)(base[lev + 1] + hdr.y) * p.lv_rec_bytes;
-      pf += *reinterpret_cast<const uint32_t*>(c0) +
-            *reinterpret_cast<const uint32_t*>(c0 + (size_t)(nch - 1) * p.lv_rec_bytes);
+      const char* r0 = p.lv_rec + (size_t)(base[lev + 1] + c0) * p.lv_rec_bytes;
+      pf += *reinterpret_cast<const uint32_t*>(r0) +
+            *reinterpret_cast<const uint32_t*>(r0 + (size_t)(nch - 1) * p.lv_rec_bytes);
     }
     // next: the last unvisited child of the deepest pending range (LIFO pop)
     while (sp > 0 && hi[(sp - 1) * st] == lo[(sp - 1) * st]) sp--;
@@ -442,36 +807,17 @@ __device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base
   return sum;
 }
 
-// Block 0 also adds the batch's level statistics to lv_acc (rtx_level_stats):
-// every level launch of the batch has ended.
-__device__ __forceinline__ void lv_bases(const KParams& p, int nlev, uint32_t* base) {
-  if (threadIdx.x == 0) {
-    uint32_t b = 0;
-    for (int d = 0; d <= nlev && d <= LV_MAXL; d++) {
-      base[d] = b;
-      b += lv_count(p, d);
-    }
-  }
-  if (blockIdx.x == 0 && p.lv_acc) {
-    const int t = (int)threadIdx.x;
-    if (t == 0) p.lv_acc[0] += p.lv_ctl->redo_n;
-    if (t == 1) p.lv_acc[1] += p.lv_ctl->dropped;
-    if (t < LV_MAXL + 1) p.lv_acc[2 + t] += p.lv_ctl->count[t];
-  }
-  __syncthreads();
-}
-
 // One camera sample's colour and first raise: its tree, or the lanes engine's
 // record when the sample overflowed the level buffers.
-__device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, int item, int nlev, uint32_t* lo,
-                                        uint32_t* hi, int st, int sd, uint32_t& e) {
+__device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, const uint32_t* pex, int item,
+                                        int nlev, uint32_t* lo, uint32_t* hi, int st, int sd, uint32_t& e) {
   const int r = p.lv_redo_of[item];
   if (r >= 0) {
     const double* q = p.lv_redo_smp + (size_t)r * 4;
     e = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
     return v3(q[0], q[1], q[2]);
   }
-  return lv_tree_sum(p, base, item, nlev, lo, hi, st, sd, e);
+  return lv_tree_sum(p, base, pex, item, nlev, lo, hi, st, sd, e);
 }
 
 // Camera#render_at's reduction (camera.rb:70-99) of pass 0: one 256-thread
@@ -480,17 +826,19 @@ __device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, 
 // neighbours), park colour and raise in LDS, then 64 threads do the pixels:
 // mean in sample order, the variance test, then the pixel or (max_sample_times
 // > pre) an extra-list entry with the pre mean parked in the output.
-// Dynamic LDS: SD * 2 words of walk stack per thread, then 64 * pre samples.
+// Dynamic LDS: nlev * 64 slice offsets, SD * 2 words of walk stack per thread,
+// then 64 * pre samples.
 template <int SD>
 __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
   __shared__ uint32_t base[LV_MAXL + 1];
   extern __shared__ uint32_t lds_fin[];
-  lv_bases(p, nlev, base);
+  uint32_t* pex = lds_fin;
+  lv_layout(p, nlev, base, pex);
   const int pre = p.pre;
   const int slot = blockIdx.x;                 // tile of the batch
-  uint32_t* lo = lds_fin + threadIdx.x;
+  uint32_t* lo = lds_fin + nlev * 64 + threadIdx.x;
   uint32_t* hi = lo + SD * 256;
-  double* scol = reinterpret_cast<double*>(lds_fin + 2 * SD * 256);   // 64 * pre * 3
+  double* scol = reinterpret_cast<double*>(lds_fin + nlev * 64 + (SD > 16 ? 0 : 2 * SD * 256));   // 64 * pre * 3
   uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
   uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];  // deep trees: private stack
   const int n_items = 64 * pre;
@@ -499,8 +847,8 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
     const ItemPos ip = decode_item(p, item0 + it);
     if (!ip.valid) continue;
     uint32_t e = 0;
-    const V3 c = SD > 16 ? lv_sample(p, base, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
-                         : lv_sample(p, base, item0 + it, nlev, lo, hi, 256, SD, e);
+    const V3 c = SD > 16 ? lv_sample(p, base, pex, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
+                         : lv_sample(p, base, pex, item0 + it, nlev, lo, hi, 256, SD, e);
     scol[3 * it] = c.x;
     scol[3 * it + 1] = c.y;
     scol[3 * it + 2] = c.z;
@@ -559,8 +907,9 @@ template <int SD>
 __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev) {
   __shared__ uint32_t base[LV_MAXL + 1];
   extern __shared__ uint32_t lds_fin[];
-  lv_bases(p, nlev, base);
-  uint32_t* lo = lds_fin + threadIdx.x;
+  uint32_t* pex = lds_fin;
+  lv_layout(p, nlev, base, pex);
+  uint32_t* lo = lds_fin + nlev * 64 + threadIdx.x;
   uint32_t* hi = lo + SD * 256;
   uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];
   const int t = blockIdx.x * 256 + (int)threadIdx.x;
@@ -579,8 +928,8 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
   for (int j = 0; j < n_extra; j++) {
     uint32_t e = 0;
     const int item = t * n_extra + j;
-    cv = vadd(cv, SD > 16 ? lv_sample(p, base, item, nlev, lo_p, hi_p, 1, LV_MAXL, e)
-                          : lv_sample(p, base, item, nlev, lo, hi, 256, SD, e));
+    cv = vadd(cv, SD > 16 ? lv_sample(p, base, pex, item, nlev, lo_p, hi_p, 1, LV_MAXL, e)
+                          : lv_sample(p, base, pex, item, nlev, lo, hi, 256, SD, e));
     if (!err) err = e;
   }
   const V3 r = vdiv(vadd(vsc(avg, (double)pre), cv), (double)p.max_samples);
@@ -590,30 +939,40 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
   if (err) record_error(p.err, err, px_key(x, y, cam.height));
 }
 
-// Per batch: the control block, count[0] = the batch's level-0 items (pass 1:
-// from the device-side extra count), the lanes engine's work counter (the
-// re-render launch); the call's first batch also the extra-list count and the
-// level statistics.  (Every level-0 lane sets its item's redo slot to -1.)
-__global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int first) {
+// Per batch: the control block (count0 = the batch's level-0 items, pass 1:
+// from the device-side extra count; the slice counters of levels 1..nlev),
+// the lanes engine's work counter (the re-render launch); the call's first
+// batch also the extra-list count and the level statistics.  (Every level-0
+// lane sets its item's redo slot to -1.)  Grid-stride over the words.
+__global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int first, int nlev) {
   const int t = blockIdx.x * 256 + (int)threadIdx.x;
-  if (t == 0) *p.work = 0;
+  const int nt = gridDim.x * 256;
+  if (t == 0) {
+    *p.work = 0;
+    uint32_t v;
+    if (p.lv_pass == 0) {
+      v = (uint32_t)n0_max;
+    } else {
+      const int left = *p.extra_count - p.lv_e0;
+      const int ent = left < 0 ? 0 : (left < p.lv_entries ? left : p.lv_entries);
+      v = (uint32_t)(ent * (p.max_samples - p.pre));
+    }
+    p.lv_ctl->count0 = v;
+    p.lv_ctl->redo_n = 0;
+    p.lv_ctl->dropped = 0;
+  }
   if (first) {
     if (t == 0) *p.extra_count = 0;
     if (p.lv_acc && t < LV_MAXL + 3) p.lv_acc[t] = 0;
   }
-  if (t < 2 * (LV_MAXL + 1) + 2) {
-    uint32_t v = 0;
-    if (t == 0) {
-      if (p.lv_pass == 0) {
-        v = (uint32_t)n0_max;
-      } else {
-        const int left = *p.extra_count - p.lv_e0;
-        const int ent = left < 0 ? 0 : (left < p.lv_entries ? left : p.lv_entries);
-        v = (uint32_t)(ent * (p.max_samples - p.pre));
-      }
-    }
-    reinterpret_cast<uint32_t*>(p.lv_ctl)[t] = v;
+  const int words = (nlev + 1 < LV_MAXL + 1 ? nlev + 1 : LV_MAXL + 1) * LV_SLICES * 32;
+  for (int w = t; w < words; w += nt) {
+    (&p.lv_ctl->sc[0][0])[w] = 0;
+    (&p.lv_ctl->sh[0][0])[w] = 0;
   }
+  const int cwords = (nlev < LV_MAXL + 1 ? nlev : LV_MAXL + 1) * LV_CLAIMS * 32;
+  for (int w = t; w < cwords; w += nt)
+    for (int k = 0; k < 3; k++) (&p.lv_ctl->claim[k][0][0])[w] = 0;
 }
 
 // Diagnostic builds: this unit's stamps (k_level), added by rtxdbg_read_stamps.
@@ -627,28 +986,23 @@ int read_level_stamps(unsigned long long* out, int reset) {
 }
 
 // ----------------------------------------------------------------- bounce-level launchers
-template <int SPH>
-static hipError_t launch_level(const KParams& p, int level, long cap_items, hipStream_t s, KernelEvents* kev) {
-  constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
-  KParams q = p;
-  q.stk_slots_max = 0;                         // no ray stack in this engine
-  const size_t lds = lds_layout(q, SPH, BS);
-  auto kern = k_level<SPH, BS>;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  int dev = 0, cus = 0, per_cu = 0;
+static hipError_t cus_and_fit(const void* kern, int bs, size_t lds, int& cus, int& per_cu) {
+  int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BS, lds);
-  if (e != hipSuccess) return e;
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, bs, lds);
   if (per_cu < 1) per_cu = 1;
-  long blocks = std::min<long>((cap_items + BS - 1) / BS, (long)cus * per_cu);
+  return e;
+}
+
+template <typename K>
+static hipError_t launch_timed(K kern, long blocks, int bs, size_t lds, hipStream_t s, KernelEvents* kev,
+                               const KParams& q, int level) {
   if (blocks < 1) blocks = 1;
   const bool ev = kev && kev->n < kev->max;
   if (ev) (void)hipEventRecord(kev->ev[2 * kev->n], s);
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BS), lds, s, q, level);
-  e = hipGetLastError();
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bs), lds, s, q, level);
+  const hipError_t e = hipGetLastError();
   if (ev) {
     (void)hipEventRecord(kev->ev[2 * kev->n + 1], s);
     kev->n++;
@@ -656,22 +1010,69 @@ static hipError_t launch_level(const KParams& p, int level, long cap_items, hipS
   return e;
 }
 
-static hipError_t launch_level_mode(const KParams& p, int mode, int level, long cap, hipStream_t s,
+// kind: 0 k_level (fused), 1 k_lv_trace, 2 k_lv_shadow.  Persistent: as many
+// workgroups as fit at once, never more than cap_items need.
+template <int SPH, int BS>
+static hipError_t launch_level_bs(const KParams& p, int kind, int level, long cap_items, hipStream_t s,
+                                  KernelEvents* kev) {
+  KParams q = p;
+  q.stk_slots_max = 0;                         // no ray stack in this engine
+  const size_t lds = lds_layout(q, SPH, BS);
+  auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  int cus = 0, per_cu = 0;
+  const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(kern), BS, lds, cus, per_cu);
+  if (e != hipSuccess) return e;
+  return launch_timed(kern, std::min<long>((cap_items + BS - 1) / BS, (long)cus * per_cu), BS, lds, s, kev, q, level);
+}
+
+// The fused kernel runs the engine's block sizes (BS_LIN / BS_BVH, 2 waves per
+// SIMD).  The split walk kernels (3 waves per SIMD) take 256-thread blocks
+// when three of them fit a CU's LDS, else the hierarchy's 512.
+#ifndef RTX_LV_FUSED_BS
+#define RTX_LV_FUSED_BS 0                  // k_level's block size (0: BS_LIN / BS_BVH)
+#endif
+template <int SPH>
+static hipError_t launch_level(const KParams& p, int kind, int level, long cap_items, hipStream_t s,
+                               KernelEvents* kev) {
+  constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL;
+  constexpr int FBS = RTX_LV_FUSED_BS ? RTX_LV_FUSED_BS : (BVH ? BS_BVH : BS_LIN);
+  if (kind == 0) return launch_level_bs<SPH, FBS>(p, kind, level, cap_items, s, kev);
+  if (BVH) {
+    KParams q = p;
+    q.stk_slots_max = 0;
+    if (3 * lds_layout(q, SPH, 256) > LDS_TOTAL_BYTES)
+      return launch_level_bs<SPH, BS_BVH>(p, kind, level, cap_items, s, kev);
+  }
+  return launch_level_bs<SPH, 256>(p, kind, level, cap_items, s, kev);
+}
+
+static hipError_t launch_level_mode(const KParams& p, int mode, int kind, int level, long cap, hipStream_t s,
                                     KernelEvents* kev) {
   switch (mode) {
-    case SPH_LIN_LDS: return launch_level<SPH_LIN_LDS>(p, level, cap, s, kev);
-    case SPH_LIN_SCALAR: return launch_level<SPH_LIN_SCALAR>(p, level, cap, s, kev);
-    case SPH_BVH_LDS: return launch_level<SPH_BVH_LDS>(p, level, cap, s, kev);
-    case SPH_BVH_GLOBAL: return launch_level<SPH_BVH_GLOBAL>(p, level, cap, s, kev);
+    case SPH_LIN_LDS: return launch_level<SPH_LIN_LDS>(p, kind, level, cap, s, kev);
+    case SPH_LIN_SCALAR: return launch_level<SPH_LIN_SCALAR>(p, kind, level, cap, s, kev);
+    case SPH_BVH_LDS: return launch_level<SPH_BVH_LDS>(p, kind, level, cap, s, kev);
+    case SPH_BVH_GLOBAL: return launch_level<SPH_BVH_GLOBAL>(p, kind, level, cap, s, kev);
   }
   return hipErrorInvalidValue;
 }
 
+static hipError_t launch_shade(const KParams& p, int level, long cap_items, hipStream_t s, KernelEvents* kev) {
+  int cus = 0, per_cu = 0;
+  const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(k_lv_shade), BS_SHADE, 0, cus, per_cu);
+  if (e != hipSuccess) return e;
+  return launch_timed(k_lv_shade, std::min<long>((cap_items + BS_SHADE - 1) / BS_SHADE, (long)cus * per_cu), BS_SHADE,
+                      0, s, kev, p, level);
+}
+
 template <int SD>
 static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStream_t s) {
-  const size_t stack = SD > 16 ? 0 : (size_t)SD * 2 * 256 * 4;
+  const size_t stack = (size_t)nlev * 64 * 4 + (SD > 16 ? 0 : (size_t)SD * 2 * 256 * 4);
   if (q.lv_pass == 0) {                        // n = tiles of the batch
-    const size_t lds = stack + (size_t)64 * q.pre * 28;
+    const size_t lds = ((stack + 7) & ~(size_t)7) + (size_t)64 * q.pre * 28;
     hipLaunchKernelGGL(k_tree_finalize<SD>, dim3((unsigned)n), dim3(256), lds, s, q, nlev);
   } else {                                     // n = extra-list entries of the batch
     hipLaunchKernelGGL(k_tree_finalize_extra<SD>, dim3((unsigned)((n + 255) / 256)), dim3(256), stack, s, q, nlev);
@@ -686,16 +1087,30 @@ static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t
 }
 
 // One batch: reset, the levels, the lanes-engine re-render of overflowed
-// samples (exits at once when there are none), the tree reduction.
+// samples (exits at once when there are none), the tree reduction.  A level's
+// launches size their grids for its capacity (level 0: the batch's items;
+// deeper levels: LV_SLICES full slices).
 static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_max, int fin_threads, hipStream_t s,
                               KernelEvents* kev, bool first) {
-  hipLaunchKernelGGL(k_level_begin, dim3(1), dim3(256), 0, s, q, n0_max, first ? 1 : 0);
+  const int words = std::min(nlev + 1, LV_MAXL + 1) * LV_SLICES * 32;
+  hipLaunchKernelGGL(k_level_begin, dim3((unsigned)std::min(64, (words + 255) / 256)), dim3(256), 0, s, q, n0_max,
+                     first ? 1 : 0, nlev);
   hipError_t e = hipGetLastError();
-  for (int d = 0; d < nlev && e == hipSuccess; d++)
-    e = launch_level_mode(q, mode, d, d == 0 ? (long)n0_max : (long)q.lv_scap, s, kev);
+  const long scap = (long)LV_SLICES << q.lv_slice_log2, hcap = (long)LV_SLICES << q.lv_hslice_log2;
+  for (int d = 0; d < nlev && e == hipSuccess; d++) {
+    const long cap = d == 0 ? (long)n0_max : scap;
+    if (!q.lv_split) {
+      e = launch_level_mode(q, mode, 0, d, cap, s, kev);
+      continue;
+    }
+    const long hits = std::min(cap, hcap);
+    e = launch_level_mode(q, mode, 1, d, cap, s, kev);
+    if (e == hipSuccess && q.scene.n_light > 0)
+      e = launch_level_mode(q, mode, 2, d, hits * q.scene.n_light, s, kev);
+    if (e == hipSuccess) e = launch_shade(q, d, hits, s, kev);
+  }
   if (e == hipSuccess) e = launch_redo(q, mode, maxs, n0_max, s);
   if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
-
   return e;
 }
 

@@ -50,13 +50,11 @@ F64_FLOP = {"SQ_INSTS_VALU_FMA_F64": 2, "SQ_INSTS_VALU_ADD_F64": 1, "SQ_INSTS_VA
 def kernel_source_sha():
     """Identity of the kernel build: sha256 over the device sources and build flags."""
     import hashlib
-    import os
-    here = os.path.dirname(os.path.abspath(__file__))
     h = hashlib.sha256()
-    for f in ("rtx_kernels.hip", "rtx_vec3.h", "rtx_scene.h", "rtx_launch.h", "rtx_capi.cpp"):
-        with open(os.path.join(here, "csrc", f), "rb") as fh:
-            h.update(fh.read())
     from . import _build
+    for f in _build.SOURCES + _build.HEADERS:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
     h.update(" ".join(_build.FLAGS).encode())
     return h.hexdigest()[:16]
 

@@ -173,3 +173,74 @@ def test_levels_color_gt1_error_reported(gpu, tmp_path):
         assert e.value.kind == "color_gt1" and "color greater than 1" in str(e.value)
         msgs.append(str(e.value))
     assert msgs[0] == msgs[1]                             # same first erring pixel (render_sync order)
+
+
+# ---- split phases (option lv_split = 1: trace / shadow / shade launches per level)
+@pytest.mark.parametrize("world,camera,ov", SCENES_SMALL)
+def test_split_phases_bit_identical(gpu, world, camera, ov):
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=3)
+    r = _renderer(sd, cd, 1, lv_split=1)
+    assert _same(r.render(seed=3), lanes)
+    st = r.level_stats()
+    assert st["redo"] == 0 and st["dropped"] == 0
+
+
+@pytest.mark.parametrize("opts", [
+    dict(lv_batch=512),
+    dict(lv_stage_pct=5, lv_floor=0),
+    dict(lv_rec_pct=101, lv_floor=0),
+    dict(lv_batch=1000, lv_stage_pct=20, lv_rec_pct=150, lv_floor=0),
+])
+def test_split_phases_batches_and_overflow(gpu, opts):
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
+    lanes = _renderer(sd, cd, 0).render(seed=5)
+    r = _renderer(sd, cd, 1, lv_split=1, **opts)
+    assert _same(r.render(seed=5), lanes)
+    if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
+        assert r.level_stats()["redo"] > 0
+
+
+def test_split_phases_extras_c4_and_errors(gpu, tmp_path):
+    import sys
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import RtxError
+    sd, cd = _scene("mix_world.yml", "mix_camera.yml", width=64, height=36, pre_sample_times=2,
+                    max_sample_times=6, variant_threshold=1e-4)
+    lanes = _renderer(sd, cd, 0).render(seed=9)
+    for opts in (dict(), dict(lv_batch=300)):
+        assert _same(_renderer(sd, cd, 1, lv_split=1, **opts).render(seed=9), lanes), opts
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_scenes
+    make_scenes.ensure_c4()
+    sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=64, height=36)
+    assert _same(_renderer(sd, cd, 1, lv_split=1).render(seed=2), _renderer(sd, cd, 0).render(seed=2))
+    src = open(os.path.join(SCENES, "c1_world.yml")).read()
+    src = src.replace("diffuse_rate:           [0.5, 0.5, 0.5]", "diffuse_rate:           [0.99, 0.99, 0.99]")
+    src = src.replace("ambient:                [0.05, 0.05, 0.05]", "ambient:                [0.3, 0.3, 0.3]", 1)
+    p = tmp_path / "bright.yml"
+    p.write_text(src)
+    sd, cd = config.load_scene(str(p), os.path.join(SCENES, "c1_camera.yml"), camera_overrides=dict(width=24, height=14))
+    msgs = []
+    for engine, opts in ((0, {}), (1, dict(lv_split=1))):
+        with pytest.raises(RtxError) as e:
+            _renderer(sd, cd, engine, **opts).render()
+        msgs.append(str(e.value))
+    assert msgs[0] == msgs[1]
+
+
+def test_split_phases_c2_full_frame(gpu):
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml")
+    fused = _renderer(sd, cd, 1, lv_split=0).render()
+    r = _renderer(sd, cd, 1, lv_split=1)
+    assert _same(r.render(), fused)
+    assert r.level_stats()["redo"] == 0
+
+
+@pytest.mark.parametrize("static", [0, 37, 100])
+def test_chunk_schedule_changes_no_bit(gpu, static):
+    """Static / sharded-claim chunk schedules (option lv_static) reorder work only."""
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=200, height=96)
+    lanes = _renderer(sd, cd, 0).render(seed=4)
+    for split in (0, 1):
+        assert _same(_renderer(sd, cd, 1, lv_static=static, lv_split=split).render(seed=4), lanes), (static, split)

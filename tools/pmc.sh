@@ -5,10 +5,10 @@ set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O
-ARGS="$@"
+ARGS=("$@")
 run() {  # name counters...
   local n=$1; shift
-  timeout -k 5 -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace -d $O/pmc_$n -o $n --output-format csv -- python3 tools/timing.py $ARGS > $O/pmc_$n.log 2>&1
+  timeout -k 5 -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace -d $O/pmc_$n -o $n --output-format csv -- python3 tools/timing.py "${ARGS[@]}" > $O/pmc_$n.log 2>&1
 }
 run a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY && \
 run b SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_INT32 && \
