@@ -641,6 +641,7 @@ extern "C" int rtxdbg_read_stamps(unsigned long long* out, int reset) {   // dia
   unsigned long long lv[16];                     // k_level's phases (slots 0-7) from rtx_levels.hip
   if (read_level_stamps(lv, reset) != 0) return -1;
   for (int k = 0; k < 8; k++) out[k] += lv[k];
+  for (int k = 8; k < 11; k++) out[k] = lv[k];   // (k_level: lanes with a ray / a walk / a hit)
   return 0;
 }
 

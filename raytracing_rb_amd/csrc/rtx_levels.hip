@@ -416,6 +416,7 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
   const int slice = sched.wave_id() & (LV_SLICES - 1);
 
   unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
+  unsigned long long nA = 0, nE = 0, nS = 0;  // lanes with a ray, an EXTEND walk, a hit (per chunk, summed)
 #define RTX_LV_STAMP(k)  \
   if (RTX_STAMPS) {      \
     t1 = stamp();        \
@@ -468,6 +469,11 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     bool hin = true;
     if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
     const bool shade = ext && besti >= 0;
+    if (RTX_STAMPS) {
+      nA += __popcll(__ballot(active));
+      nE += __popcll(__ballot(ext));
+      nS += __popcll(__ballot(shade));
+    }
     RTX_LV_STAMP(1)
     V3 delta = hit, nrm = hit, nn = hit;
     double c = 0.0;
@@ -514,6 +520,9 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     for (int k = 0; k < 6; k++) atomicAdd(&rtx_stamps[k], tS[k]);
     atomicAdd(&rtx_stamps[6], nchunks);
     atomicAdd(&rtx_stamps[7], 1ull);
+    atomicAdd(&rtx_stamps[8], nA);
+    atomicAdd(&rtx_stamps[9], nE);
+    atomicAdd(&rtx_stamps[10], nS);
   }
 }
 

@@ -31,7 +31,10 @@ lib.rtxdbg_read_stamps(st, 1)
 v = list(st)
 tot = sum(v[:6])
 names = ["A claim/load/lens/highlight", "B EXTEND walk", "C hit_info/normal/cos", "D SHADOW walks + lights",
-         "E child mask + wave prefix + atomic", "F children/leaf/record stores"]
+         "E (unused)", "F mask, slot alloc, children, leaf, record"]
 print("waves %d  chunks %d  cycles/chunk %.0f" % (v[7], v[6], tot / max(1, v[6])))
 for n, x in zip(names, v[:6]):
     print("%-38s %5.1f%%  %8.0f cycles/chunk" % (n, 100.0 * x / tot, x / max(1, v[6])))
+ch = max(1, v[6])
+print("lanes per chunk: with a ray %.1f, EXTEND walk %.1f, hit (shading, SHADOW walks) %.1f" % (
+    v[8] / ch, v[9] / ch, v[10] / ch))
