@@ -274,7 +274,10 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          overflow them are re-rendered by the lanes engine, same bits), "lv_split" (bounce levels: 0 one fused
          launch per level, 1 three launches per level over dense queues: trace, shadow, shade; same bits; used up
          to 16 lights), "lv_static" (bounce levels: % of a level launch's 64-ray chunks scheduled statically, the
-         rest claimed from sharded counters; -1 [default] = 100 up to 512 spheres, else 50; same bits). */
+         rest claimed from sharded counters; -1 [default] = 100 up to 512 spheres, else 50; same bits),
+         "lv_compact" (bounce levels: 1 park the rays that hit something in a per-wave LDS ring and run the
+         shadow walks and shading on full waves, 0 off, -1 [default] = on whenever the rings fit the walk's
+         LDS; same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

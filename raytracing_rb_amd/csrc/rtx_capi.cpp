@@ -77,6 +77,7 @@ struct rtx_context {
   int64_t opt_lv_floor = 1 << 20;    // bounce levels: at least this many staging and 4x this many tree records
   int64_t opt_lv_split = 0;          // bounce levels: 1 = three phase launches per level (trace / shadow / shade)
   int64_t opt_lv_static = -1;        // bounce levels: % of a launch's chunks scheduled statically (-1 auto)
+  int64_t opt_lv_compact = -1;       // bounce levels: 1 = park hits in an LDS ring and shade full waves, -1 auto (when it fits)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
@@ -390,7 +391,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lds_stack", c->opt_lds_stack}, {"tile_order", c->opt_tile_order},   {"sphere_src", c->opt_sphere_src},
       {"kernel_events", c->opt_kernel_events}, {"lv_batch", c->opt_lv_batch},
       {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor},
-      {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}};
+      {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -462,6 +463,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_static")) {         // bounce levels: % of chunks scheduled statically, -1 auto
     if (value < -1 || value > 100) return fail(c, RTX_EINVAL, "lv_static must be in [-1, 100]");
     c->opt_lv_static = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_compact")) {        // bounce levels: hit compaction in k_level, -1 auto
+    if (value < -1 || value > 1) return fail(c, RTX_EINVAL, "lv_compact must be -1, 0 or 1");
+    c->opt_lv_compact = value;
     return RTX_OK;
   }
   if (!strcmp(key, "kernel_events")) {     // 1: HIP events around the ray-tree launches (rtx_kernel_time)
@@ -851,6 +857,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_hit = split ? (double*)q : nullptr;  q += sz_hit;
   p.lv_area = split ? (double*)q : nullptr; q += sz_area;
   p.lv_split = split ? 1 : 0;
+  p.lv_compact = (int32_t)c->opt_lv_compact;   // the launcher turns it off when the rings do not fit LDS
   // Static chunks cost no atomics; dynamic claims balance rays of very
   // different cost.  Auto: all static while the sphere records fit one walk
   // workgroup's LDS with room to spare (C2: 5.35 vs 5.9 ms at 50 %), half

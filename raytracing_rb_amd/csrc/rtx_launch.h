@@ -86,6 +86,8 @@ struct KParams {
   int32_t lv_static_pct;           // % of a level launch's chunks scheduled statically (the rest: sharded claims)
   double* lv_hit;                  // split: hit queue, LV_HIT_BYTES per hit, LV_SLICES << lv_hslice_log2 slots
   double* lv_area;                 // split: {1 - covers, raise} per (hit, light)
+  int32_t lv_compact;              // k_level: park hits in an LDS ring, shade full waves (-1 auto, 0 off, 1 on)
+  int32_t lds_ring;                // k_level (compacting): LDS byte offset of the per-wave hit rings
 };
 
 // Where the sphere walk reads its records:

@@ -315,46 +315,22 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
     if (nl == 0 && cd > 0 && !(vr(vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt))) < 0.0001))
       mask |= ((1u << pt) - 1u) << 2;       // every path-tracing child (same attenuation)
   }
-  // room in the next level: this wave's slice, wave prefix count + one atomic
+  // Room in the next level: this wave's slice, wave prefix count + one
+  // atomic.  The atomic is issued here and its value read only after the
+  // reflection / refraction rays and the leaf are computed, so its round trip
+  // overlaps that arithmetic instead of stalling the wave.
   const uint32_t log2cap = (uint32_t)p.lv_slice_log2, cap = 1u << log2cap;
-  const uint32_t off0 = lv_wave_alloc(lv_slice_ctr(p.lv_ctl->sc[level + 1], slice), __popc(mask));
-  const uint32_t child0 = ((uint32_t)slice << log2cap) + off0;   // slot of the first child (k_tree_finalize)
+  const int nch = __popc(mask);
+  const int incl = (int)wave_scan_incl((uint32_t)nch);
+  const int wtotal = __shfl(incl, 63);
+  uint32_t wraw = 0;
+  if (wtotal > 0 && __lane_id() == 0) wraw = atomicAdd(lv_slice_ctr(p.lv_ctl->sc[level + 1], slice), (uint32_t)wtotal);
+  Ray refl, refr;
+  bool has_refr = false;
   if (shade) {
-    double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
-    uint32_t off = off0;
-    auto put = [&](const Ray& r, V3 att, uint64_t path) {
-      if (off < cap) lv_store_ray(outs + (size_t)(((uint32_t)slice << log2cap) + off) * RAY_DOUBLES, r, att, path, root,
-                                  x, y, sample);
-      else {
-        lv_redo(p, root);
-        atomicAdd(&p.lv_ctl->dropped, 1u);
-      }
-      off++;
-    };
-    const Ray refl = reflection(cur.ray, nn, c, hit, delta, errS);
-    if (mask & 1u) put(refl, vmul(cur.att, v3p(m->refl_att)), cur.path * R + 1);
-    if (may_refract) {
-      Ray refr;
-      if (refraction(cur.ray, nn, c, hit, refl.d, rate, refr, errS) && (mask & 2u))
-        put(refr, vmul(cur.att, v3p(m->refr_att)), cur.path * R + 2);
-    }
-    if (nl == 0) {
-      // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
-      const V3 att = vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt));
-      const V3 left = vnorm(vertical_vector(nrm, errP), errP);
-      const V3 up = vcross(nn, left);
-      Ray r;
-      r.o = vadd(hit, delta);
-      for (int k = 0; k < pt; k++) {
-        const double theta = rand01(p.seed, x, y, sample, cur.path, 2 * k) * PI / 2.0;
-        const double phi = rand01(p.seed, x, y, sample, cur.path, 2 * k + 1) * PI * 2.0;
-        double sth, cth, sph, cph;
-        RTX_SINCOS(theta, &sth, &cth);
-        RTX_SINCOS(phi, &sph, &cph);
-        r.d = vadd(vsc(nn, sth), vsc(vadd(vsc(left, cph), vsc(up, sph)), cth));
-        if (mask >> (2 + k) & 1u) put(r, att, cur.path * R + 3 + (uint64_t)k);
-      }
-    } else {
+    refl = reflection(cur.ray, nn, c, hit, delta, errS);
+    if (may_refract) has_refr = refraction(cur.ray, nn, c, hit, refl.d, rate, refr, errS) && (mask & 2u);
+    if (nl != 0) {
       // WorldObject#local_lighting's colour (world_object.rb:51-74), texture filter
       lc = vdiv(lc, (double)nl);
       V3 color;
@@ -388,6 +364,40 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
       leafp[1] = leaf.y;
       leafp[2] = leaf.z;
       nleaf = 1;
+    }
+  }
+  const uint32_t off0 = (wtotal > 0 ? (uint32_t)__shfl((int)wraw, 0) : 0u) + (uint32_t)(incl - nch);
+  const uint32_t child0 = ((uint32_t)slice << log2cap) + off0;   // slot of the first child (k_tree_finalize)
+  if (shade) {
+    double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
+    uint32_t off = off0;
+    auto put = [&](const Ray& r, V3 att, uint64_t path) {
+      if (off < cap) lv_store_ray(outs + (size_t)(((uint32_t)slice << log2cap) + off) * RAY_DOUBLES, r, att, path, root,
+                                  x, y, sample);
+      else {
+        lv_redo(p, root);
+        atomicAdd(&p.lv_ctl->dropped, 1u);
+      }
+      off++;
+    };
+    if (mask & 1u) put(refl, vmul(cur.att, v3p(m->refl_att)), cur.path * R + 1);
+    if (has_refr) put(refr, vmul(cur.att, v3p(m->refr_att)), cur.path * R + 2);
+    if (nl == 0) {
+      // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
+      const V3 att = vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt));
+      const V3 left = vnorm(vertical_vector(nrm, errP), errP);
+      const V3 up = vcross(nn, left);
+      Ray r;
+      r.o = vadd(hit, delta);
+      for (int k = 0; k < pt; k++) {
+        const double theta = rand01(p.seed, x, y, sample, cur.path, 2 * k) * PI / 2.0;
+        const double phi = rand01(p.seed, x, y, sample, cur.path, 2 * k + 1) * PI * 2.0;
+        double sth, cth, sph, cph;
+        RTX_SINCOS(theta, &sth, &cth);
+        RTX_SINCOS(phi, &sph, &cph);
+        r.d = vadd(vsc(nn, sth), vsc(vadd(vsc(left, cph), vsc(up, sph)), cth));
+        if (mask >> (2 + k) & 1u) put(r, att, cur.path * R + 3 + (uint64_t)k);
+      }
     }
   }
   if (active) {
@@ -513,6 +523,226 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
     RTX_LV_STAMP(3)
     lv_finish(p, level, slice, shade, active, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec,
               nleaf, errA, errS, errL, errP);
+    RTX_LV_STAMP(5)
+  }
+#undef RTX_LV_STAMP
+  if (RTX_STAMPS && __lane_id() == 0) {
+    for (int k = 0; k < 6; k++) atomicAdd(&rtx_stamps[k], tS[k]);
+    atomicAdd(&rtx_stamps[6], nchunks);
+    atomicAdd(&rtx_stamps[7], 1ull);
+    atomicAdd(&rtx_stamps[8], nA);
+    atomicAdd(&rtx_stamps[9], nE);
+    atomicAdd(&rtx_stamps[10], nS);
+  }
+}
+
+// ----------------------------------------------------------------- hit compaction
+// Option lv_compact.  In k_level the shading half of a chunk
+// (intersect_parameters, the shadow walks of local_lights, local_lighting and
+// the children) runs on the lanes whose ray hit something, ~64 % of them on
+// C2.  k_level_c splits every chunk at that point: each wave first runs the
+// highlights and the nearest-hit walk for 64 rays, writes the records of the
+// rays that stop there, and parks the hits in its own LDS ring (a ballot rank
+// gives each hit its slot); whenever 64 hits are parked it pops them and runs
+// the shading half on a full wave.  Every ray sees the same operations on the
+// same values as in k_level, so the trees, hence the frames, are bit-identical.
+//
+// Ring: LV_RING slots per wave, structure of arrays (field f of slot k at
+// (f * LV_RING + k) * 8 bytes: consecutive lanes hit consecutive banks); at
+// most 63 hits stay parked between chunks, so 63 + 64 < LV_RING never overwrite
+// an unread slot.  A parked hit: the hit point, the ray's origin and
+// direction, {dense index, queue slot}, {object | :in << 31, raises}.  The
+// rest of the ray (attenuation, path, RNG key) is reloaded from the level's
+// queue (level 0: the camera sample's item).
+constexpr int LV_RING = 128;
+constexpr int LV_RING_FIELDS = 11;
+constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
+
+template <int SPH, int BS>
+__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
+  const SceneDev& S = p.scene;
+  extern __shared__ float4 lds_sph[];
+  char* lds = reinterpret_cast<char*>(lds_sph);
+  LvQueue in;
+  lv_in_queue(p, level, in);
+  if (in.chunks == 0) return;                 // uniform: before any barrier
+  lv_stage_scene<SPH, BS>(p, lds_sph);
+  const uint32_t base = lv_base(p, level);
+  const int depth = p.cam->depth - level;
+  LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
+  const int slice = sched.wave_id() & (LV_SLICES - 1);
+  const int lane = (int)__lane_id();
+  double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * LV_RING_WAVE_BYTES);
+  uint32_t head = 0, pend = 0;                // wave-uniform: first parked slot, parked hits
+  bool got = true;
+
+  unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
+  unsigned long long nA = 0, nE = 0, nS = 0;
+#define RTX_LV_STAMP(k)  \
+  if (RTX_STAMPS) {      \
+    t1 = stamp();        \
+    tS[k] += t1 - t0;    \
+    t0 = t1;             \
+  }
+  while (true) {
+    uint32_t chunk = 0;
+    if (got) got = sched.claim(in.chunks, chunk);   // (never again once exhausted)
+    if (RTX_STAMPS) t0 = stamp();
+    if (got) {
+      if (RTX_STAMPS) nchunks++;
+      // ---- first half: the ray, rt_map's cutoff, highlights, World#intersect
+      uint32_t s, off, i;
+      bool active = in.item(chunk, s, off, i);
+      const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
+      Item cur;
+      int root = 0, x = 0, y = 0, sample = 0;
+      bool alive = false;
+      if (active) {
+        bool valid;
+        lv_ray(p, level, slot, cur, root, x, y, sample, valid);
+        if (level == 0) p.lv_redo_of[i] = -1;
+        active = valid;
+        alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // ray_tracer.rb:52
+        if (active && base + i >= p.lv_lcap) {
+          lv_redo(p, root);
+          active = alive = false;
+        }
+      }
+      char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
+      double* leafp = reinterpret_cast<double*>(rec + 8);
+      uint32_t errA = 0, errL = 0;
+      int nleaf = 0;
+      bool fired = false;
+      if (alive)
+        fired = highlight_leaves(S, cur, [&](V3 c) {
+          leafp[3 * nleaf] = c.x;
+          leafp[3 * nleaf + 1] = c.y;
+          leafp[3 * nleaf + 2] = c.z;
+          nleaf++;
+        }, errA);
+      RTX_LV_STAMP(0)
+      const bool ext = alive && !fired;
+      double best = S.max_distance, total = 0.0;
+      int besti = -1;
+      V3 hit = v3(0.0, 0.0, 0.0);
+      bool hin = true;
+      if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
+      const bool shade = ext && besti >= 0;
+      if (RTX_STAMPS) {
+        nA += __popcll(__ballot(active));
+        nE += __popcll(__ballot(ext));
+        nS += __popcll(__ballot(shade));
+      }
+      RTX_LV_STAMP(1)
+      if (active && !shade) {                 // the ray ends here: its record (k_level's, no children)
+        const uint32_t err = errA ? errA : errL;
+        *reinterpret_cast<uint2*>(rec) = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8), 0u);
+      }
+      // park the hits: slot head + pend + (rank among the wave's hits)
+      const uint64_t hm = __ballot(shade);
+      if (shade) {
+        const uint32_t k = (head + pend + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))) & (LV_RING - 1);
+        double* r = ring + k;
+        r[0 * LV_RING] = hit.x;
+        r[1 * LV_RING] = hit.y;
+        r[2 * LV_RING] = hit.z;
+        r[3 * LV_RING] = cur.ray.o.x;
+        r[4 * LV_RING] = cur.ray.o.y;
+        r[5 * LV_RING] = cur.ray.o.z;
+        r[6 * LV_RING] = cur.ray.d.x;
+        r[7 * LV_RING] = cur.ray.d.y;
+        r[8 * LV_RING] = cur.ray.d.z;
+        r[9 * LV_RING] = __builtin_bit_cast(double, (uint64_t)i | (uint64_t)slot << 32);
+        r[10 * LV_RING] = __builtin_bit_cast(
+            double, (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) | (uint64_t)((errA & 0xffu) | (errL & 0xffu) << 8) << 32);
+      }
+      pend += (uint32_t)__popcll(hm);
+      RTX_LV_STAMP(4)
+    }
+    if (pend < 64 && (got || pend == 0)) {
+      if (!got) break;                        // no chunk left and nothing parked
+      continue;                               // not a full wave of hits yet
+    }
+    // ---- second half on up to 64 parked hits (64, except the final flush)
+    const uint32_t take = pend < 64 ? pend : 64u;
+    const bool shade = (uint32_t)lane < take;
+    Item cur;
+    V3 hit = v3(0.0, 0.0, 0.0);
+    uint32_t i = 0, errA = 0, errL = 0, errS = 0, errP = 0;
+    int besti = 0, root = 0, x = 0, y = 0, sample = 0;
+    bool hin = true;
+    if (shade) {
+      const double* r = ring + ((head + (uint32_t)lane) & (LV_RING - 1));
+      hit = v3(r[0 * LV_RING], r[1 * LV_RING], r[2 * LV_RING]);
+      cur.ray.o = v3(r[3 * LV_RING], r[4 * LV_RING], r[5 * LV_RING]);
+      cur.ray.d = v3(r[6 * LV_RING], r[7 * LV_RING], r[8 * LV_RING]);
+      const uint64_t is = __builtin_bit_cast(uint64_t, r[9 * LV_RING]);
+      const uint64_t be = __builtin_bit_cast(uint64_t, r[10 * LV_RING]);
+      i = (uint32_t)is;
+      besti = (int)((uint32_t)be & 0x7fffffffu);
+      hin = ((uint32_t)be >> 31) != 0;
+      errA = (uint32_t)(be >> 32) & 0xffu;
+      errL = (uint32_t)(be >> 40) & 0xffu;
+      if (level == 0) {                       // the camera sample: item i (lv_ray)
+        root = (int)i;
+        const ItemPos ip = decode_item(p, root);
+        x = p.x0 + ip.px;
+        y = row_to_y(p, ip.row);
+        sample = ip.sample;
+        cur.att = v3(1.0, 1.0, 1.0);
+        cur.path = 1;
+      } else {                                // the staged child at its queue slot (lv_ray)
+        const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)(is >> 32) * RAY_DOUBLES);
+        const double2 d = q[3], e = q[4], f = q[5];
+        cur.att = v3(d.x, d.y, e.x);
+        cur.path = __builtin_bit_cast(uint64_t, e.y);
+        const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
+        root = (int)(uint32_t)rs;
+        sample = (int)(rs >> 32);
+        x = (int)(uint32_t)xy;
+        y = (int)(xy >> 32);
+      }
+    }
+    head = (head + take) & (LV_RING - 1);
+    pend -= take;
+    char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
+    RTX_LV_STAMP(4)
+    V3 delta = hit, nrm = hit, nn = hit;
+    double c = 0.0;
+    if (shade) {
+      hit_info(S, besti, cur.ray, hit, delta, nrm, hin);
+      nn = vnorm(nrm, errS);                  // n.normalize (world_object.rb:123)
+      c = vcos(cur.ray.d, nrm, errS);         // ray.front.cos(-n): same bits as cos(n)
+    }
+    const V3 qo = vadd(hit, delta);           // the shadow rays' target point (world.rb:76)
+    RTX_LV_STAMP(2)
+    V3 lc = v3(0.0, 0.0, 0.0);
+    int nl = 0;
+    for (int li = 0; li < S.n_light; li++) {  // World#local_lights + local_lighting's light loop
+      if (!shade) continue;
+      const LightDev& L = S.light[li];
+      const V3 qL = v3p(L.pos);
+      double tot = 1.0;
+      double b2 = 0.0;
+      int bi2 = -1;
+      V3 h2 = qo;
+      bool in2 = true;
+      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL);
+      const double area = tot > 0 ? tot : 0.0;
+      if (area > 0) {
+        nl++;
+        const double pw = S.sse_is_two ? area * area : rx_pow(area, S.sse);
+        const V3 lcol = vsc(v3p(L.color), pw / (double)S.n_light);
+        const V3 ll = vnorm(vsub(v3p(L.pos), hit), errP);
+        double ldn = vdot(ll, nn);
+        if (ldn > 1) ldn = 1.0;
+        else if (ldn < 0) ldn = 0.0;
+        lc = vadd(lc, vsc(lcol, ldn));
+      }
+    }
+    RTX_LV_STAMP(3)
+    lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec, 0,
+              errA, errS, errL, errP);
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
@@ -1026,8 +1256,18 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
                                   KernelEvents* kev) {
   KParams q = p;
   q.stk_slots_max = 0;                         // no ray stack in this engine
-  const size_t lds = lds_layout(q, SPH, BS);
+  size_t lds = lds_layout(q, SPH, BS);
   auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
+  if (kind == 0 && q.lv_compact != 0) {        // hit compaction when the rings fit next to the walk's LDS
+    constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL;
+    const size_t ring = (lds + 15) & ~(size_t)15;
+    const size_t need = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES;
+    if (need <= (BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES)) {
+      q.lds_ring = (int32_t)ring;
+      lds = need;
+      kern = k_level_c<SPH, BS>;
+    }
+  }
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
@@ -1090,6 +1330,9 @@ static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStrea
 }
 
 static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t s) {
+  // a walk keeps one pending child range per level below the root: nlev - 1
+  // entries; the smaller stack lets 8 blocks share a CU (C2, depth 5) instead of 6
+  if (nlev <= 5) return launch_finalize_sd<4>(q, nlev, n, s);
   if (nlev <= 8) return launch_finalize_sd<8>(q, nlev, n, s);
   if (nlev <= 16) return launch_finalize_sd<16>(q, nlev, n, s);
   return launch_finalize_sd<64>(q, nlev, n, s);

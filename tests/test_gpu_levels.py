@@ -244,3 +244,63 @@ def test_chunk_schedule_changes_no_bit(gpu, static):
     lanes = _renderer(sd, cd, 0).render(seed=4)
     for split in (0, 1):
         assert _same(_renderer(sd, cd, 1, lv_static=static, lv_split=split).render(seed=4), lanes), (static, split)
+
+
+# ---- hit compaction (option lv_compact: k_level_c parks hits in an LDS ring, shades full waves)
+@pytest.mark.parametrize("world,camera,ov", SCENES_SMALL)
+def test_compaction_bit_identical(gpu, world, camera, ov):
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=3)
+    for compact in (0, 1):
+        r = _renderer(sd, cd, 1, lv_compact=compact)
+        assert _same(r.render(seed=3), lanes), compact
+        st = r.level_stats()
+        assert st["redo"] == 0 and st["dropped"] == 0
+
+
+@pytest.mark.parametrize("opts", [
+    dict(lv_batch=512),
+    dict(lv_stage_pct=5, lv_floor=0),                    # children past a slice: re-rendered whole
+    dict(lv_rec_pct=101, lv_floor=0),                    # records past the arena
+    dict(lv_static=37),                                  # sharded claims: parked hits cross chunk claims
+])
+def test_compaction_batches_overflow_schedule(gpu, opts):
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
+    lanes = _renderer(sd, cd, 0).render(seed=5)
+    r = _renderer(sd, cd, 1, lv_compact=1, **opts)
+    assert _same(r.render(seed=5), lanes)
+    if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
+        assert r.level_stats()["redo"] > 0
+
+
+def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
+    """Raise sites keep their order through the ring; C4's hierarchy leaves no
+    LDS for the rings, so the option falls back to k_level (same bits)."""
+    import sys
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import RtxError
+    src = open(os.path.join(SCENES, "c1_world.yml")).read()
+    src = src.replace("diffuse_rate:           [0.5, 0.5, 0.5]", "diffuse_rate:           [0.99, 0.99, 0.99]")
+    src = src.replace("ambient:                [0.05, 0.05, 0.05]", "ambient:                [0.3, 0.3, 0.3]", 1)
+    p = tmp_path / "bright.yml"
+    p.write_text(src)
+    sd, cd = config.load_scene(str(p), os.path.join(SCENES, "c1_camera.yml"), camera_overrides=dict(width=24, height=14))
+    msgs = []
+    for engine, opts in ((0, {}), (1, dict(lv_compact=1)), (1, dict(lv_compact=0))):
+        with pytest.raises(RtxError) as e:
+            _renderer(sd, cd, engine, **opts).render()
+        msgs.append(str(e.value))
+    assert msgs[0] == msgs[1] == msgs[2]
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_scenes
+    make_scenes.ensure_c4()
+    sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=64, height=36)
+    assert _same(_renderer(sd, cd, 1, lv_compact=1).render(seed=2), _renderer(sd, cd, 0).render(seed=2))
+
+
+def test_compaction_c2_full_frame(gpu):
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml")
+    plain = _renderer(sd, cd, 1, lv_compact=0).render()
+    r = _renderer(sd, cd, 1, lv_compact=1)
+    assert _same(r.render(), plain)
+    assert r.level_stats()["redo"] == 0
