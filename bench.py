@@ -373,7 +373,7 @@ def main():
                 "frac": hw["frac"] if hw else None,
                 "traffic": (int(pm["traffic_bytes_per_frame"]) if pm and pm.get("traffic_bytes_per_frame")
                             else None),
-                "kernel": pm["kernel"] if pm else roofline.DOMINANT_KERNEL[engine],
+                "kernel": pm["kernel"] if pm else "/".join(np.atleast_1d(roofline.DOMINANT_KERNEL[engine])),
                 "kernel_ms_per_frame": round(kern_frame_ms, 4),
                 "kernel_launches_per_frame": kern_launches,
                 "kernel_avg_ms": round(kern_frame_ms / max(1, kern_launches), 4),

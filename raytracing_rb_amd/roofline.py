@@ -39,8 +39,9 @@ FRAMEBUFFER_BYTES_PER_PX = 24      # float64 RGB written once per pixel
 def algorithmic_ops(counts):
     return sum(COST[k] * int(counts.get(k, 0)) for k in COST)
 
-# The dominant (ray-tree) kernel of each engine, as rocprofv3 names it.
-DOMINANT_KERNEL = {"lanes": "k_render", "levels": "k_level"}
+# The dominant (ray-tree) kernel of each engine, as rocprofv3 names it (the
+# bounce levels run k_level_c when the hit rings fit LDS, else k_level).
+DOMINANT_KERNEL = {"lanes": "k_render", "levels": ("k_level_c", "k_level")}
 
 # FP64 FLOP per lane of one wave instruction of each counted class.
 F64_FLOP = {"SQ_INSTS_VALU_FMA_F64": 2, "SQ_INSTS_VALU_ADD_F64": 1, "SQ_INSTS_VALU_MUL_F64": 1,

@@ -26,16 +26,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def dispatch_values(d, kernel):
-    """{counter: [value per dispatch in dispatch order]} for kernels whose name starts with `kernel`
-    (counting launches, k_render<true,...>, excluded)."""
+def dispatch_values(d, kernel, seen=None):
+    """{counter: [value per dispatch in dispatch order]} for kernels whose short name is `kernel`
+    (a name or a tuple of names; counting launches, k_render<true,...>, excluded).  The short
+    names that matched are added to `seen`."""
+    names = (kernel,) if isinstance(kernel, str) else tuple(kernel)
     per = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
             short = name.split("(")[0].split("<")[0].strip()
-            if short.split("::")[-1] != kernel or "k_renderILb1E" in name or "<true" in name:
+            if short.split("::")[-1] not in names or "k_renderILb1E" in name or "<true" in name:
                 continue
+            if seen is not None:
+                seen.add(short.split("::")[-1])
             key = int(r["Dispatch_Id"])
             per.setdefault(r["Counter_Name"], {}).setdefault(key, 0.0)
             per[r["Counter_Name"]][key] += float(r["Counter_Value"])
@@ -54,16 +58,18 @@ def main():
     a = ap.parse_args()
     from raytracing_rb_amd import roofline
     kernel = roofline.DOMINANT_KERNEL[a.engine]
-    per_frame, launches = {}, None
+    per_frame, launches, seen = {}, None, set()
     for d in a.dirs:
-        for c, vals in dispatch_values(d, kernel).items():
+        for c, vals in dispatch_values(d, kernel, seen).items():
             if len(vals) % a.frames:
                 raise SystemExit("%s: %d dispatches of %s is not a multiple of %d frames" % (d, len(vals), c, a.frames))
             lpf = len(vals) // a.frames
             launches = lpf
             kept = vals[a.skip * lpf:]
             per_frame[c] = sum(kept) / (a.frames - a.skip)
-    out = {"workload": a.workload, "engine": a.engine, "kernel": kernel, "session": a.session,
+    if not seen:
+        raise SystemExit("no dispatch of %s in %s" % (kernel, a.dirs))
+    out = {"workload": a.workload, "engine": a.engine, "kernel": "/".join(sorted(seen)), "session": a.session,
            "source_sha": roofline.kernel_source_sha(), "launches_per_frame": launches,
            "frames": a.frames - a.skip, "per_frame": per_frame,
            "source": [os.path.relpath(d, ROOT) for d in a.dirs]}
