@@ -60,6 +60,10 @@ struct rtx_context {
   size_t scratch_bytes = 0;
   double* d_stk = nullptr;           // per-lane global ray-stack regions
   size_t stk_bytes = 0;
+  double* d_stk2 = nullptr;          // the same for the second half of a two-stream level render
+  size_t stk2_bytes = 0;
+  hipStream_t aux = nullptr;         // bounce levels: the second half's stream (lv_streams = 2)
+  hipEvent_t lv_ev[2] = {};          // ... after the first batch's reset / after the second half
   int* d_work = nullptr;             // ring of per-launch work counters (launches on different streams)
   unsigned work_seq = 0;
   int64_t opt_force_stack = 0;
@@ -78,6 +82,7 @@ struct rtx_context {
   int64_t opt_lv_split = 0;          // bounce levels: 1 = three phase launches per level (trace / shadow / shade)
   int64_t opt_lv_static = -1;        // bounce levels: % of a launch's chunks scheduled statically (-1 auto)
   int64_t opt_lv_compact = -1;       // bounce levels: 1 = park hits in an LDS ring and shade full waves, -1 auto (when it fits)
+  int64_t opt_lv_streams = 2;        // bounce levels: 2 = the region's tiles in two halves on two streams at once
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
@@ -90,7 +95,7 @@ struct rtx_context {
   std::vector<int> comm_devs;
   std::vector<ncclComm_t> comms;
   // rtx_kernel_time: event pairs around each ray-tree kernel launch of the last render call
-  static constexpr int MAX_EV = 32;
+  static constexpr int MAX_EV = 128;
   hipEvent_t ev[2 * MAX_EV] = {};
   int n_ev = 0;
 };
@@ -369,6 +374,10 @@ void rtx_context_destroy(rtx_context* c) {
   hipFree(c->d_cam);
   hipFree(c->d_scratch);
   hipFree(c->d_stk);
+  hipFree(c->d_stk2);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  for (hipEvent_t ev : c->lv_ev)
+    if (ev) (void)hipEventDestroy(ev);
   hipFree(c->d_work);
   hipFree(c->d_lvstats);
   hipFree(c->d_multi);
@@ -391,7 +400,8 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lds_stack", c->opt_lds_stack}, {"tile_order", c->opt_tile_order},   {"sphere_src", c->opt_sphere_src},
       {"kernel_events", c->opt_kernel_events}, {"lv_batch", c->opt_lv_batch},
       {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor},
-      {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact}};
+      {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact},
+      {"lv_streams", c->opt_lv_streams}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -463,6 +473,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_static")) {         // bounce levels: % of chunks scheduled statically, -1 auto
     if (value < -1 || value > 100) return fail(c, RTX_EINVAL, "lv_static must be in [-1, 100]");
     c->opt_lv_static = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_streams")) {        // bounce levels: 1 one stream, 2 two halves on two streams
+    if (value < 1 || value > 2) return fail(c, RTX_EINVAL, "lv_streams must be 1 or 2");
+    c->opt_lv_streams = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_compact")) {        // bounce levels: hit compaction in k_level, -1 auto
@@ -819,7 +834,9 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const size_t npx = (size_t)p.nx * p.nrows;
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   const int per_tile = 64 * p.pre;
-  const int batch_tiles = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, tiles));
+  const int halves = (c->opt_lv_streams == 2 && tiles >= 2) ? 2 : 1;   // lv_streams (below)
+  const int batch_tiles =
+      (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, (tiles + halves - 1) / halves));
   // level-0 items of one batch: pass 0 (tiles) or pass 1 (>= one pixel's extra samples)
   const size_t n0 = std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, p.max_samples - p.pre));
   const size_t fl = (size_t)c->opt_lv_floor;
@@ -842,20 +859,29 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const size_t hcap = (size_t)LV_SLICES << hlog2;
   const size_t sz_hit = split ? al256(hcap * LV_HIT_BYTES) : 0,
                sz_area = split ? al256(hcap * (size_t)std::max(1, c->scene.n_light) * 16) : 0;
-  const size_t total = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_extra + sz_hit + sz_area;
+  // One buffer set per half: with lv_streams = 2 the region's tiles are
+  // rendered in two halves at once, the second on the context's aux stream
+  // (the halves' level tails, launch gaps and reductions overlap the other
+  // half's levels).  The extra-sample list and the statistics are shared
+  // (appended / added atomically); each half has its own level buffers, its
+  // own lanes-engine work counter and ray stacks for its overflow re-render.
+  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area;
+  const size_t total = halves * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
   HIPCHK(c, hipMallocAsync((void**)&buf, total, stream));
-  char* q = buf;
-  p.lv_ctl = (LevelCtl*)q;                  q += sz_ctl;
-  p.lv_redo_of = (int32_t*)q;               q += sz_redo;
-  p.lv_redo_list = (int32_t*)q;             q += sz_redo;
-  p.lv_redo_smp = (double*)q;               q += sz_smp;
-  p.lv_stage[0] = (double*)q;               q += sz_stage;
-  p.lv_stage[1] = (double*)q;               q += sz_stage;
-  p.lv_rec = q;                             q += sz_rec;
-  p.lv_hit = split ? (double*)q : nullptr;  q += sz_hit;
-  p.lv_area = split ? (double*)q : nullptr; q += sz_area;
+  auto carve = [&](KParams& k, char* q) {
+    k.lv_ctl = (LevelCtl*)q;                  q += sz_ctl;
+    k.lv_redo_of = (int32_t*)q;               q += sz_redo;
+    k.lv_redo_list = (int32_t*)q;             q += sz_redo;
+    k.lv_redo_smp = (double*)q;               q += sz_smp;
+    k.lv_stage[0] = (double*)q;               q += sz_stage;
+    k.lv_stage[1] = (double*)q;               q += sz_stage;
+    k.lv_rec = q;                             q += sz_rec;
+    k.lv_hit = split ? (double*)q : nullptr;  q += sz_hit;
+    k.lv_area = split ? (double*)q : nullptr;
+  };
+  carve(p, buf);
   p.lv_split = split ? 1 : 0;
   p.lv_compact = (int32_t)c->opt_lv_compact;   // the launcher turns it off when the rings do not fit LDS
   // Static chunks cost no atomics; dynamic claims balance rays of very
@@ -863,7 +889,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // workgroup's LDS with room to spare (C2: 5.35 vs 5.9 ms at 50 %), half
   // static for large hierarchies (C4: 437 vs 518 ms all static).
   p.lv_static_pct = c->opt_lv_static >= 0 ? (int32_t)c->opt_lv_static : (c->scene.n_sphere <= 512 ? 100 : 50);
-  p.extra_count = (int32_t*)q;
+  p.extra_count = (int32_t*)(buf + halves * set);
   p.extra_list = p.extra_count + 64;
   p.lv_scap = (uint32_t)scap;
   p.lv_slice_log2 = slog2;
@@ -872,11 +898,32 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_rec_bytes = rec_bytes;
   p.lv_acc = c->d_lvstats;
   p.samples = nullptr;
+  LvAux aux{};
+  if (halves == 2) {
+    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    for (hipEvent_t& ev : c->lv_ev)
+      if (!ev) HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const size_t stk = (size_t)p.stk_glb_lanes * (size_t)maxs * 12 * sizeof(double);
+    if (stk > c->stk2_bytes) {
+      hipFree(c->d_stk2);
+      c->d_stk2 = nullptr;
+      c->stk2_bytes = 0;
+      HIPCHK(c, hipMalloc(&c->d_stk2, stk));
+      c->stk2_bytes = stk;
+    }
+    aux.pb = p;
+    carve(aux.pb, buf + set);
+    aux.pb.work = reinterpret_cast<int*>(&aux.pb.lv_ctl->pad[0]);   // zeroed by its half's k_level_begin
+    aux.pb.stk_glb = c->d_stk2;
+    aux.s2 = c->aux;
+    aux.ev_first = c->lv_ev[0];
+    aux.ev_done = c->lv_ev[1];
+  }
   KernelEvents kev{c->ev, 0, rtx_context::MAX_EV};
   if (c->opt_kernel_events && !c->ev[0])
     for (int k = 0; k < 2 * rtx_context::MAX_EV; k++) HIPCHK(c, hipEventCreate(&c->ev[k]));
   const hipError_t e = launch_levels(p, sph_mode(c), maxs, std::max(1, c->cam.depth), batch_tiles, stream,
-                                     c->opt_kernel_events ? &kev : nullptr);
+                                     c->opt_kernel_events ? &kev : nullptr, halves == 2 ? &aux : nullptr);
   if (c->opt_kernel_events) c->n_ev = kev.n;
   const hipError_t f = hipFreeAsync(buf, stream);
   HIPCHK(c, e);
@@ -990,13 +1037,28 @@ rtx_status rtx_level_stats(rtx_context* c, int64_t* out, int32_t n) {
 rtx_status rtx_kernel_time(rtx_context* c, double* total_ms, int32_t* launches) {
   if (!c || !total_ms) return fail(c, RTX_EINVAL, "null argument");
   HIPCHK(c, hipSetDevice(c->device));
-  double sum = 0.0;
+  // The union of the launches' intervals (the two halves of a two-stream
+  // level render overlap), each placed relative to the first launch's start.
+  std::vector<std::pair<double, double>> iv;
   for (int k = 0; k < c->n_ev; k++) {
-    float ms = 0.0f;
+    float a = 0.0f, b = 0.0f;
     HIPCHK(c, hipEventSynchronize(c->ev[2 * k + 1]));
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev[2 * k], c->ev[2 * k + 1]));
-    sum += ms;
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[2 * k]));
+    HIPCHK(c, hipEventElapsedTime(&b, c->ev[0], c->ev[2 * k + 1]));
+    iv.emplace_back(a, b);
   }
+  std::sort(iv.begin(), iv.end());
+  double sum = 0.0, lo = 0.0, hi = -1e300;
+  for (const auto& v : iv) {
+    if (v.first > hi) {
+      if (hi > lo) sum += hi - lo;
+      lo = v.first;
+      hi = v.second;
+    } else if (v.second > hi) {
+      hi = v.second;
+    }
+  }
+  if (hi > lo) sum += hi - lo;
   *total_ms = sum;
   if (launches) *launches = c->n_ev;
   return RTX_OK;

@@ -964,7 +964,7 @@ __device__ __forceinline__ ItemPos decode_item(const KParams& p, int k) {
     const int tiles_x = (p.nx + 7) >> 3;
     const int per = 64 * p.pre;
     const int slot = k / per, r = k - slot * per;
-    const int tile = p.lv_t0 + slot;
+    const int tile = p.lv_t0 + slot * p.lv_tstride;
     const int l = r / p.pre;
     ip.sample = r - l * p.pre;
     ip.px = (tile % tiles_x) * 8 + ((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));

@@ -66,10 +66,11 @@ struct KParams {
   int32_t* tile_order;
   int32_t* tile_cls;
   // bounce-level engine: one batch = pass 0 (the pre samples of the pixels of
-  // tiles [lv_t0, lv_t0 + lv_tiles)) or pass 1 (the extra samples of extra-list
+  // tiles lv_t0 + k * lv_tstride, k < lv_tiles) or pass 1 (the extra samples of extra-list
   // entries [lv_e0, lv_e0 + lv_entries)); level-0 item k of the batch is
   // decode_item(k); trees are stored per level in lv_rec (lv_rec_bytes each).
   int32_t lv_pass, lv_t0, lv_tiles, lv_e0, lv_entries;
+  int32_t lv_tstride;              // 1, or 2 for the interleaved halves of a two-stream render
   uint32_t lv_scap;                // ray records per staging buffer (levels >= 1): LV_SLICES << lv_slice_log2
   int32_t lv_slice_log2;           // slots per slice of a level's ray queue (log2)
   int32_t lv_hslice_log2;          // split phases: slots per slice of a level's hit queue (log2)
@@ -117,8 +118,19 @@ hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s);
 // lv_* buffers of `p` are the caller's: lv_redo_of / lv_rec / staging sized for
 // batch_tiles * 64 * pre level-0 items; lanes-engine buffers (stk_glb) too, for
 // the overflow re-render.
+// Two halves at once (option lv_streams = 2): the tiles [0, T/2) of pass 0 on
+// `s` with the buffers of `p`, the rest on `s2` with the buffers of `pb`
+// (its own level buffers, work counter and lanes-engine stacks; the
+// extra-sample list and the statistics shared with `p`).  `s2` starts after
+// the first reset on `s` (ev_first); `s` waits for `s2` (ev_done) before the
+// extra samples (pass 1), which run on `s` alone.
+struct LvAux {
+  KParams pb;
+  hipStream_t s2;
+  hipEvent_t ev_first, ev_done;
+};
 hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tiles, hipStream_t s,
-                         KernelEvents* kev = nullptr);
+                         KernelEvents* kev = nullptr, const LvAux* aux = nullptr);
 // Tree-record bytes for a scene with n_light lights (one leaf per fired light).
 int levels_rec_bytes(int n_light);
 constexpr size_t RAY_BYTES = 96;                // staged ray record of the bounce-level engine

@@ -984,9 +984,10 @@ __device__ __forceinline__ void lv_layout(const KParams& p, int nlev, uint32_t* 
   }
   if (blockIdx.x == 0 && p.lv_acc) {
     const int t = (int)threadIdx.x;
-    if (t == 0) p.lv_acc[0] += p.lv_ctl->redo_n;
-    if (t == 1) p.lv_acc[1] += p.lv_ctl->dropped;
-    if (t < nlev) p.lv_acc[2 + t] += t == 0 ? p.lv_ctl->count0 : tot[t];
+    // atomic: the two halves of a two-stream render add into the same totals
+    if (t == 0) atomicAdd(&p.lv_acc[0], (unsigned long long)p.lv_ctl->redo_n);
+    if (t == 1) atomicAdd(&p.lv_acc[1], (unsigned long long)p.lv_ctl->dropped);
+    if (t < nlev) atomicAdd(&p.lv_acc[2 + t], (unsigned long long)(t == 0 ? p.lv_ctl->count0 : tot[t]));
   }
   __syncthreads();
 }
@@ -1097,7 +1098,7 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
   const int l = (int)threadIdx.x;
   if (l >= 64) return;
   const int tiles_x = (p.nx + 7) >> 3;
-  const int tile = p.lv_t0 + slot;
+  const int tile = p.lv_t0 + slot * p.lv_tstride;
   const int px_ = (tile % tiles_x) * 8 + ((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));
   const int row = (tile / tiles_x) * 8 + (((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4));
   if (px_ >= p.nx || row >= p.nrows) return;
@@ -1343,11 +1344,12 @@ static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t
 // launches size their grids for its capacity (level 0: the batch's items;
 // deeper levels: LV_SLICES full slices).
 static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_max, int fin_threads, hipStream_t s,
-                              KernelEvents* kev, bool first) {
+                              KernelEvents* kev, bool first, hipEvent_t after_begin = nullptr) {
   const int words = std::min(nlev + 1, LV_MAXL + 1) * LV_SLICES * 32;
   hipLaunchKernelGGL(k_level_begin, dim3((unsigned)std::min(64, (words + 255) / 256)), dim3(256), 0, s, q, n0_max,
                      first ? 1 : 0, nlev);
   hipError_t e = hipGetLastError();
+  if (e == hipSuccess && after_begin) e = hipEventRecord(after_begin, s);
   const long scap = (long)LV_SLICES << q.lv_slice_log2, hcap = (long)LV_SLICES << q.lv_hslice_log2;
   for (int d = 0; d < nlev && e == hipSuccess; d++) {
     const long cap = d == 0 ? (long)n0_max : scap;
@@ -1367,21 +1369,38 @@ static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_ma
 }
 
 hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tiles, hipStream_t s,
-                         KernelEvents* kev) {
+                         KernelEvents* kev, const LvAux* aux) {
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   if (tiles == 0) return hipSuccess;
   mode = resolve_mode(p.scene, mode);
   batch_tiles = std::max(1, std::min(batch_tiles, tiles));
   const int per_tile = 64 * p.pre;
   p.tile_order = nullptr;
+  if (aux && tiles < 2) aux = nullptr;
+  // The halves interleave tiles (even / odd): neighbouring tiles cost alike,
+  // so the halves are balanced and each one's tail overlaps the other's work.
+  const int stride = aux ? 2 : 1;
   hipError_t e = hipSuccess;                   // (the first batch's k_level_begin zeroes the extra count)
-  for (int t0 = 0; t0 < tiles && e == hipSuccess; t0 += batch_tiles) {
-    KParams q = p;
-    q.lv_pass = 0;
-    q.lv_t0 = t0;
-    q.lv_tiles = std::min(batch_tiles, tiles - t0);
-    q.lv_e0 = q.lv_entries = 0;
-    e = level_batch(q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles, s, kev, t0 == 0);
+  // batches of the tiles phase + stride * k (k < n) with the buffers of `base` on stream `st`
+  auto run = [&](const KParams& base, int phase, int n, hipStream_t st, hipEvent_t after_first_begin) {
+    for (int k0 = 0; k0 < n && e == hipSuccess; k0 += batch_tiles) {
+      KParams q = base;
+      q.lv_pass = 0;
+      q.lv_t0 = phase + stride * k0;
+      q.lv_tstride = stride;
+      q.lv_tiles = std::min(batch_tiles, n - k0);
+      q.lv_e0 = q.lv_entries = 0;
+      const bool first = phase == 0 && k0 == 0;
+      e = level_batch(q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles, st, kev, first,
+                      first ? after_first_begin : nullptr);
+    }
+  };
+  run(p, 0, (tiles + stride - 1) / stride, s, aux ? aux->ev_first : nullptr);
+  if (aux && e == hipSuccess) {
+    e = hipStreamWaitEvent(aux->s2, aux->ev_first, 0);    // after the shared totals are zeroed
+    run(aux->pb, 1, tiles / 2, aux->s2, nullptr);
+    if (e == hipSuccess) e = hipEventRecord(aux->ev_done, aux->s2);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, aux->ev_done, 0);
   }
   if (e != hipSuccess || p.max_samples <= p.pre) return e;
   // extra samples of the pixels the variance test listed (count on the device)
@@ -1394,6 +1413,7 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
     q.lv_e0 = e0;
     q.lv_entries = std::min(entries, npx - e0);
     q.lv_t0 = q.lv_tiles = 0;
+    q.lv_tstride = 1;
     e = level_batch(q, mode, maxs, nlev, q.lv_entries * n_extra, q.lv_entries, s, kev, false);
   }
   return e;

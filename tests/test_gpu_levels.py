@@ -304,3 +304,78 @@ def test_compaction_c2_full_frame(gpu):
     r = _renderer(sd, cd, 1, lv_compact=1)
     assert _same(r.render(), plain)
     assert r.level_stats()["redo"] == 0
+
+
+# ---- two halves on two streams (option lv_streams = 2, the default)
+@pytest.mark.parametrize("world,camera,ov", SCENES_SMALL)
+def test_two_streams_bit_identical(gpu, world, camera, ov):
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=3)
+    stats = []
+    for streams in (1, 2):
+        r = _renderer(sd, cd, 1, lv_streams=streams)
+        assert _same(r.render(seed=3), lanes), streams
+        stats.append(r.level_stats())
+    assert stats[0] == stats[1]                           # shared totals added atomically by both halves
+
+
+@pytest.mark.parametrize("opts", [
+    dict(lv_batch=512),                                   # several batches per half, each half on its stream
+    dict(lv_stage_pct=5, lv_floor=0),                     # both halves re-render overflowed samples (own stacks)
+    dict(lv_rec_pct=101, lv_floor=0),
+    dict(lv_static=37, lv_batch=1000),
+])
+def test_two_streams_batches_and_overflow(gpu, opts):
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
+    lanes = _renderer(sd, cd, 0).render(seed=5)
+    r = _renderer(sd, cd, 1, lv_streams=2, **opts)
+    assert _same(r.render(seed=5), lanes)
+    if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
+        assert r.level_stats()["redo"] > 0
+
+
+def test_two_streams_extras_tiles_and_errors(gpu, tmp_path):
+    """render_at's extra samples: both halves append to one extra list; tile
+    shares and raise sites as with one stream."""
+    import torch
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import RtxError
+    sd, cd = _scene("mix_world.yml", "mix_camera.yml", width=64, height=36, pre_sample_times=2,
+                    max_sample_times=6, variant_threshold=1e-4)
+    lanes = _renderer(sd, cd, 0).render(seed=9)
+    for opts in (dict(), dict(lv_batch=300)):
+        assert _same(_renderer(sd, cd, 1, lv_streams=2, **opts).render(seed=9), lanes), opts
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=160, height=90)
+    one, two = _renderer(sd, cd, 1, lv_streams=1), _renderer(sd, cd, 1, lv_streams=2)
+    for k, n in ((0, 3), (2, 3), (1, 8)):
+        rows = one.lib.rtx_tiles_rows_per_rank(cd.height, 8, n)
+        a = torch.zeros((rows, cd.width, 3), dtype=torch.float64, device="cuda")
+        b = torch.zeros_like(a)
+        one.render_tiles_device(a.data_ptr(), 8, k, n, seed=2)
+        two.render_tiles_device(b.data_ptr(), 8, k, n, seed=2)
+        torch.cuda.synchronize()
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64)), (k, n)
+    src = open(os.path.join(SCENES, "c1_world.yml")).read()
+    src = src.replace("diffuse_rate:           [0.5, 0.5, 0.5]", "diffuse_rate:           [0.99, 0.99, 0.99]")
+    src = src.replace("ambient:                [0.05, 0.05, 0.05]", "ambient:                [0.3, 0.3, 0.3]", 1)
+    p = tmp_path / "bright.yml"
+    p.write_text(src)
+    sd, cd = config.load_scene(str(p), os.path.join(SCENES, "c1_camera.yml"), camera_overrides=dict(width=24, height=14))
+    msgs = []
+    for engine, opts in ((0, {}), (1, dict(lv_streams=2)), (1, dict(lv_streams=1))):
+        with pytest.raises(RtxError) as e:
+            _renderer(sd, cd, engine, **opts).render()
+        msgs.append(str(e.value))
+    assert msgs[0] == msgs[1] == msgs[2]
+
+
+def test_two_streams_c2_full_frame_and_kernel_time(gpu):
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml")
+    one = _renderer(sd, cd, 1, lv_streams=1).render()
+    r = _renderer(sd, cd, 1, lv_streams=2)
+    assert _same(r.render(), one)
+    assert r.level_stats()["redo"] == 0
+    r.set_option("kernel_events", 1)
+    r.render()
+    ms, launches = r.kernel_time()
+    assert launches == 10 and 0.5 < ms < 50.0, (ms, launches)   # union of the two halves' level launches
