@@ -277,7 +277,9 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          rest claimed from sharded counters; -1 [default] = 100 up to 512 spheres, else 50; same bits),
          "lv_compact" (bounce levels: 1 park the rays that hit something in a per-wave LDS ring and run the
          shadow walks and shading on full waves, 0 off, -1 [default] = on whenever the rings fit the walk's
-         LDS; same bits). */
+         LDS; same bits), "lv_streams" (bounce levels: the region's 8x8 tiles in this many interleaved parts,
+         1..4, rendered at once on as many HIP streams, parts 1.. on streams the context owns; one part's level
+         tails and reductions overlap the others' work; 2 [default]; same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

@@ -60,10 +60,10 @@ struct rtx_context {
   size_t scratch_bytes = 0;
   double* d_stk = nullptr;           // per-lane global ray-stack regions
   size_t stk_bytes = 0;
-  double* d_stk2 = nullptr;          // the same for the second half of a two-stream level render
-  size_t stk2_bytes = 0;
-  hipStream_t aux = nullptr;         // bounce levels: the second half's stream (lv_streams = 2)
-  hipEvent_t lv_ev[2] = {};          // ... after the first batch's reset / after the second half
+  double* d_stk2[LV_MAX_PARTS - 1] = {};   // the same for parts 1.. of a multi-stream level render
+  size_t stk2_bytes[LV_MAX_PARTS - 1] = {};
+  hipStream_t aux[LV_MAX_PARTS - 1] = {};  // bounce levels: the streams of parts 1.. (lv_streams)
+  hipEvent_t lv_ev[LV_MAX_PARTS] = {};     // ... after the first batch's reset / after each part
   int* d_work = nullptr;             // ring of per-launch work counters (launches on different streams)
   unsigned work_seq = 0;
   int64_t opt_force_stack = 0;
@@ -82,7 +82,7 @@ struct rtx_context {
   int64_t opt_lv_split = 0;          // bounce levels: 1 = three phase launches per level (trace / shadow / shade)
   int64_t opt_lv_static = -1;        // bounce levels: % of a launch's chunks scheduled statically (-1 auto)
   int64_t opt_lv_compact = -1;       // bounce levels: 1 = park hits in an LDS ring and shade full waves, -1 auto (when it fits)
-  int64_t opt_lv_streams = 2;        // bounce levels: 2 = the region's tiles in two halves on two streams at once
+  int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
@@ -374,8 +374,10 @@ void rtx_context_destroy(rtx_context* c) {
   hipFree(c->d_cam);
   hipFree(c->d_scratch);
   hipFree(c->d_stk);
-  hipFree(c->d_stk2);
-  if (c->aux) (void)hipStreamDestroy(c->aux);
+  for (int j = 0; j < LV_MAX_PARTS - 1; j++) {
+    hipFree(c->d_stk2[j]);
+    if (c->aux[j]) (void)hipStreamDestroy(c->aux[j]);
+  }
   for (hipEvent_t ev : c->lv_ev)
     if (ev) (void)hipEventDestroy(ev);
   hipFree(c->d_work);
@@ -475,8 +477,8 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_lv_static = value;
     return RTX_OK;
   }
-  if (!strcmp(key, "lv_streams")) {        // bounce levels: 1 one stream, 2 two halves on two streams
-    if (value < 1 || value > 2) return fail(c, RTX_EINVAL, "lv_streams must be 1 or 2");
+  if (!strcmp(key, "lv_streams")) {        // bounce levels: tiles in this many interleaved parts on as many streams
+    if (value < 1 || value > LV_MAX_PARTS) return fail(c, RTX_EINVAL, "lv_streams must be in [1, %d]", LV_MAX_PARTS);
     c->opt_lv_streams = value;
     return RTX_OK;
   }
@@ -834,9 +836,9 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const size_t npx = (size_t)p.nx * p.nrows;
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   const int per_tile = 64 * p.pre;
-  const int halves = (c->opt_lv_streams == 2 && tiles >= 2) ? 2 : 1;   // lv_streams (below)
+  const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_streams, tiles));   // lv_streams (below)
   const int batch_tiles =
-      (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, (tiles + halves - 1) / halves));
+      (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, (tiles + parts - 1) / parts));
   // level-0 items of one batch: pass 0 (tiles) or pass 1 (>= one pixel's extra samples)
   const size_t n0 = std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, p.max_samples - p.pre));
   const size_t fl = (size_t)c->opt_lv_floor;
@@ -859,14 +861,14 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const size_t hcap = (size_t)LV_SLICES << hlog2;
   const size_t sz_hit = split ? al256(hcap * LV_HIT_BYTES) : 0,
                sz_area = split ? al256(hcap * (size_t)std::max(1, c->scene.n_light) * 16) : 0;
-  // One buffer set per half: with lv_streams = 2 the region's tiles are
-  // rendered in two halves at once, the second on the context's aux stream
-  // (the halves' level tails, launch gaps and reductions overlap the other
-  // half's levels).  The extra-sample list and the statistics are shared
-  // (appended / added atomically); each half has its own level buffers, its
+  // One buffer set per part: with lv_streams = P the region's tiles are
+  // rendered in P interleaved parts at once, parts 1.. on the context's aux
+  // streams (one part's level tails, launch gaps and reductions overlap the
+  // others' levels).  The extra-sample list and the statistics are shared
+  // (appended / added atomically); each part has its own level buffers, its
   // own lanes-engine work counter and ray stacks for its overflow re-render.
   const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area;
-  const size_t total = halves * set + sz_extra;
+  const size_t total = parts * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
   HIPCHK(c, hipMallocAsync((void**)&buf, total, stream));
@@ -889,7 +891,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // workgroup's LDS with room to spare (C2: 5.35 vs 5.9 ms at 50 %), half
   // static for large hierarchies (C4: 437 vs 518 ms all static).
   p.lv_static_pct = c->opt_lv_static >= 0 ? (int32_t)c->opt_lv_static : (c->scene.n_sphere <= 512 ? 100 : 50);
-  p.extra_count = (int32_t*)(buf + halves * set);
+  p.extra_count = (int32_t*)(buf + parts * set);
   p.extra_list = p.extra_count + 64;
   p.lv_scap = (uint32_t)scap;
   p.lv_slice_log2 = slog2;
@@ -899,31 +901,35 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_acc = c->d_lvstats;
   p.samples = nullptr;
   LvAux aux{};
-  if (halves == 2) {
-    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+  if (parts > 1) {
+    aux.parts = parts;
     for (hipEvent_t& ev : c->lv_ev)
       if (!ev) HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    const size_t stk = (size_t)p.stk_glb_lanes * (size_t)maxs * 12 * sizeof(double);
-    if (stk > c->stk2_bytes) {
-      hipFree(c->d_stk2);
-      c->d_stk2 = nullptr;
-      c->stk2_bytes = 0;
-      HIPCHK(c, hipMalloc(&c->d_stk2, stk));
-      c->stk2_bytes = stk;
-    }
-    aux.pb = p;
-    carve(aux.pb, buf + set);
-    aux.pb.work = reinterpret_cast<int*>(&aux.pb.lv_ctl->pad[0]);   // zeroed by its half's k_level_begin
-    aux.pb.stk_glb = c->d_stk2;
-    aux.s2 = c->aux;
     aux.ev_first = c->lv_ev[0];
-    aux.ev_done = c->lv_ev[1];
+    const size_t stk = (size_t)p.stk_glb_lanes * (size_t)maxs * 12 * sizeof(double);
+    for (int j = 0; j < parts - 1; j++) {
+      if (!c->aux[j]) HIPCHK(c, hipStreamCreateWithFlags(&c->aux[j], hipStreamNonBlocking));
+      if (stk > c->stk2_bytes[j]) {
+        hipFree(c->d_stk2[j]);
+        c->d_stk2[j] = nullptr;
+        c->stk2_bytes[j] = 0;
+        HIPCHK(c, hipMalloc(&c->d_stk2[j], stk));
+        c->stk2_bytes[j] = stk;
+      }
+      KParams& q = aux.pb[j];
+      q = p;
+      carve(q, buf + (size_t)(j + 1) * set);
+      q.work = reinterpret_cast<int*>(&q.lv_ctl->pad[0]);   // zeroed by its part's k_level_begin
+      q.stk_glb = c->d_stk2[j];
+      aux.s2[j] = c->aux[j];
+      aux.ev_done[j] = c->lv_ev[j + 1];
+    }
   }
   KernelEvents kev{c->ev, 0, rtx_context::MAX_EV};
   if (c->opt_kernel_events && !c->ev[0])
     for (int k = 0; k < 2 * rtx_context::MAX_EV; k++) HIPCHK(c, hipEventCreate(&c->ev[k]));
   const hipError_t e = launch_levels(p, sph_mode(c), maxs, std::max(1, c->cam.depth), batch_tiles, stream,
-                                     c->opt_kernel_events ? &kev : nullptr, halves == 2 ? &aux : nullptr);
+                                     c->opt_kernel_events ? &kev : nullptr, parts > 1 ? &aux : nullptr);
   if (c->opt_kernel_events) c->n_ev = kev.n;
   const hipError_t f = hipFreeAsync(buf, stream);
   HIPCHK(c, e);
@@ -1037,7 +1043,7 @@ rtx_status rtx_level_stats(rtx_context* c, int64_t* out, int32_t n) {
 rtx_status rtx_kernel_time(rtx_context* c, double* total_ms, int32_t* launches) {
   if (!c || !total_ms) return fail(c, RTX_EINVAL, "null argument");
   HIPCHK(c, hipSetDevice(c->device));
-  // The union of the launches' intervals (the two halves of a two-stream
+  // The union of the launches' intervals (the parts of a multi-stream
   // level render overlap), each placed relative to the first launch's start.
   std::vector<std::pair<double, double>> iv;
   for (int k = 0; k < c->n_ev; k++) {

@@ -118,16 +118,19 @@ hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s);
 // lv_* buffers of `p` are the caller's: lv_redo_of / lv_rec / staging sized for
 // batch_tiles * 64 * pre level-0 items; lanes-engine buffers (stk_glb) too, for
 // the overflow re-render.
-// Two halves at once (option lv_streams = 2): the tiles [0, T/2) of pass 0 on
-// `s` with the buffers of `p`, the rest on `s2` with the buffers of `pb`
-// (its own level buffers, work counter and lanes-engine stacks; the
-// extra-sample list and the statistics shared with `p`).  `s2` starts after
-// the first reset on `s` (ev_first); `s` waits for `s2` (ev_done) before the
-// extra samples (pass 1), which run on `s` alone.
+// Parts at once (option lv_streams = P > 1): pass 0's tiles interleaved over
+// P parts, tile t in part t mod P; part 0 on `s` with the buffers of `p`,
+// part j > 0 on s2[j - 1] with the buffers of pb[j - 1] (own level buffers,
+// work counter and lanes-engine stacks; the extra-sample list and the
+// statistics shared with `p`).  The parts j > 0 start after the first reset
+// on `s` (ev_first); `s` waits for all of them (ev_done) before the extra
+// samples (pass 1), which run on `s` alone.
+constexpr int LV_MAX_PARTS = 4;
 struct LvAux {
-  KParams pb;
-  hipStream_t s2;
-  hipEvent_t ev_first, ev_done;
+  int parts;                       // P (2 .. LV_MAX_PARTS)
+  KParams pb[LV_MAX_PARTS - 1];
+  hipStream_t s2[LV_MAX_PARTS - 1];
+  hipEvent_t ev_first, ev_done[LV_MAX_PARTS - 1];
 };
 hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tiles, hipStream_t s,
                          KernelEvents* kev = nullptr, const LvAux* aux = nullptr);

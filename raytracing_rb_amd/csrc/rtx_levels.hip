@@ -1376,10 +1376,11 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
   batch_tiles = std::max(1, std::min(batch_tiles, tiles));
   const int per_tile = 64 * p.pre;
   p.tile_order = nullptr;
-  if (aux && tiles < 2) aux = nullptr;
-  // The halves interleave tiles (even / odd): neighbouring tiles cost alike,
-  // so the halves are balanced and each one's tail overlaps the other's work.
-  const int stride = aux ? 2 : 1;
+  if (aux && tiles < aux->parts) aux = nullptr;
+  // The parts interleave tiles (tile t in part t mod P): neighbouring tiles
+  // cost alike, so the parts are balanced and each one's tail overlaps the
+  // others' work.
+  const int stride = aux ? aux->parts : 1;
   hipError_t e = hipSuccess;                   // (the first batch's k_level_begin zeroes the extra count)
   // batches of the tiles phase + stride * k (k < n) with the buffers of `base` on stream `st`
   auto run = [&](const KParams& base, int phase, int n, hipStream_t st, hipEvent_t after_first_begin) {
@@ -1396,12 +1397,12 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
     }
   };
   run(p, 0, (tiles + stride - 1) / stride, s, aux ? aux->ev_first : nullptr);
-  if (aux && e == hipSuccess) {
-    e = hipStreamWaitEvent(aux->s2, aux->ev_first, 0);    // after the shared totals are zeroed
-    run(aux->pb, 1, tiles / 2, aux->s2, nullptr);
-    if (e == hipSuccess) e = hipEventRecord(aux->ev_done, aux->s2);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, aux->ev_done, 0);
+  for (int j = 1; aux && j < aux->parts && e == hipSuccess; j++) {
+    e = hipStreamWaitEvent(aux->s2[j - 1], aux->ev_first, 0);    // after the shared totals are zeroed
+    run(aux->pb[j - 1], j, (tiles - j + stride - 1) / stride, aux->s2[j - 1], nullptr);
+    if (e == hipSuccess) e = hipEventRecord(aux->ev_done[j - 1], aux->s2[j - 1]);
   }
+  for (int j = 1; aux && j < aux->parts && e == hipSuccess; j++) e = hipStreamWaitEvent(s, aux->ev_done[j - 1], 0);
   if (e != hipSuccess || p.max_samples <= p.pre) return e;
   // extra samples of the pixels the variance test listed (count on the device)
   const int n_extra = p.max_samples - p.pre;

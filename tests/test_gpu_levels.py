@@ -312,11 +312,11 @@ def test_two_streams_bit_identical(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=3)
     stats = []
-    for streams in (1, 2):
+    for streams in (1, 2, 3, 4):
         r = _renderer(sd, cd, 1, lv_streams=streams)
         assert _same(r.render(seed=3), lanes), streams
         stats.append(r.level_stats())
-    assert stats[0] == stats[1]                           # shared totals added atomically by both halves
+    assert all(st == stats[0] for st in stats)            # shared totals added atomically by every part
 
 
 @pytest.mark.parametrize("opts", [
@@ -328,10 +328,11 @@ def test_two_streams_bit_identical(gpu, world, camera, ov):
 def test_two_streams_batches_and_overflow(gpu, opts):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
     lanes = _renderer(sd, cd, 0).render(seed=5)
-    r = _renderer(sd, cd, 1, lv_streams=2, **opts)
-    assert _same(r.render(seed=5), lanes)
-    if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
-        assert r.level_stats()["redo"] > 0
+    for streams in (2, 4):
+        r = _renderer(sd, cd, 1, lv_streams=streams, **opts)
+        assert _same(r.render(seed=5), lanes), streams
+        if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
+            assert r.level_stats()["redo"] > 0
 
 
 def test_two_streams_extras_tiles_and_errors(gpu, tmp_path):
@@ -343,10 +344,10 @@ def test_two_streams_extras_tiles_and_errors(gpu, tmp_path):
     sd, cd = _scene("mix_world.yml", "mix_camera.yml", width=64, height=36, pre_sample_times=2,
                     max_sample_times=6, variant_threshold=1e-4)
     lanes = _renderer(sd, cd, 0).render(seed=9)
-    for opts in (dict(), dict(lv_batch=300)):
-        assert _same(_renderer(sd, cd, 1, lv_streams=2, **opts).render(seed=9), lanes), opts
+    for opts in (dict(), dict(lv_batch=300), dict(lv_streams=3), dict(lv_streams=4, lv_batch=300)):
+        assert _same(_renderer(sd, cd, 1, **dict(dict(lv_streams=2), **opts)).render(seed=9), lanes), opts
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=160, height=90)
-    one, two = _renderer(sd, cd, 1, lv_streams=1), _renderer(sd, cd, 1, lv_streams=2)
+    one, two = _renderer(sd, cd, 1, lv_streams=1), _renderer(sd, cd, 1, lv_streams=3)
     for k, n in ((0, 3), (2, 3), (1, 8)):
         rows = one.lib.rtx_tiles_rows_per_rank(cd.height, 8, n)
         a = torch.zeros((rows, cd.width, 3), dtype=torch.float64, device="cuda")

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--size", default="")
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--share", default="", help="k/N: time rank k's share of N ranks (8-row tiles)")
     ap.add_argument("opts", nargs="*")
     a = ap.parse_args()
     import torch
@@ -41,18 +42,25 @@ def main():
                                os.path.join(ROOT, "scenes", a.scene + "_camera.yml"), camera_overrides=ov)
     out = torch.empty((cd.height, cd.width, 3), dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream()
+    share = tuple(int(v) for v in a.share.split("/")) if a.share else None
+
+    def render(r):
+        if share:
+            r.render_tiles_device(out.data_ptr(), 8, share[0], share[1], stream=s.cuda_stream)
+        else:
+            r.render_device(out.data_ptr(), stream=s.cuda_stream)
     for o in (a.opts or ["{}"]):
         opts = json.loads(o)
         r = Renderer(sd, cd)              # a fresh context per option set: options do not carry over
         for k, v in opts.items():
             r.set_option(k, v)
-        r.render_device(out.data_ptr(), stream=s.cuda_stream)
+        render(r)
         r.sync(s.cuda_stream)
         ts = []
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            r.render_device(out.data_ptr(), stream=s.cuda_stream)
+            render(r)
             e1.record(s)
             e1.synchronize()
             ts.append(e0.elapsed_time(e1))
@@ -61,8 +69,9 @@ def main():
         r.close()
         ts.sort()
         sha = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
-        print("%-8s %-40s min %9.3f ms  median %9.3f ms  %8.2f Mpix/s  sha %s" % (
-            a.scene, o, ts[0], ts[len(ts) // 2], cd.width * cd.height / ts[len(ts) // 2] / 1e3, sha), flush=True)
+        print("%-8s %-40s min %9.3f ms  median %9.3f ms  %8.2f Mpix/s  sha %s%s" % (
+            a.scene, o, ts[0], ts[len(ts) // 2], cd.width * cd.height / ts[len(ts) // 2] / 1e3, sha,
+            "  (share %s: Mpix/s of the whole frame)" % a.share if share else ""), flush=True)
         if st:
             print("         levels: rays per level %s, redo %d, dropped %d" % (st["rays"], st["redo"], st["dropped"]),
                   flush=True)
