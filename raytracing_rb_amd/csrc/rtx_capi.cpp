@@ -82,6 +82,7 @@ struct rtx_context {
   int64_t opt_lv_split = 0;          // bounce levels: 1 = three phase launches per level (trace / shadow / shade)
   int64_t opt_lv_static = -1;        // bounce levels: % of a launch's chunks scheduled statically (-1 auto)
   int64_t opt_lv_compact = -1;       // bounce levels: 1 = park hits in an LDS ring and shade full waves, -1 auto (when it fits)
+  int64_t opt_lv_grid_div = 1;       // bounce levels: persistent level grids = resident workgroups / this
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
@@ -266,12 +267,15 @@ struct Bvh4Builder {
 
   int32_t leaf(int lo, int hi) {
     const int id = (int)(slot_obj.size() / BVH_LEAF);
-    for (int u = 0; u < BVH_LEAF; u++) {
+    float soa[4][BVH_LEAF];                      // a leaf's float32 records component-major:
+    for (int u = 0; u < BVH_LEAF; u++) {         // {x0..x3}, {y0..y3}, {z0..z3}, {R^2 0..3}
       const int rec = lo + u < hi ? sp[lo + u].rec : -1;
       slot_obj.push_back(rec >= 0 ? sph_obj[rec] : -1);
       slot64.push_back(rec >= 0 ? sph64[rec] : Sphere64{{0.0, 0.0, 0.0}, -1.0});
-      for (int k = 0; k < 4; k++) slot32.push_back(rec >= 0 ? sph32[4 * rec + k] : 0.0f);
+      for (int k = 0; k < 4; k++) soa[k][u] = rec >= 0 ? sph32[4 * rec + k] : 0.0f;
     }
+    for (int k = 0; k < 4; k++)
+      for (int u = 0; u < BVH_LEAF; u++) slot32.push_back(soa[k][u]);
     return ~(int32_t)((id << 2) | (hi - lo - 1));
   }
 
@@ -292,8 +296,8 @@ struct Bvh4Builder {
     for (int k = 0; k < 4; k++) {               // empty slot: a point far outside every scene,
       n.child[k] = BVH_NONE;                     // which no finite ray's slab test accepts
       for (int a = 0; a < 3; a++) {
-        n.lo[a][k] = 3e38f;
-        n.hi[a][k] = 3e38f;
+        n.lh[a][k][0] = 3e38f;
+        n.lh[a][k][1] = 3e38f;
       }
     }
     const int below = pushes + ng - 1;          // visiting one child leaves <= ng-1 siblings pushed
@@ -302,8 +306,8 @@ struct Bvh4Builder {
       float blo[3], bhi[3];
       box(g[k], g[k + 1], blo, bhi);
       for (int a = 0; a < 3; a++) {
-        n.lo[a][k] = blo[a];
-        n.hi[a][k] = bhi[a];
+        n.lh[a][k][0] = blo[a];
+        n.lh[a][k][1] = bhi[a];
       }
       n.child[k] = build(g[k], g[k + 1], below);
     }
@@ -403,7 +407,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"kernel_events", c->opt_kernel_events}, {"lv_batch", c->opt_lv_batch},
       {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor},
       {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact},
-      {"lv_streams", c->opt_lv_streams}};
+      {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -475,6 +479,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_static")) {         // bounce levels: % of chunks scheduled statically, -1 auto
     if (value < -1 || value > 100) return fail(c, RTX_EINVAL, "lv_static must be in [-1, 100]");
     c->opt_lv_static = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_grid_div")) {       // bounce levels: level grids = resident workgroups / this
+    if (value < 1 || value > 8) return fail(c, RTX_EINVAL, "lv_grid_div must be in [1, 8]");
+    c->opt_lv_grid_div = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_streams")) {        // bounce levels: tiles in this many interleaved parts on as many streams
@@ -885,7 +894,8 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;
-  p.lv_compact = (int32_t)c->opt_lv_compact;   // the launcher turns it off when the rings do not fit LDS
+  p.lv_compact = (int32_t)c->opt_lv_compact;
+  p.lv_grid_div = (int32_t)c->opt_lv_grid_div;   // the launcher turns it off when the rings do not fit LDS
   // Static chunks cost no atomics; dynamic claims balance rays of very
   // different cost.  Auto: all static while the sphere records fit one walk
   // workgroup's LDS with room to spare (C2: 5.35 vs 5.9 ms at 50 %), half

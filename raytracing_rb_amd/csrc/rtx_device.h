@@ -16,6 +16,7 @@ namespace rtx {
 constexpr double PI = 3.141592653589793;   // Math::PI == M_PI
 constexpr double EPS = 1e-5;               // Alex::EPSILON (src/libs/algebra.rb:2)
 constexpr float CULL_M = 2e-5f;            // pre-test margin (exact culls)
+typedef float F2 __attribute__((ext_vector_type(2)));   // packed FP32 pair (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32)
 
 struct Ray {
   V3 o, d;                          // Alex::Ray#position, #front
@@ -464,6 +465,9 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
   const float ix = 1.0f / ex, iy = 1.0f / ey, iz = 1.0f / ez;
   const float ax = (ox + mS) * ix, ay = (oy + mS) * iy, az = (oz + mS) * iz;   // lo - mS side
   const float bx = (ox - mS) * ix, by = (oy - mS) * iy, bz = (oz - mS) * iz;   // hi + mS side
+  // packed operands of the slab test: {lo, hi} * {i, i} + {-a, -b} per axis
+  const F2 pix = {ix, ix}, piy = {iy, iy}, piz = {iz, iz};
+  const F2 pax = {-ax, -bx}, pay = {-ay, -by}, paz = {-az, -bz};
   // A non-finite or zero ray makes no cull (comparisons would be unordered).
   const bool fin = __builtin_isfinite(dd) && __builtin_isfinite(Sx) && l1 > 0.0f && __builtin_isfinite(ix) &&
                    __builtin_isfinite(iy) && __builtin_isfinite(iz);
@@ -523,12 +527,12 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         ch[k] = nodes[ref].child[k];
-        const float t0x = __builtin_fmaf(nodes[ref].lo[0][k], ix, -ax);
-        const float t1x = __builtin_fmaf(nodes[ref].hi[0][k], ix, -bx);
-        const float t0y = __builtin_fmaf(nodes[ref].lo[1][k], iy, -ay);
-        const float t1y = __builtin_fmaf(nodes[ref].hi[1][k], iy, -by);
-        const float t0z = __builtin_fmaf(nodes[ref].lo[2][k], iz, -az);
-        const float t1z = __builtin_fmaf(nodes[ref].hi[2][k], iz, -bz);
+        // {t0, t1} per axis in one v_pk_fma_f32 each: the same fused FP32 operations as
+        // fmaf(lo, i, -a), fmaf(hi, i, -b)
+        const F2 tx = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&nodes[ref].lh[0][k][0]), pix, pax);
+        const F2 ty = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&nodes[ref].lh[1][k][0]), piy, pay);
+        const F2 tz = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&nodes[ref].lh[2][k][0]), piz, paz);
+        const float t0x = tx.x, t1x = tx.y, t0y = ty.x, t1y = ty.y, t0z = tz.x, t1z = tz.y;
         const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
         const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
         // empty slots hold a box at (3e38, 3e38, 3e38): never wanted by a finite ray
@@ -557,18 +561,27 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
       const int v = ~ref;
       const int slot0 = (v >> 2) * BVH_LEAF;
       const int cnt = (v & 3) + 1;
-      float4 c[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) c[u] = leaf4[slot0 + u];
+      // the leaf's 4 records as {x0..x3}, {y0..y3}, {z0..z3}, {R^2 0..3}: the
+      // pre-test of §2.1 on two spheres per packed FP32 instruction (the same
+      // operations as the per-sphere form in query())
+      const float4 cx = leaf4[slot0], cy = leaf4[slot0 + 1], cz = leaf4[slot0 + 2], cw = leaf4[slot0 + 3];
       uint32_t keep = 0;
+      const F2 po = {ox, ox}, poy = {oy, oy}, poz = {oz, oz};
+      const F2 pdx = {dx, dx}, pdy = {dy, dy}, pdz = {dz, dz}, pdd = {dd, dd}, pkl = {kline, kline};
+      const F2 pms = {ms2, ms2};
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const float ocx = c[u].x - ox, ocy = c[u].y - oy, ocz = c[u].z - oz;
-        const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
-        const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
-        const bool miss_line = __builtin_fmaf(s, dd, -q * q) > __builtin_fmaf(dd, c[u].w, kline);
-        const bool behind = q < qneg && s > c[u].w + ms2;
-        keep |= (miss_line || behind) ? 0u : (1u << u);
+      for (int h = 0; h < 2; h++) {
+        const F2 X = h ? F2{cx.z, cx.w} : F2{cx.x, cx.y}, Y = h ? F2{cy.z, cy.w} : F2{cy.x, cy.y};
+        const F2 Z = h ? F2{cz.z, cz.w} : F2{cz.x, cz.y}, Wr = h ? F2{cw.z, cw.w} : F2{cw.x, cw.y};
+        const F2 ocx = X - po, ocy = Y - poy, ocz = Z - poz;
+        const F2 s = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
+        const F2 q = __builtin_elementwise_fma(ocx, pdx, __builtin_elementwise_fma(ocy, pdy, ocz * pdz));
+        const F2 l = __builtin_elementwise_fma(s, pdd, -(q * q));
+        const F2 r = __builtin_elementwise_fma(pdd, Wr, pkl);
+        const F2 wm = Wr + pms;
+        const bool m0 = l.x > r.x || (q.x < qneg && s.x > wm.x);   // misses the line, or wholly behind
+        const bool m1 = l.y > r.y || (q.y < qneg && s.y > wm.y);
+        keep |= (m0 ? 0u : 1u << (2 * h)) | (m1 ? 0u : 2u << (2 * h));
       }
       keep &= (1u << cnt) - 1u;
       while (keep) {

@@ -1275,7 +1275,8 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   int cus = 0, per_cu = 0;
   const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(kern), BS, lds, cus, per_cu);
   if (e != hipSuccess) return e;
-  return launch_timed(kern, std::min<long>((cap_items + BS - 1) / BS, (long)cus * per_cu), BS, lds, s, kev, q, level);
+  const long grid = std::max<long>(1, (long)cus * per_cu / std::max(1, q.lv_grid_div));
+  return launch_timed(kern, std::min<long>((cap_items + BS - 1) / BS, grid), BS, lds, s, kev, q, level);
 }
 
 // The fused kernel runs the engine's block sizes (BS_LIN / BS_BVH, 2 waves per

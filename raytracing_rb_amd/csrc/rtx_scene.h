@@ -58,8 +58,8 @@ constexpr int BVH_LEAF = 4;
 constexpr int32_t BVH_NONE = 0x7fffffff;
 constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); more -> ordered re-walk
 struct Bvh4Node {
-  float lo[3][4];         // lo[axis][child]
-  float hi[3][4];
+  float lh[3][4][2];      // [axis][child] = {lo, hi}: both slab planes of an axis in one 8-byte pair
+                          // (one packed FP32 FMA, v_pk_fma_f32, gives both slab distances)
   int32_t child[4];
 };
 static_assert(sizeof(Bvh4Node) == 112, "Bvh4Node layout");
@@ -103,7 +103,7 @@ struct SceneDev {
   const double* boxes;    // BOX_GEO doubles per box
   const Material* mat;
   const Bvh4Node* bvh;    // n_nodes nodes, root = 0
-  const float* bvh_sph32; // 4 floats per slot {cx, cy, cz, R^2}, leaf order
+  const float* bvh_sph32; // 16 floats per leaf (4 slots): {cx 0..3}, {cy 0..3}, {cz 0..3}, {R^2 0..3}
   const Sphere64* bvh_sph64; // binary64 record per slot
   const int32_t* bvh_obj; // slot -> global (YAML) object index (-1 = padding)
   const int32_t* sph_obj; // sphere record -> global (YAML) object index
