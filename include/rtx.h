@@ -279,7 +279,10 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          shadow walks and shading on full waves, 0 off, -1 [default] = on whenever the rings fit the walk's
          LDS; same bits), "lv_streams" (bounce levels: the region's 8x8 tiles in this many interleaved parts,
          1..4, rendered at once on as many HIP streams, parts 1.. on streams the context owns; one part's level
-         tails and reductions overlap the others' work; 2 [default]; same bits). */
+         tails and reductions overlap the others' work; 2 [default]; same bits), "lv_grid_div" (bounce levels:
+         level grids = resident workgroups / this, 1 [default]), "lv_redo_blocks" (bounce levels: at most this
+         many workgroups for the lanes-engine re-render of overflowed samples, launched after every batch and
+         nearly always empty; 8 [default], 0 = every resident workgroup; same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

@@ -83,6 +83,7 @@ struct rtx_context {
   int64_t opt_lv_static = -1;        // bounce levels: % of a launch's chunks scheduled statically (-1 auto)
   int64_t opt_lv_compact = -1;       // bounce levels: 1 = park hits in an LDS ring and shade full waves, -1 auto (when it fits)
   int64_t opt_lv_grid_div = 1;       // bounce levels: persistent level grids = resident workgroups / this
+  int64_t opt_lv_redo_blocks = 8;    // bounce levels: workgroups of the overflow re-render launch (0: all resident)
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
@@ -407,7 +408,8 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"kernel_events", c->opt_kernel_events}, {"lv_batch", c->opt_lv_batch},
       {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor},
       {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact},
-      {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div}};
+      {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
+      {"lv_redo_blocks", c->opt_lv_redo_blocks}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -484,6 +486,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_grid_div")) {       // bounce levels: level grids = resident workgroups / this
     if (value < 1 || value > 8) return fail(c, RTX_EINVAL, "lv_grid_div must be in [1, 8]");
     c->opt_lv_grid_div = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_redo_blocks")) {    // bounce levels: overflow re-render grid cap, 0 = all resident
+    if (value < 0 || value > (1 << 20)) return fail(c, RTX_EINVAL, "lv_redo_blocks must be in [0, 2^20]");
+    c->opt_lv_redo_blocks = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_streams")) {        // bounce levels: tiles in this many interleaved parts on as many streams
@@ -895,7 +902,8 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   carve(p, buf);
   p.lv_split = split ? 1 : 0;
   p.lv_compact = (int32_t)c->opt_lv_compact;
-  p.lv_grid_div = (int32_t)c->opt_lv_grid_div;   // the launcher turns it off when the rings do not fit LDS
+  p.lv_grid_div = (int32_t)c->opt_lv_grid_div;
+  p.lv_redo_blocks = (int32_t)c->opt_lv_redo_blocks;   // the launcher turns it off when the rings do not fit LDS
   // Static chunks cost no atomics; dynamic claims balance rays of very
   // different cost.  Auto: all static while the sphere records fit one walk
   // workgroup's LDS with room to spare (C2: 5.35 vs 5.9 ms at 50 %), half

@@ -691,6 +691,12 @@ static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   const long need = ((long)nwork + BS - 1) / BS;
   long blocks = std::min<long>(need, (long)cus * per_cu);
   blocks = std::min<long>(blocks, (long)p.stk_glb_lanes / BS);   // lanes with a global ray-stack region
+  // The re-render of overflowed samples (SRC_LIST) is launched after every
+  // batch and is nearly always empty; its grid is capped (option
+  // lv_redo_blocks) so that it does not wait for a whole chip's worth of CUs
+  // that another stream's level launch holds (the batch's tree reduction
+  // waits behind it).
+  if (SRC == SRC_LIST && p.lv_redo_blocks > 0) blocks = std::min<long>(blocks, p.lv_redo_blocks);
   if (blocks <= 0) return hipSuccess;
   if (!g_work_zeroed) e = hipMemsetAsync(p.work, 0, sizeof(int), s);
   if (e != hipSuccess) return e;

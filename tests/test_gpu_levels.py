@@ -102,6 +102,8 @@ def test_levels_match_golden(gpu, name):
     dict(lv_stage_pct=5, lv_floor=0),                    # staging overflow: re-rendered by the lanes engine
     dict(lv_rec_pct=101, lv_floor=0),                    # tree-record overflow at level 1
     dict(lv_batch=1000, lv_stage_pct=20, lv_rec_pct=150, lv_floor=0),
+    dict(lv_stage_pct=5, lv_floor=0, lv_redo_blocks=1),  # the re-render on a single workgroup
+    dict(lv_stage_pct=5, lv_floor=0, lv_redo_blocks=0),  # ... on every resident workgroup
 ])
 def test_levels_batches_and_overflow_change_no_bit(gpu, opts):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)

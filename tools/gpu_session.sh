@@ -5,13 +5,21 @@
 #       quick          = tests + bench
 #       pmc            = PMC passes + bench + kernel-trace stats
 #       bench          = bench + kernel-trace stats
+#       levels         = the bounce-level GPU tests only
+#       timing         = option sweep: bash tools/gpu_session.sh TAG timing SCENE REPS SHARE OPT...
+#                        (SHARE = k/N for one rank's share, or - for the whole frame; each OPT a JSON
+#                        option set; output $OUT/timing_SCENE[_shareN].log)
+#       stamps         = phase stamps of the levels engine (diagnostic build _variants/librtx_stamps.so):
+#                        bash tools/gpu_session.sh TAG stamps SCENE OPT...   (OPT as key=value)
 # ENGINE: rtx engine option for the PMC passes (0 lanes, 1 levels; default: the library default)
 # Every GPU step has its own time limit; steps are chained with && (stop at the first failure).
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-r02}
 MODE=${2:-full}
-ENGINE=${3:-}
+shift 2 2>/dev/null || shift $#
+ENGINE=
+if [ "$MODE" != timing ] && [ "$MODE" != stamps ]; then ENGINE=${1:-}; fi
 OUT=gpurun_out/$TAG
 mkdir -p $OUT profiles
 ENGOPT='{}'
@@ -60,7 +68,25 @@ bench_c4() {
   timeout -k 10 600 python bench.py --workload c4 --steps 3 --warmup 1 > $OUT/bench_c4.json 2> $OUT/bench_c4.err
 }
 
+levels() {
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_levels.py -x -v --timeout 120 --timeout-method thread > $OUT/pytest_levels.log 2>&1
+}
+timing() {  # SCENE REPS SHARE OPT...
+  local scene=$1 reps=$2 share=$3; shift 3
+  local log=$OUT/timing_$scene.log sh=()
+  if [ "$share" != - ]; then sh=(--share $share); log=$OUT/timing_${scene}_share${share#*/}.log; fi
+  timeout -k 10 300 python3 tools/timing.py --scene $scene --reps $reps "${sh[@]}" "$@" >> $log 2>&1
+}
+stamps() {  # SCENE OPT...
+  local scene=$1; shift
+  RTX_LIB=_variants/librtx_stamps.so timeout -k 10 120 python3 tools/stamps_levels.py $scene "$@" \
+    > $OUT/stamps_${scene}_$(echo "$@" | tr ' =' '_-').log 2>&1
+}
+
 case $MODE in
+  levels) levels ;;
+  timing) timing "$@" ;;
+  stamps) stamps "$@" ;;
   full)  tests && smoke && pmc && bench && bench_c4 ;;
   quick) tests && timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err ;;
   pmc)   pmc && bench ;;
