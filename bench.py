@@ -142,12 +142,16 @@ def stub_main(args, world, rank):
     if world > 1:
         dist.init_process_group("gloo")
         assert dist.get_world_size() == args.gpus
-    df = DistributedFrame(W, H, TILE_ROWS, rank, world, "cpu")
+    df = DistributedFrame(W, H, TILE_ROWS, rank, world, "cpu", buffers=2)
     ys = torch.as_tensor(rank_rows(H, TILE_ROWS, rank, world), dtype=torch.float64)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    pending, frame = [], None
+    for _ in range(args.steps):                # the GPU bench's pipelined step
         df.packed.copy_(ys[:, None, None].expand_as(df.packed))
-        frame = df.gather()
+        if pending:
+            frame = df.gather_finish(pending.pop())
+        pending.append(df.gather_start())
+    frame = df.gather_finish(pending.pop())
     elapsed = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -263,11 +267,27 @@ def main():
         def step():
             share_step(*emulate)
     else:
-        df = DistributedFrame(W, H, TILE_ROWS, rank, world, dev)
+        # Frame i's gather overlaps frame i + 1's render (two packed buffers):
+        # step i renders frame i, then finishes frame i - 1's gather (rank 0
+        # unpacks it), then starts frame i's.  drain() finishes the last one
+        # before the timed region closes, so all K frames are rendered AND
+        # gathered inside it.
+        df = DistributedFrame(W, H, TILE_ROWS, rank, world, dev, buffers=2)
+        pending = []
 
         def step():
             r.render_tiles_device(df.packed.data_ptr(), TILE_ROWS, rank, world, seed=1, stream=sp)
-            df.gather()
+            if pending:
+                df.gather_finish(pending.pop())
+            pending.append(df.gather_start())
+
+        def drain():
+            while pending:
+                df.gather_finish(pending.pop())
+
+    if world == 1:
+        def drain():
+            pass
 
     def barrier():
         if world > 1:
@@ -276,6 +296,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    drain()
     barrier()
     r.sync(sp)                              # raises if a reference raise site fired
 
@@ -284,6 +305,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
+    drain()
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0

@@ -1060,41 +1060,12 @@ __device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, 
   return lv_tree_sum(p, base, pex, item, nlev, lo, hi, st, sd, e);
 }
 
-// Camera#render_at's reduction (camera.rb:70-99) of pass 0: one 256-thread
-// block per 8x8 tile of the batch.  The block's threads sum the tile's
-// 64 x pre sample trees (item order (pixel, sample): a wave's trees are
-// neighbours), park colour and raise in LDS, then 64 threads do the pixels:
-// mean in sample order, the variance test, then the pixel or (max_sample_times
-// > pre) an extra-list entry with the pre mean parked in the output.
-// Dynamic LDS: nlev * 64 slice offsets, SD * 2 words of walk stack per thread,
-// then 64 * pre samples.
-template <int SD>
-__global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
-  __shared__ uint32_t base[LV_MAXL + 1];
-  extern __shared__ uint32_t lds_fin[];
-  uint32_t* pex = lds_fin;
-  lv_layout(p, nlev, base, pex);
+// render_at's per-pixel stage of pass 0 (camera.rb:70-99) once a tile's
+// 64 x pre sample colours / raises are in LDS (scol, serr): 64 threads, one
+// per pixel of the tile.
+__device__ __forceinline__ void lv_tile_pixels(const KParams& p, const double* scol, const uint32_t* serr) {
   const int pre = p.pre;
-  const int slot = blockIdx.x;                 // tile of the batch
-  uint32_t* lo = lds_fin + nlev * 64 + threadIdx.x;
-  uint32_t* hi = lo + SD * 256;
-  double* scol = reinterpret_cast<double*>(lds_fin + nlev * 64 + (SD > 16 ? 0 : 2 * SD * 256));   // 64 * pre * 3
-  uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
-  uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];  // deep trees: private stack
-  const int n_items = 64 * pre;
-  const int item0 = slot * n_items;
-  for (int it = (int)threadIdx.x; it < n_items; it += 256) {
-    const ItemPos ip = decode_item(p, item0 + it);
-    if (!ip.valid) continue;
-    uint32_t e = 0;
-    const V3 c = SD > 16 ? lv_sample(p, base, pex, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
-                         : lv_sample(p, base, pex, item0 + it, nlev, lo, hi, 256, SD, e);
-    scol[3 * it] = c.x;
-    scol[3 * it + 1] = c.y;
-    scol[3 * it + 2] = c.z;
-    serr[it] = e;
-  }
-  __syncthreads();
+  const int slot = blockIdx.x;
   const int l = (int)threadIdx.x;
   if (l >= 64) return;
   const int tiles_x = (p.nx + 7) >> 3;
@@ -1139,6 +1110,216 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
   o[1] = avg.y;
   o[2] = avg.z;
   if (err) record_error(p.err, err, px_key(x, y, cam.height));
+}
+
+// Camera#render_at's reduction (camera.rb:70-99) of pass 0: one 256-thread
+// block per 8x8 tile of the batch.  The block's threads sum the tile's
+// 64 x pre sample trees (item order (pixel, sample): a wave's trees are
+// neighbours), park colour and raise in LDS, then 64 threads do the pixels:
+// mean in sample order, the variance test, then the pixel or (max_sample_times
+// > pre) an extra-list entry with the pre mean parked in the output.
+// Dynamic LDS: nlev * 64 slice offsets, SD * 2 words of walk stack per thread,
+// then 64 * pre samples.
+template <int SD>
+__global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
+  extern __shared__ uint32_t lds_fin[];
+  uint32_t* pex = lds_fin;
+  lv_layout(p, nlev, base, pex);
+  const int pre = p.pre;
+  const int slot = blockIdx.x;                 // tile of the batch
+  uint32_t* lo = lds_fin + nlev * 64 + threadIdx.x;
+  uint32_t* hi = lo + SD * 256;
+  double* scol = reinterpret_cast<double*>(lds_fin + nlev * 64 + (SD > 16 ? 0 : 2 * SD * 256));   // 64 * pre * 3
+  uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
+  uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];  // deep trees: private stack
+  const int n_items = 64 * pre;
+  const int item0 = slot * n_items;
+  for (int it = (int)threadIdx.x; it < n_items; it += 256) {
+    const ItemPos ip = decode_item(p, item0 + it);
+    if (!ip.valid) continue;
+    uint32_t e = 0;
+    const V3 c = SD > 16 ? lv_sample(p, base, pex, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
+                         : lv_sample(p, base, pex, item0 + it, nlev, lo, hi, 256, SD, e);
+    scol[3 * it] = c.x;
+    scol[3 * it + 1] = c.y;
+    scol[3 * it + 2] = c.z;
+    serr[it] = e;
+  }
+  __syncthreads();
+  lv_tile_pixels(p, scol, serr);
+}
+
+// The same reduction with the tile's trees gathered into LDS first (option
+// lv_fin_cap > 0).  k_tree_finalize's walks are chains of dependent global
+// loads, one per visited record (the next record is known only once the
+// current one has arrived), and a wave runs as many steps as its largest
+// tree: the kernel spent ~80 % of its wave time waiting (r03k).  Here the
+// block copies its 64 x pre trees into LDS level by level: level 0 is the
+// tile's items, and level d + 1 is the children of level d, placed by a block
+// prefix count over the parents in LDS order (so a parent's children stay
+// contiguous and in slot order, as in the level queues) and loaded by the
+// parent's thread; every load of a level is in flight at once, so the
+// block waits nlev round trips in all.  Then each thread walks its trees in
+// LDS exactly as lv_tree_sum does (pre-order, children in reverse slot order,
+// the same additions in the same order: the same bits).  A tile whose trees
+// do not fit `cap` records falls back to the global walk (lv_tree_sum).
+//
+// Dynamic LDS: nlev * 64 slice offsets | 64 * pre colours (24 B) + raises
+// (4 B) | SD * 256 walk-stack words | cap first-child indices (u16) | cap
+// records (lv_rec_bytes each; the fallback's walk stacks alias them).
+__host__ __device__ __forceinline__ size_t lv_fin_g_rec_off(int nlev, int pre, int sd, int cap) {
+  const size_t o = (size_t)nlev * 64 * 4;
+  return (((o + 7) & ~(size_t)7) + (size_t)64 * pre * 28 + (size_t)sd * 256 * 4 + (size_t)cap * 2 + 15) &
+         ~(size_t)15;
+}
+
+// lv_tree_sum over the tree copied into LDS (record `root` of level 0).  The
+// pending child ranges (lo | hi << 16) are LDS words stk[k * 256], k < SD
+// (a register array indexed by the stack depth would live in scratch).
+template <int SD>
+__device__ __forceinline__ V3 lv_tree_sum_lds(const char* recs, const uint16_t* kid, uint32_t* stk, int rb, int root,
+                                              int nlev, uint32_t& err_out) {
+  int sp = 0;
+  V3 sum = v3(0.0, 0.0, 0.0);
+  uint32_t err = 0;
+  bool gt1 = false;
+  int lev = 0;
+  uint32_t q = (uint32_t)root;
+  while (true) {
+    const char* rec = recs + (size_t)q * rb;
+    const uint32_t hx = *reinterpret_cast<const uint32_t*>(rec);
+    const double* lf = reinterpret_cast<const double*>(rec + 8);
+    if (!err) err = hx & 0xffu;
+    const int nleaf = (int)(hx >> 8 & 0xffu);
+    for (int k = 0; k < nleaf; k++) {         // rt_reduce (ray_tracer.rb:292-298), in emission order
+      sum = vadd(sum, v3(lf[3 * k], lf[3 * k + 1], lf[3 * k + 2]));
+      if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) gt1 = true;
+    }
+    const uint32_t nch = (uint32_t)__popc(hx >> 16);
+    if (nch && lev + 1 < nlev && sp < SD) {
+      const uint32_t c0 = kid[q];
+      stk[sp * 256] = c0 | (c0 + nch) << 16;
+      sp++;
+    }
+    // next: the last unvisited child of the deepest pending range (LIFO pop)
+    uint32_t e = 0;
+    while (sp > 0) {
+      e = stk[(sp - 1) * 256];
+      if ((e & 0xffffu) != e >> 16) break;
+      sp--;
+    }
+    if (sp == 0) break;
+    e -= 1u << 16;
+    stk[(sp - 1) * 256] = e;
+    q = e >> 16;
+    lev = sp;
+  }
+  err_out = err ? err : (gt1 ? (uint32_t)ERR_COLOR_GT1 : 0u);
+  return sum;
+}
+
+template <int SD>
+__global__ __launch_bounds__(256) void k_tree_finalize_g(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
+  __shared__ uint32_t wpart[4];
+  extern __shared__ uint32_t lds_fin[];
+  uint32_t* pex = lds_fin;
+  lv_layout(p, nlev, base, pex);
+  const int pre = p.pre, cap = p.lv_fin_cap, rb = p.lv_rec_bytes;
+  const int n_items = 64 * pre;
+  const int item0 = blockIdx.x * n_items;
+  const int tid = (int)threadIdx.x, wave = tid >> 6, lane = (int)__lane_id();
+  char* lb = reinterpret_cast<char*>(lds_fin);
+  double* scol = reinterpret_cast<double*>(lb + (((size_t)nlev * 64 * 4 + 7) & ~(size_t)7));
+  uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
+  uint32_t* stk = serr + n_items + tid;
+  uint16_t* kid = reinterpret_cast<uint16_t*>(serr + n_items + SD * 256);
+  char* recs = lb + lv_fin_g_rec_off(nlev, pre, SD, cap);
+  const int nq = rb >> 4;                      // 16-B words per record
+  const uint32_t log2cap = (uint32_t)p.lv_slice_log2, smask = (1u << log2cap) - 1u;
+  bool fits = n_items <= cap;
+  // ---- level 0: the tile's items (padding and re-rendered samples: no tree)
+  if (fits) {
+    for (int it = tid; it < n_items; it += 256) {
+      const int item = item0 + it;
+      uint4* dst = reinterpret_cast<uint4*>(recs + (size_t)it * rb);
+      if (decode_item(p, item).valid && p.lv_redo_of[item] < 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(p.lv_rec + (size_t)(base[0] + item) * rb);
+        for (int w = 0; w < nq; w++) dst[w] = src[w];
+      } else {
+        dst[0] = make_uint4(0u, 0u, 0u, 0u);   // no leaves, no children
+      }
+    }
+  }
+  __syncthreads();
+  // ---- level d + 1: the children of level d's records [lo, hi)
+  int lo = 0, hi = n_items;
+  for (int d = 0; fits && d + 1 < nlev; d++) {
+    const int n = hi - lo;
+    const int m = (n + 255) >> 8;              // parents per thread, a contiguous run
+    const int a = lo + tid * m, b = min(a + m, hi);
+    uint32_t cnt = 0;
+    for (int k = a; k < b; k++) cnt += (uint32_t)__popc(*reinterpret_cast<const uint32_t*>(recs + (size_t)k * rb) >> 16);
+    const uint32_t incl = wave_scan_incl(cnt);
+    if (lane == 63) wpart[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const uint32_t v = wpart[w];
+      before += w < wave ? v : 0u;
+      total += v;
+    }
+    __syncthreads();                           // wpart is reused by the next level
+    if (total == 0) break;
+    if (hi + (int)total > cap) {               // uniform: the tile's trees do not fit
+      fits = false;
+      break;
+    }
+    uint32_t pos = (uint32_t)hi + before + incl - cnt;
+    for (int k = a; k < b; k++) {
+      const uint2 hdr = *reinterpret_cast<const uint2*>(recs + (size_t)k * rb);
+      const uint32_t nch = (uint32_t)__popc(hdr.x >> 16);
+      kid[k] = (uint16_t)pos;
+      if (!nch) continue;
+      // the children's slot -> their dense index at level d + 1 (as lv_tree_sum)
+      const uint32_t c0 = pex[(d + 1) * 64 + (hdr.y >> log2cap)] + (hdr.y & smask);
+      const uint4* src = reinterpret_cast<const uint4*>(p.lv_rec + (size_t)(base[d + 1] + c0) * rb);
+      uint4* dst = reinterpret_cast<uint4*>(recs + (size_t)pos * rb);
+      for (uint32_t w = 0; w < nch * (uint32_t)nq; w++) dst[w] = src[w];
+      pos += nch;
+    }
+    __syncthreads();
+    lo = hi;
+    hi += (int)total;
+  }
+  // ---- the sums, in trace_sync's order
+  uint32_t* slo = reinterpret_cast<uint32_t*>(recs) + tid;   // fallback walk stacks (alias the records)
+  uint32_t* shi = slo + SD * 256;
+  if (!fits) __syncthreads();                  // every thread is past its last read of the records
+  for (int it = tid; it < n_items; it += 256) {
+    const int item = item0 + it;
+    if (!decode_item(p, item).valid) continue;
+    uint32_t e = 0;
+    V3 c;
+    const int r = p.lv_redo_of[item];
+    if (r >= 0) {
+      const double* q = p.lv_redo_smp + (size_t)r * 4;
+      e = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
+      c = v3(q[0], q[1], q[2]);
+    } else if (fits) {
+      c = lv_tree_sum_lds<SD>(recs, kid, stk, rb, it, nlev, e);
+    } else {
+      c = lv_tree_sum(p, base, pex, item, nlev, slo, shi, 256, SD, e);
+    }
+    scol[3 * it] = c.x;
+    scol[3 * it + 1] = c.y;
+    scol[3 * it + 2] = c.z;
+    serr[it] = e;
+  }
+  __syncthreads();
+  lv_tile_pixels(p, scol, serr);
 }
 
 // Pass 1: one thread per extra-list entry of the batch: (pre mean * pre +
@@ -1331,7 +1512,34 @@ static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStrea
   return hipGetLastError();
 }
 
+// Pass 0 with the trees gathered into LDS (lv_fin_cap > 0; register walk
+// stacks of SD entries, nlev - 1 <= SD).
+template <int SD>
+static hipError_t launch_finalize_g(KParams q, int nlev, int n, hipStream_t s) {
+  // at most as many records as fit a CU's LDS next to the rest
+  // (the kernel's static LDS, and 16 B for the alignment of the record area)
+  hipFuncAttributes fa{};
+  size_t stat = 16 * 1024;
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_tree_finalize_g<SD>)) == hipSuccess)
+    stat = fa.sharedSizeBytes;
+  const size_t fixed = lv_fin_g_rec_off(nlev, q.pre, SD, 0) + stat + 16;
+  const long fit = fixed < LDS_TOTAL_BYTES ? (long)((LDS_TOTAL_BYTES - fixed) / (q.lv_rec_bytes + 2)) : 0;
+  q.lv_fin_cap = (int32_t)std::min<long>(q.lv_fin_cap, fit);
+  const size_t recs = (size_t)q.lv_fin_cap * q.lv_rec_bytes;
+  const size_t lds = lv_fin_g_rec_off(nlev, q.pre, SD, q.lv_fin_cap) + std::max(recs, (size_t)SD * 2 * 256 * 4);
+  if (lds + stat > LDS_TOTAL_BYTES) return launch_finalize_sd<16>(q, nlev, n, s);   // (pre too large: the walk)
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tree_finalize_g<SD>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_tree_finalize_g<SD>, dim3((unsigned)n), dim3(256), lds, s, q, nlev);
+  return hipGetLastError();
+}
+
 static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t s) {
+  if (q.lv_pass == 0 && q.lv_fin_cap > 0) {
+    if (nlev <= 5) return launch_finalize_g<4>(q, nlev, n, s);
+    if (nlev <= 9) return launch_finalize_g<8>(q, nlev, n, s);
+  }
   // a walk keeps one pending child range per level below the root: nlev - 1
   // entries; the smaller stack lets 8 blocks share a CU (C2, depth 5) instead of 6
   if (nlev <= 5) return launch_finalize_sd<4>(q, nlev, n, s);

@@ -65,15 +65,25 @@ class DistributedFrame:
     """One rank's share of tile-sharded rendering + the RCCL gather to rank 0.
 
     Needs an initialized torch.distributed process group (``nccl`` = RCCL on
-    ROCm, or ``gloo`` for CPU tests).  ``render_fn(packed)`` must fill this
-    rank's packed buffer ([rows_per_rank, W, 3] float64)."""
+    ROCm, or ``gloo`` for CPU tests).  The caller renders this rank's tiles
+    into ``packed`` ([rows_per_rank, W, 3] float64), then either ``gather()``
+    (blocking) or, to overlap frame i's gather with frame i + 1's render,
+    ``h = gather_start()`` ... render the next frame into the new ``packed``
+    ... ``gather_finish(h)``.  With ``buffers=2`` the packed buffers alternate,
+    so the render of frame i + 1 never writes the buffer frame i's gather
+    reads; rank 0's unpack of frame i is queued on the caller's stream before
+    the gather of frame i + 1 is issued (a collective waits for the stream it
+    is issued from), so the single receive buffer is never overwritten early."""
 
-    def __init__(self, width, height, tile_rows, rank, nranks, device):
+    def __init__(self, width, height, tile_rows, rank, nranks, device, buffers=1):
         import torch
         self.width, self.height = width, height
         self.tile_rows, self.rank, self.nranks = tile_rows, rank, nranks
         self.rows = rows_per_rank(height, tile_rows, nranks)
-        self.packed = torch.zeros((self.rows, width, 3), dtype=torch.float64, device=device)
+        self.bufs = [torch.zeros((self.rows, width, 3), dtype=torch.float64, device=device)
+                     for _ in range(max(1, buffers))]
+        self._i = 0
+        self.packed = self.bufs[0]
         self.gathered = None
         if rank == 0:
             self.gathered = torch.zeros((nranks * self.rows, width, 3), dtype=torch.float64, device=device)
@@ -82,18 +92,31 @@ class DistributedFrame:
             self.dst = torch.as_tensor(dst, device=device)
             self.frame = torch.zeros((height, width, 3), dtype=torch.float64, device=device)
 
-    def gather(self):
-        """ONE collective: every rank's packed tiles to rank 0; rank 0 returns the frame."""
+    def gather_start(self):
+        """Start ONE collective (every rank's packed tiles to rank 0) without
+        waiting for it, and move ``packed`` to the next buffer."""
         import torch.distributed as dist
-        if self.nranks == 1:
-            chunks = None
-            self.gathered = self.packed
-        elif self.rank == 0:
-            chunks = list(self.gathered.chunk(self.nranks, 0))
-            dist.gather(self.packed, chunks, dst=0)
-        else:
-            dist.gather(self.packed, None, dst=0)
+        buf = self.packed
+        work = None
+        if self.nranks > 1:
+            chunks = list(self.gathered.chunk(self.nranks, 0)) if self.rank == 0 else None
+            work = dist.gather(buf, chunks, dst=0, async_op=True)
+        self._i = (self._i + 1) % len(self.bufs)
+        self.packed = self.bufs[self._i]
+        return work, buf
+
+    def gather_finish(self, handle):
+        """Wait for a started gather (the caller's stream waits for it); rank 0
+        unpacks the rows and returns the frame."""
+        work, buf = handle
+        if work is not None:
+            work.wait()
         if self.rank == 0:
-            self.frame.index_copy_(0, self.dst, self.gathered.index_select(0, self.src))
+            src = buf if self.nranks == 1 else self.gathered
+            self.frame.index_copy_(0, self.dst, src.index_select(0, self.src))
             return self.frame
         return None
+
+    def gather(self):
+        """ONE collective: every rank's packed tiles to rank 0; rank 0 returns the frame."""
+        return self.gather_finish(self.gather_start())

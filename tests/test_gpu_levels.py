@@ -382,3 +382,33 @@ def test_two_streams_c2_full_frame_and_kernel_time(gpu):
     r.render()
     ms, launches = r.kernel_time()
     assert launches == 10 and 0.5 < ms < 50.0, (ms, launches)   # union of the two halves' level launches
+
+
+# ---- tree reduction with the tile's trees gathered into LDS (option lv_fin_cap)
+@pytest.mark.parametrize("world,camera,ov", [
+    ("c2_world.yml", "c2_camera.yml", dict(width=120, height=70)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, monte_carlo_diffusion_times=3, trace_depth=6)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, pre_sample_times=2, max_sample_times=5,
+                                             variant_threshold=0.0)),
+])
+def test_gathered_reduction_changes_no_bit(gpu, world, camera, ov):
+    """lv_fin_cap: LDS gather (default), a cap that makes some tiles fall back
+    to the global walk, one below a tile's level 0 (every tile falls back), and
+    the global walk alone (0) render the same bits as the lanes engine."""
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=4)
+    for cap in (1024, 4096, 300, 100, 0):
+        r = _renderer(sd, cd, 1, lv_fin_cap=cap)
+        assert _same(r.render(seed=4), lanes), cap
+        r.close()
+
+
+def test_gathered_reduction_with_overflow(gpu):
+    """Re-rendered samples (their trees are not followed) inside gathered tiles."""
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
+    lanes = _renderer(sd, cd, 0).render(seed=6)
+    for cap in (1024, 300):
+        r = _renderer(sd, cd, 1, lv_fin_cap=cap, lv_stage_pct=5, lv_floor=0)
+        assert _same(r.render(seed=6), lanes), cap
+        assert r.level_stats()["redo"] > 0
+        r.close()

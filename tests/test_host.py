@@ -264,6 +264,55 @@ def test_distributed_gather_gloo_world2():
     assert np.array_equal(frame, ref)
 
 
+def _gloo_pipeline_worker(rank, world, port, H, W, tr, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    df = tiles.DistributedFrame(W, H, tr, rank, world, "cpu", buffers=2)
+    ys = torch.as_tensor(tiles.rank_rows(H, tr, rank, world), dtype=torch.float64)
+    frames, pending = [], []
+    for i in range(5):                          # bench.py's pipelined step: frame i = row index + 1000 i
+        df.packed.copy_((ys + 1000.0 * i)[:, None, None].expand_as(df.packed))
+        if pending:
+            f = df.gather_finish(pending.pop())
+            if rank == 0:
+                frames.append(f.clone().numpy())
+        pending.append(df.gather_start())
+    f = df.gather_finish(pending.pop())
+    if rank == 0:
+        frames.append(f.clone().numpy())
+        q.put(frames)
+    dist.destroy_process_group()
+
+
+def test_distributed_pipelined_gather_gloo_world3():
+    """Double-buffered asynchronous gather (frame i's gather overlaps frame
+    i + 1's render): every gathered frame is the one its ranks rendered."""
+    import multiprocessing as mp
+    import socket
+    H, W, tr, world = 37, 5, 8, 3
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_pipeline_worker, args=(r, world, port, H, W, tr, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    frames = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(frames) == 5
+    rows = np.repeat(np.arange(H, dtype=np.float64)[:, None], W, 1)
+    for i, f in enumerate(frames):
+        for c in range(3):
+            assert np.array_equal(f[:, :, c], rows + 1000.0 * i), i
+
+
 def test_bench_launches_its_own_ranks_gloo_stub():
     """bench.py --gpus 2 without torch.distributed.run starts the 2 ranks itself
     (launch_ranks), the world size is checked, the one gather runs and rank 0
