@@ -328,8 +328,24 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
   Ray refl, refr;
   bool has_refr = false;
   if (shade) {
-    refl = reflection(cur.ray, nn, c, hit, delta, errS);
-    if (may_refract) has_refr = refraction(cur.ray, nn, c, hit, refl.d, rate, refr, errS) && (mask & 2u);
+    // intersect_parameters builds both rays for every hit (sphere.rb:88-101,
+    // world_object.rb:121-137), and their normalizes can raise.  A child that
+    // the cutoff drops (mask bit clear: always at the last level) needs only
+    // those raises: the zero-vector test of its normalize (vnorm's own test,
+    // sqrt(s) == 0 iff s == 0), not its direction.  The refraction's test
+    // needs the reflected direction, so the reflection is built in full then.
+    const bool refr_live = (mask & 2u) != 0;
+    const bool refr_chk = may_refract && !refr_live && !(sqrt(1.0 - c * c) / rate >= 1);   // refraction()'s TIR test
+    if ((mask & 1u) || refr_live || refr_chk) {
+      refl = reflection(cur.ray, nn, c, hit, delta, errS);
+    } else if (vr(vadd(vsc(nn, 2.0 * c * vr(cur.ray.d)), cur.ray.d)) == 0) {
+      if (!errS) errS = ERR_ZERO_VEC;
+    }
+    if (refr_live) {
+      has_refr = refraction(cur.ray, nn, c, hit, refl.d, rate, refr, errS);
+    } else if (refr_chk && vr(vadd(refl.d, cur.ray.d)) == 0) {
+      if (!errS) errS = ERR_ZERO_VEC;
+    }
     if (nl != 0) {
       // WorldObject#local_lighting's colour (world_object.rb:51-74), texture filter
       lc = vdiv(lc, (double)nl);
@@ -382,8 +398,11 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
     };
     if (mask & 1u) put(refl, vmul(cur.att, v3p(m->refl_att)), cur.path * R + 1);
     if (has_refr) put(refr, vmul(cur.att, v3p(m->refr_att)), cur.path * R + 2);
-    if (nl == 0) {
-      // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
+    if (nl == 0 && (mask >> 2) != 0) {
+      // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta.
+      // Skipped when every path-tracing child is cut off: its only raise
+      // sites (vertical_vector's zero test, the normalize of a vector with a
+      // component 1) cannot fire unless n.normalize raised first (errS).
       const V3 att = vmul(cur.att, vdiv(v3p(m->diffuse), (double)pt));
       const V3 left = vnorm(vertical_vector(nrm, errP), errP);
       const V3 up = vcross(nn, left);

@@ -412,3 +412,76 @@ def test_gathered_reduction_with_overflow(gpu):
         assert _same(r.render(seed=6), lanes), cap
         assert r.level_stats()["redo"] > 0
         r.close()
+
+
+# ---- raises of children the cutoff drops (lv_finish builds only their normalize tests)
+HEADON_WORLD = """max_distance: 10000
+soft_shadow_exponent: 2
+lights:
+  - type: Spot
+    properties:
+      name: side
+      position: [2.0, -30.0, 4.0]
+      radius: 0.0
+      color: [1.0, 1.0, 1.0]
+      high_light_rate: 1.0
+      high_light_angle: 0.5
+world_objects:
+  - type: Plane
+    properties:
+      name: pane
+      point: [5.0, 0, 0]
+      front: [-1, 0, 0]
+      up: [0, 0, 1]
+      refractive_rate: 1.5
+      diffuse_rate: [0.3, 0.3, 0.3]
+      ambient: [0.02, 0.02, 0.02]
+      reflective_attenuation: [%s]
+      refractive_attenuation: [%s]
+"""
+HEADON_CAMERA = """position: [0.0, 0.0, 0.0]
+up: [0.0, 0.0, 1.0]
+front: [1.0, 0.0, 0.0]
+retina_width: 0.5
+retina_height: 0.5
+aperture_radius: 0.0
+image_distance: 1.0
+focal_distance: 0.5
+width: 4
+height: 4
+pre_sample_times: 1
+max_sample_times: 1
+variant_threshold: 0.001
+trace_depth: %d
+monte_carlo_diffusion_times: 1
+"""
+
+
+@pytest.mark.parametrize("refl,refr,depth", [
+    ("0.5, 0.5, 0.5", "0.0, 0.0, 0.0", 2),   # refraction child dead: only its normalize test runs
+    ("0.5, 0.5, 0.5", "0.5, 0.5, 0.5", 1),   # depth 1: both children dead
+    ("0.0, 0.0, 0.0", "0.0, 0.0, 0.0", 2),   # both dead by attenuation
+    ("0.5, 0.5, 0.5", "0.5, 0.5, 0.5", 2),   # both alive: the full rays
+])
+def test_dead_child_raises_match_lanes_and_oracle(gpu, tmp_path, refl, refr, depth):
+    """Pixel (2, 2)'s ray is exactly (1, 0, 0) and meets the pane head-on: the
+    refraction's (reflection + ray.front).normalize is a zero vector
+    (world_object.rb:133), which raises whether or not the refraction ray
+    survives the cutoff.  Both engines (and split phases) report the same
+    raise at the same pixel as the oracle."""
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import RtxError
+    from oracle.c_oracle import Oracle
+    w, c = tmp_path / "w.yml", tmp_path / "c.yml"
+    w.write_text(HEADON_WORLD % (refl, refr))
+    c.write_text(HEADON_CAMERA % depth)
+    sd, cd = config.load_scene(str(w), str(c))
+    _, status, rc = Oracle(sd, cd).render()
+    assert status[2, 2] != 0 and rc != 0
+    msgs = []
+    for engine, opts in ((0, {}), (1, {}), (1, dict(lv_split=1)), (1, dict(lv_compact=0))):
+        with pytest.raises(RtxError) as e:
+            _renderer(sd, cd, engine, **opts).render()
+        assert e.value.kind == "zero_vec", (engine, opts, str(e.value))
+        msgs.append(str(e.value))
+    assert len(set(msgs)) == 1, msgs

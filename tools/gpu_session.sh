@@ -9,6 +9,7 @@
 #       timing         = option sweep: bash tools/gpu_session.sh TAG timing SCENE REPS SHARE OPT...
 #                        (SHARE = k/N for one rank's share, or - for the whole frame; each OPT a JSON
 #                        option set; output $OUT/timing_SCENE[_shareN].log)
+#       baseline       = BASELINE.md's table (tools/baseline_table.py: CPU restatement + 1-GPU + projections)
 #       stamps         = phase stamps of the levels engine (diagnostic build _variants/librtx_stamps.so):
 #                        bash tools/gpu_session.sh TAG stamps SCENE OPT...   (OPT as key=value)
 # ENGINE: rtx engine option for the PMC passes (0 lanes, 1 levels; default: the library default)
@@ -83,8 +84,13 @@ stamps() {  # SCENE OPT...
     > $OUT/stamps_${scene}_$(echo "$@" | tr ' =' '_-').log 2>&1
 }
 
+baseline() {
+  timeout -k 10 900 python3 tools/baseline_table.py $OUT > $OUT/baseline.log 2>&1
+}
+
 case $MODE in
   levels) levels ;;
+  baseline) baseline ;;
   timing) timing "$@" ;;
   stamps) stamps "$@" ;;
   full)  tests && smoke && pmc && bench && bench_c4 ;;
