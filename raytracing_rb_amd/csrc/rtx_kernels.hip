@@ -642,6 +642,8 @@ extern "C" int rtxdbg_read_stamps(unsigned long long* out, int reset) {   // dia
   if (read_level_stamps(lv, reset) != 0) return -1;
   for (int k = 0; k < 8; k++) out[k] += lv[k];
   for (int k = 8; k < 11; k++) out[k] = lv[k];   // (k_level: lanes with a ray / a walk / a hit)
+  if (lv[13])                                     // k_tree_finalize's phases (a levels-engine frame)
+    for (int k = 11; k < 14; k++) out[k] = lv[k];
   return 0;
 }
 

@@ -1144,7 +1144,9 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
   __shared__ uint32_t base[LV_MAXL + 1];
   extern __shared__ uint32_t lds_fin[];
   uint32_t* pex = lds_fin;
+  const unsigned long long ts0 = RTX_STAMPS ? stamp() : 0ull;   // RTX_STAMPS diagnostic build only
   lv_layout(p, nlev, base, pex);
+  const unsigned long long ts1 = RTX_STAMPS ? stamp() : 0ull;
   const int pre = p.pre;
   const int slot = blockIdx.x;                 // tile of the batch
   uint32_t* lo = lds_fin + nlev * 64 + threadIdx.x;
@@ -1164,6 +1166,14 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
     scol[3 * it + 1] = c.y;
     scol[3 * it + 2] = c.z;
     serr[it] = e;
+  }
+  if (RTX_STAMPS) {                           // layout / walks (wave lifetime parts), waves
+    const unsigned long long ts2 = stamp();
+    if (__lane_id() == 0) {
+      atomicAdd(&rtx_stamps[11], ts1 - ts0);
+      atomicAdd(&rtx_stamps[12], ts2 - ts1);
+      atomicAdd(&rtx_stamps[13], 1ull);
+    }
   }
   __syncthreads();
   lv_tile_pixels(p, scol, serr);
