@@ -23,6 +23,7 @@ struct ErrState {
 constexpr int LV_MAXL = 64;                     // levels (= trace_depth) the engine supports
 constexpr int LV_SLICES = 64;                   // slices per queue (one per lane of a consumer wave)
 constexpr int LV_CLAIMS = 16;                   // sharded chunk-claim counters per launch
+constexpr int LV_DONE = 16;                     // wave-completion counters per level launch (lv_level_done)
 struct LevelCtl {
   uint32_t count0;                              // level-0 items of the batch
   uint32_t redo_n;                              // level-0 items handed to the lanes engine (capacity overflow)
@@ -31,6 +32,13 @@ struct LevelCtl {
   uint32_t sc[LV_MAXL + 1][LV_SLICES * 32];     // rays allocated in slice s of level d: sc[d][32 s]
   uint32_t sh[LV_MAXL + 1][LV_SLICES * 32];     // split phases: hits of level d in slice s
   uint32_t claim[3][LV_MAXL + 1][LV_CLAIMS * 32]; // chunk claims: [launch kind: fused/trace, shadow, shade][level][j * 32]
+  // compact layout of level d (written by the last workgroup of the launch that allocated it)
+  uint32_t lay_cnt[LV_MAXL + 2][LV_SLICES];     // rays in slice s (clamped to the slice)
+  uint32_t lay_pex[LV_MAXL + 2][LV_SLICES];     // exclusive ray prefix of slice s
+  uint32_t lay_cin[LV_MAXL + 2][LV_SLICES];     // inclusive 64-ray chunk prefix of slice s
+  uint32_t lay_base[LV_MAXL + 2];               // first record of level d in the arena
+  uint32_t done[LV_MAXL + 2];                   // completed done_sub counters of the launch allocating level d
+  uint32_t done_sub[LV_MAXL + 1][LV_DONE * 32]; // finished waves w (w mod LV_DONE = j) of that launch: [d][32 j]
 };
 
 struct KParams {

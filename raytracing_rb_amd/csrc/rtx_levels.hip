@@ -125,25 +125,64 @@ struct LvQueue {
   }
 };
 
-// Dense ray count of level e (>= 1) of the batch (a wave reduction of its slices).
-__device__ __forceinline__ uint32_t lv_level_total(const KParams& p, int e) {
-  const int lane = (int)__lane_id();
-  const uint32_t cap = 1u << p.lv_slice_log2;
-  uint32_t c = p.lv_ctl->sc[e][lane * 32];
-  c = c < cap ? c : cap;
-  return (uint32_t)__shfl((int)wave_scan_incl(c), 63);
-}
+// Level d's first record in the arena (the dense counts of levels < d), from
+// the compact layout (lv_level_done).
+__device__ __forceinline__ uint32_t lv_base(const KParams& p, int level) { return p.lv_ctl->lay_base[level]; }
 
-// Level d's first record in the arena: the dense counts of levels < d.
-__device__ __forceinline__ uint32_t lv_base(const KParams& p, int level) {
-  uint32_t base = level > 0 ? p.lv_ctl->count0 : 0u;
-  for (int e = 1; e < level; e++) base += lv_level_total(p, e);
-  return base;
-}
-
+// A level's queue: level 0 is one dense slice; levels >= 1 read the compact
+// layout the launch that allocated them left (lv_level_done: three coalesced
+// 256-B loads, where reading the 64 slice counters, one per 128-B line, cost
+// every wave of every launch a 64-line gather from the same hot lines).
 __device__ __forceinline__ void lv_in_queue(const KParams& p, int level, LvQueue& q) {
-  if (level == 0) q.dense(p.lv_ctl->count0);
-  else q.sliced(p.lv_ctl->sc[level], 1u << p.lv_slice_log2, 1u);
+  if (level == 0) {
+    q.dense(p.lv_ctl->count0);
+    return;
+  }
+  const int lane = (int)__lane_id();
+  q.cnt = p.lv_ctl->lay_cnt[level][lane];
+  q.pex = p.lv_ctl->lay_pex[level][lane];
+  q.cin = p.lv_ctl->lay_cin[level][lane];
+  q.total = (uint32_t)__shfl((int)(q.pex + q.cnt), 63);
+  q.chunks = (uint32_t)__shfl((int)q.cin, 63);
+}
+
+// The end of a launch that allocated level e's rays (k_level, k_level_c,
+// k_lv_shade of level e - 1): the grid's last wave to finish writes level e's
+// compact layout: per slice the ray count (clamped to the slice), the
+// exclusive ray prefix and the inclusive 64-ray chunk prefix, and the first
+// record of level e + 1.  No barrier (a wave that is done leaves at once and
+// frees its SIMD slots) and no fence (a device-scope release fence writes
+// back the XCD's L2: 2048 of them cost C2 0.7 ms): wave w counts itself on
+// counter w mod LV_DONE (each on its own line), the wave that completes a
+// counter counts it on the top counter, and the wave that completes the top
+// counter is the last one.  Every slice allocation is a device-scope atomic
+// whose value its wave consumed before it got here, and the counts are
+// device-scope atomics too, all performed at the same coherence point: the
+// last wave's atomic loads see every allocation.  (The ray records are read
+// by later launches only: kernel boundaries order them.)
+__device__ __forceinline__ void lv_level_done(const KParams& p, int e) {
+  if (e > LV_MAXL) return;
+  const int lane = (int)__lane_id();
+  const uint32_t W = gridDim.x * (blockDim.x >> 6);
+  const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint32_t j = w % LV_DONE;
+  const uint32_t quota = W / LV_DONE + (j < W % LV_DONE ? 1u : 0u);
+  const uint32_t nsub = W < LV_DONE ? W : (uint32_t)LV_DONE;
+  uint32_t last = 0;
+  if (lane == 0) {
+    if (__hip_atomic_fetch_add(&p.lv_ctl->done_sub[e][j * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        quota - 1)
+      last = __hip_atomic_fetch_add(&p.lv_ctl->done[e], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsub - 1;
+  }
+  if (!__shfl((int)last, 0)) return;
+  const uint32_t cap = 1u << p.lv_slice_log2;
+  uint32_t c = __hip_atomic_load(&p.lv_ctl->sc[e][lane * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  c = c < cap ? c : cap;
+  const uint32_t incl = wave_scan_incl(c);
+  p.lv_ctl->lay_cnt[e][lane] = c;
+  p.lv_ctl->lay_pex[e][lane] = incl - c;
+  p.lv_ctl->lay_cin[e][lane] = wave_scan_incl((c + 63u) >> 6);
+  if (lane == 63) p.lv_ctl->lay_base[e + 1] = p.lv_ctl->lay_base[e] + incl;
 }
 
 // Chunk schedule of a launch: the first p.lv_static_pct % of the chunks
@@ -431,7 +470,7 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
 // Level `level` (0 .. trace_depth-1) of one batch in one launch (option
 // lv_split = 0).  Persistent, static chunk schedule.
 template <int SPH, int BS>
-__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level) {
+__device__ __forceinline__ void k_level_body(const KParams& p, int level) {
   const SceneDev& S = p.scene;
   extern __shared__ float4 lds_sph[];
   char* lds = reinterpret_cast<char*>(lds_sph);
@@ -555,6 +594,12 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
   }
 }
 
+template <int SPH, int BS>
+__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level) {
+  k_level_body<SPH, BS>(p, level);
+  lv_level_done(p, level + 1);
+}
+
 // ----------------------------------------------------------------- hit compaction
 // Option lv_compact.  In k_level the shading half of a chunk
 // (intersect_parameters, the shadow walks of local_lights, local_lighting and
@@ -578,7 +623,7 @@ constexpr int LV_RING_FIELDS = 11;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
 
 template <int SPH, int BS>
-__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
+__device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   const SceneDev& S = p.scene;
   extern __shared__ float4 lds_sph[];
   char* lds = reinterpret_cast<char*>(lds_sph);
@@ -775,6 +820,12 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int leve
   }
 }
 
+template <int SPH, int BS>
+__global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
+  k_level_c_body<SPH, BS>(p, level);
+  lv_level_done(p, level + 1);
+}
+
 // ----------------------------------------------------------------- split phases
 // Option lv_split = 1: every level runs as three launches,
 // each over a dense queue, so a wave's 64 lanes do the same phase of rt_map:
@@ -909,7 +960,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_shadow(KParams p, in
   }
 }
 
-__global__ __launch_bounds__(BS_SHADE, RTX_LV_SHADE_WPS) void k_lv_shade(KParams p, int level) {
+__device__ __forceinline__ void k_lv_shade_body(const KParams& p, int level) {
   const SceneDev& S = p.scene;
   const uint32_t hlog2 = (uint32_t)p.lv_hslice_log2;
   LvQueue in;
@@ -977,36 +1028,27 @@ __global__ __launch_bounds__(BS_SHADE, RTX_LV_SHADE_WPS) void k_lv_shade(KParams
   }
 }
 
+__global__ __launch_bounds__(BS_SHADE, RTX_LV_SHADE_WPS) void k_lv_shade(KParams p, int level) {
+  k_lv_shade_body(p, level);
+  lv_level_done(p, level + 1);
+}
+
 // ----------------------------------------------------------------- tree reduction
 // The batch's level layout for the reductions: base[d] = first record of level
 // d, pex[d * 64 + s] = dense index of slice s's first ray at level d (d >= 1).
 // Block 0 also adds the batch's level statistics to lv_acc (rtx_level_stats):
 // every level launch of the batch has ended.
 __device__ __forceinline__ void lv_layout(const KParams& p, int nlev, uint32_t* base, uint32_t* pex) {
-  __shared__ uint32_t tot[LV_MAXL + 1];
-  const int wave = (int)(threadIdx.x >> 6), lane = (int)__lane_id();
-  const uint32_t cap = 1u << p.lv_slice_log2;
-  for (int e = 1 + wave; e < nlev; e += (int)(blockDim.x >> 6)) {
-    uint32_t c = p.lv_ctl->sc[e][lane * 32];
-    c = c < cap ? c : cap;
-    const uint32_t incl = wave_scan_incl(c);
-    pex[e * 64 + lane] = incl - c;
-    if (lane == 63) tot[e] = incl;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t b = 0;
-    for (int d = 0; d <= nlev && d <= LV_MAXL; d++) {
-      base[d] = b;
-      if (d < nlev) b += d == 0 ? p.lv_ctl->count0 : tot[d];
-    }
-  }
+  const int t = (int)threadIdx.x;
+  for (int w = t; w < nlev * 64; w += (int)blockDim.x)
+    if (w >= 64) pex[w] = p.lv_ctl->lay_pex[w >> 6][w & 63];
+  if (t <= nlev && t <= LV_MAXL) base[t] = p.lv_ctl->lay_base[t];
   if (blockIdx.x == 0 && p.lv_acc) {
-    const int t = (int)threadIdx.x;
     // atomic: the two halves of a two-stream render add into the same totals
     if (t == 0) atomicAdd(&p.lv_acc[0], (unsigned long long)p.lv_ctl->redo_n);
     if (t == 1) atomicAdd(&p.lv_acc[1], (unsigned long long)p.lv_ctl->dropped);
-    if (t < nlev) atomicAdd(&p.lv_acc[2 + t], (unsigned long long)(t == 0 ? p.lv_ctl->count0 : tot[t]));
+    if (t < nlev)
+      atomicAdd(&p.lv_acc[2 + t], (unsigned long long)(p.lv_ctl->lay_base[t + 1] - p.lv_ctl->lay_base[t]));
   }
   __syncthreads();
 }
@@ -1410,7 +1452,12 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
     p.lv_ctl->count0 = v;
     p.lv_ctl->redo_n = 0;
     p.lv_ctl->dropped = 0;
+    p.lv_ctl->lay_base[0] = 0;
+    p.lv_ctl->lay_base[1] = v;
   }
+  if (t < LV_MAXL + 2) p.lv_ctl->done[t] = 0;
+  const int dwords = (nlev + 1 < LV_MAXL + 1 ? nlev + 1 : LV_MAXL + 1) * LV_DONE * 32;
+  for (int w = t; w < dwords; w += nt) (&p.lv_ctl->done_sub[0][0])[w] = 0;
   if (first) {
     if (t == 0) *p.extra_count = 0;
     if (p.lv_acc && t < LV_MAXL + 3) p.lv_acc[t] = 0;
