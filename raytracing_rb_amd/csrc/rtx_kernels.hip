@@ -643,7 +643,7 @@ extern "C" int rtxdbg_read_stamps(unsigned long long* out, int reset) {   // dia
   for (int k = 0; k < 8; k++) out[k] += lv[k];
   for (int k = 8; k < 11; k++) out[k] = lv[k];   // (k_level: lanes with a ray / a walk / a hit)
   if (lv[13])                                     // k_tree_finalize's phases (a levels-engine frame)
-    for (int k = 11; k < 14; k++) out[k] = lv[k];
+    for (int k = 11; k < 15; k++) out[k] = lv[k];
   return 0;
 }
 

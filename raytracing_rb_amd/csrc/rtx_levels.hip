@@ -1296,7 +1296,9 @@ __global__ __launch_bounds__(256) void k_tree_finalize_g(KParams p, int nlev) {
   __shared__ uint32_t wpart[4];
   extern __shared__ uint32_t lds_fin[];
   uint32_t* pex = lds_fin;
+  const unsigned long long ts0 = RTX_STAMPS ? stamp() : 0ull;   // RTX_STAMPS diagnostic build only
   lv_layout(p, nlev, base, pex);
+  const unsigned long long ts1 = RTX_STAMPS ? stamp() : 0ull;
   const int pre = p.pre, cap = p.lv_fin_cap, rb = p.lv_rec_bytes;
   const int n_items = 64 * pre;
   const int item0 = blockIdx.x * n_items;
@@ -1365,6 +1367,7 @@ __global__ __launch_bounds__(256) void k_tree_finalize_g(KParams p, int nlev) {
     lo = hi;
     hi += (int)total;
   }
+  const unsigned long long tsg = RTX_STAMPS ? stamp() : 0ull;
   // ---- the sums, in trace_sync's order
   uint32_t* slo = reinterpret_cast<uint32_t*>(recs) + tid;   // fallback walk stacks (alias the records)
   uint32_t* shi = slo + SD * 256;
@@ -1388,6 +1391,15 @@ __global__ __launch_bounds__(256) void k_tree_finalize_g(KParams p, int nlev) {
     scol[3 * it + 1] = c.y;
     scol[3 * it + 2] = c.z;
     serr[it] = e;
+  }
+  if (RTX_STAMPS) {                           // layout / gather + walks, waves; gather part in [14]
+    const unsigned long long ts2 = stamp();
+    if (__lane_id() == 0) {
+      atomicAdd(&rtx_stamps[11], ts1 - ts0);
+      atomicAdd(&rtx_stamps[12], ts2 - ts1);
+      atomicAdd(&rtx_stamps[13], 1ull);
+      atomicAdd(&rtx_stamps[14], tsg - ts1);
+    }
   }
   __syncthreads();
   lv_tile_pixels(p, scol, serr);

@@ -39,6 +39,6 @@ ch = max(1, v[6])
 print("lanes per chunk: with a ray %.1f, EXTEND walk %.1f, hit (shading, SHADOW walks) %.1f" % (
     v[8] / ch, v[9] / ch, v[10] / ch))
 if v[13]:
-    print("k_tree_finalize: %d waves, per wave %.0f cycles slice layout + %.0f cycles tree walks" % (
-        v[13], v[11] / v[13], v[12] / v[13]))
+    print("k_tree_finalize: %d waves, per wave %.0f cycles slice layout + %.0f cycles tree walks"
+          " (of which LDS gather %.0f)" % (v[13], v[11] / v[13], v[12] / v[13], v[14] / v[13]))
 
