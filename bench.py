@@ -2,11 +2,17 @@
 """Headline benchmark: Mpixels/s at 1920x1080, 4x AA, depth 5, 64 spheres (C2).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
-                    [--workload c2|c4] [--emulate-rank k/N] [--no-projection]
+                    [--workload c2|c4] [--emulate-rank k/N] [--no-projection] [--inflight F]
 
 One step = one complete C2 frame (BASELINE.json configs[2]): 1920x1080 pixels,
 Camera#render_at with pre = max = 4 samples, trace_depth 5, 64 spheres + ground
 plane + area light, counter RNG seed 1, scene resident in HBM before timing.
+Frames are pipelined (`--inflight F`, default 2): F independent contexts on F
+streams, frame i on context i mod F, so one frame's last levels and tree
+reduction overlap the next frame's first levels.  Every one of the K timed
+frames is rendered completely (and, multi-GPU, gathered to rank 0) inside the
+timed region; `ms_per_step` is the time per frame of that stream of frames,
+`frame_latency_ms` one frame rendered alone.
 
 Multi-GPU (C3, BASELINE.json configs[3]): one process per GPU.  Under
 torch.distributed.run (WORLD_SIZE set) this process is one rank; with
@@ -182,6 +188,10 @@ def main():
     ap.add_argument("--bvh", type=int, default=1, help="sphere walk: 0 ordered linear, 1 auto, 2 hierarchy")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="extra rtx_set_option before timing (experiments)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: F contexts, each on its own stream, render consecutive frames "
+                         "(frame i on context i mod F; every frame complete, and gathered, inside the timed "
+                         "region); 1 = one frame at a time")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # CPU test of the rank plumbing
     args = ap.parse_args()
 
@@ -241,49 +251,92 @@ def main():
 
     scene, cam = config.load_scene(WORLD, CAMERA)
     W, H = cam.width, cam.height
-    r = Renderer(scene, cam, device=local_rank)
-    r.set_option("bvh", args.bvh)
-    for kv in args.option:
-        key, val = kv.split("=", 1)
-        r.set_option(key, int(val))
+    # F frames in flight: F independent contexts (own level buffers, own
+    # camera copy), each on its own stream; frame i renders on context i mod F,
+    # so frame i + 1's levels fill the CUs frame i's last levels and tree
+    # reduction leave idle.  Each context then renders its frame as one part
+    # (lv_streams = 1: the overlap comes from the other frame; two parts per
+    # frame on top of that measured slower, profiles/r03x).
+    F = max(1, args.inflight)
+    rs = []
+    for _ in range(F):
+        rc = Renderer(scene, cam, device=local_rank)
+        rc.set_option("bvh", args.bvh)
+        if F > 1:
+            rc.set_option("lv_streams", 1)
+        for kv in args.option:
+            key, val = kv.split("=", 1)
+            rc.set_option(key, int(val))
+        rs.append(rc)
+    r = rs[0]
     engine = r.engine()
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
+    streams = [stream] if F == 1 else [torch.cuda.Stream(dev) for _ in range(F)]
+    counter = [0]
+
+    def next_ctx():
+        j = counter[0] % F
+        counter[0] += 1
+        return j
 
     packed_for = {}
 
+    def share_render(k, n, j):
+        if (k, n, j) not in packed_for:
+            packed_for[(k, n, j)] = torch.empty((rows_per_rank(H, TILE_ROWS, n), W, 3), dtype=torch.float64,
+                                                device=dev)
+        rs[j].render_tiles_device(packed_for[(k, n, j)].data_ptr(), TILE_ROWS, k, n, seed=1,
+                                  stream=streams[j].cuda_stream)
+
     def share_step(k, n):
-        if (k, n) not in packed_for:
-            packed_for[(k, n)] = torch.empty((rows_per_rank(H, TILE_ROWS, n), W, 3), dtype=torch.float64,
-                                             device=dev)
-        r.render_tiles_device(packed_for[(k, n)].data_ptr(), TILE_ROWS, k, n, seed=1, stream=sp)
+        share_render(k, n, next_ctx())
 
     if world == 1 and emulate is None:
-        frame = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+        frames = [torch.empty((H, W, 3), dtype=torch.float64, device=dev) for _ in range(F)]
+
+        def render_full(j):
+            rs[j].render_device(frames[j].data_ptr(), seed=1, stream=streams[j].cuda_stream)
 
         def step():
-            r.render_device(frame.data_ptr(), seed=1, stream=sp)
+            render_full(next_ctx())
     elif world == 1:
         def step():
             share_step(*emulate)
     else:
-        # Frame i's gather overlaps frame i + 1's render (two packed buffers):
-        # step i renders frame i, then finishes frame i - 1's gather (rank 0
-        # unpacks it), then starts frame i's.  drain() finishes the last one
-        # before the timed region closes, so all K frames are rendered AND
-        # gathered inside it.
-        df = DistributedFrame(W, H, TILE_ROWS, rank, world, dev, buffers=2)
+        # Frame i renders on context / stream / packed buffer j = i mod F; the
+        # current stream waits for it, finishes frame i - 1's gather (rank 0
+        # unpacks it; buffer j' may be rendered into again after that), then
+        # starts frame i's gather asynchronously, so it overlaps frame i + 1's
+        # render.  drain() finishes the last one before the timed region
+        # closes: all K frames are rendered AND gathered inside it.
+        df = DistributedFrame(W, H, TILE_ROWS, rank, world, dev, buffers=F)
         pending = []
+        free_ev = [None] * F
+
+        def finish_one():
+            h, jj = pending.pop(0)
+            df.gather_finish(h)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            free_ev[jj] = ev
 
         def step():
-            r.render_tiles_device(df.packed.data_ptr(), TILE_ROWS, rank, world, seed=1, stream=sp)
-            if pending:
-                df.gather_finish(pending.pop())
-            pending.append(df.gather_start())
+            j = next_ctx()
+            if free_ev[j] is not None:
+                streams[j].wait_event(free_ev[j])
+            rs[j].render_tiles_device(df.bufs[j].data_ptr(), TILE_ROWS, rank, world, seed=1,
+                                      stream=streams[j].cuda_stream)
+            done = torch.cuda.Event()
+            done.record(streams[j])
+            while pending:
+                finish_one()
+            stream.wait_event(done)
+            pending.append((df.gather_start(df.bufs[j]), j))
 
         def drain():
             while pending:
-                df.gather_finish(pending.pop())
+                finish_one()
 
     if world == 1:
         def drain():
@@ -294,11 +347,15 @@ def main():
             dist.barrier(device_ids=[local_rank])
         torch.cuda.synchronize(dev)
 
+    def check_raises():
+        for j in range(F):
+            rs[j].sync(streams[j].cuda_stream)   # raises if a reference raise site fired
+
     for _ in range(args.warmup):
         step()
     drain()
     barrier()
-    r.sync(sp)                              # raises if a reference raise site fired
+    check_raises()
 
     # ---- timed region: exactly K steps, barrier + synchronize on both sides
     barrier()
@@ -313,7 +370,19 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    r.sync(sp)
+    check_raises()
+
+    # ---- one frame alone (latency; F = 1 semantics), outside the timed region
+    latency_ms = None
+    if world == 1 and emulate is None:
+        lat = []
+        for _ in range(5):
+            torch.cuda.synchronize(dev)
+            a = time.perf_counter()
+            render_full(0)
+            torch.cuda.synchronize(dev)
+            lat.append((time.perf_counter() - a) * 1e3)
+        latency_ms = float(np.median(lat))
 
     # ---- the dominant kernel alone: HIP events on its launch stream around
     # every ray-tree kernel launch (rtx_kernel_time), outside the timed region
@@ -321,11 +390,11 @@ def main():
     kern_ms, kern_launches = [], 0
     for _ in range(max(3, min(args.steps, 10))):
         if world == 1 and emulate is None:
-            r.render_device(frame.data_ptr(), seed=1, stream=sp)
+            render_full(0)
         elif world == 1:
-            share_step(*emulate)
+            share_render(emulate[0], emulate[1], 0)
         else:
-            r.render_tiles_device(df.packed.data_ptr(), TILE_ROWS, rank, world, seed=1, stream=sp)
+            r.render_tiles_device(df.bufs[0].data_ptr(), TILE_ROWS, rank, world, seed=1, stream=streams[0].cuda_stream)
         ms, kern_launches = r.kernel_time()
         kern_ms.append(ms)
     r.set_option("kernel_events", 0)
@@ -335,22 +404,28 @@ def main():
     projection = None
     if world == 1 and emulate is None and not args.no_projection:
         def timed(fn, reps=3):
-            fn()
+            """Per-frame ms of fn(j) over F frames in flight (frame i on context i mod F), median of reps."""
+            for j in range(F):
+                fn(j)
             torch.cuda.synchronize(dev)
             ts = []
+            nf = 4 * F
             for _ in range(reps):
                 a = time.perf_counter()
-                fn()
+                for i in range(nf):
+                    fn(i % F)
                 torch.cuda.synchronize(dev)
-                ts.append(time.perf_counter() - a)
+                ts.append((time.perf_counter() - a) / nf)
             return float(np.median(ts)) * 1e3
-        full_ms = timed(step)
-        projection = {"method": "each rank's share rendered alone on this GPU (rtx_render_tiles_device), "
-                                "median of 3 after 1 warm-up; projected frame = max over ranks; the RCCL "
-                                "gather is estimated separately at %.0f GB/s per xGMI link" % XGMI_LINK_GBS,
+        full_ms = timed(render_full)
+        projection = {"method": "each rank's share rendered alone on this GPU (rtx_render_tiles_device) with the "
+                                "bench's %d frame(s) in flight, per-frame median of 3 x %d frames after a warm-up; "
+                                "projected frame = max over ranks; the RCCL gather is estimated separately at %.0f "
+                                "GB/s per xGMI link (the multi-GPU step overlaps it with the next frame's render)"
+                                % (F, 4 * F, XGMI_LINK_GBS),
                       "full_frame_ms": round(full_ms, 4), "per_n": {}}
         for n in PROJECT_N:
-            shares = [timed(lambda k=k: share_step(k, n)) for k in range(n)]
+            shares = [timed(lambda j, k=k: share_render(k, n, j)) for k in range(n)]
             packed_bytes = rows_per_rank(H, TILE_ROWS, n) * W * 3 * 8
             gather_ms = packed_bytes / (XGMI_LINK_GBS * 1e9) * 1e3
             mx = max(shares)
@@ -378,6 +453,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "frames_in_flight": F,
+            "frame_latency_ms": round(latency_ms, 4) if latency_ms is not None else None,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -426,7 +503,8 @@ def main():
         if projection:
             line["projection"] = projection
         print(json.dumps(line), flush=True)
-    r.close()
+    for rc in rs:
+        rc.close()
     if world > 1:
         dist.barrier(device_ids=[local_rank])
         dist.destroy_process_group()

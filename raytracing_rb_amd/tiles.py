@@ -92,17 +92,21 @@ class DistributedFrame:
             self.dst = torch.as_tensor(dst, device=device)
             self.frame = torch.zeros((height, width, 3), dtype=torch.float64, device=device)
 
-    def gather_start(self):
+    def gather_start(self, buf=None):
         """Start ONE collective (every rank's packed tiles to rank 0) without
-        waiting for it, and move ``packed`` to the next buffer."""
+        waiting for it.  Without ``buf``: gather ``packed`` and move ``packed``
+        to the next buffer; with ``buf``: gather that one (the caller manages
+        the buffers and their reuse)."""
         import torch.distributed as dist
-        buf = self.packed
+        advance = buf is None
+        buf = self.packed if buf is None else buf
         work = None
         if self.nranks > 1:
             chunks = list(self.gathered.chunk(self.nranks, 0)) if self.rank == 0 else None
             work = dist.gather(buf, chunks, dst=0, async_op=True)
-        self._i = (self._i + 1) % len(self.bufs)
-        self.packed = self.bufs[self._i]
+        if advance:
+            self._i = (self._i + 1) % len(self.bufs)
+            self.packed = self.bufs[self._i]
         return work, buf
 
     def gather_finish(self, handle):

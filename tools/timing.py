@@ -11,6 +11,7 @@ import hashlib
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -24,6 +25,8 @@ def main():
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--share", default="", help="k/N: time rank k's share of N ranks (8-row tiles)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="frames in flight: K contexts on K streams render consecutive frames (throughput per frame)")
     ap.add_argument("opts", nargs="*")
     a = ap.parse_args()
     import torch
@@ -51,6 +54,41 @@ def main():
             r.render_device(out.data_ptr(), stream=s.cuda_stream)
     for o in (a.opts or ["{}"]):
         opts = json.loads(o)
+        if a.inflight > 1:
+            # K independent contexts (own buffers and camera copy), frame i on context/stream i mod K
+            rs, ss, outs = [], [], []
+            for _ in range(a.inflight):
+                r = Renderer(sd, cd)
+                for k, v in opts.items():
+                    r.set_option(k, v)
+                rs.append(r)
+                ss.append(torch.cuda.Stream())
+                outs.append(torch.empty_like(out))
+            def frame(i):
+                k = i % a.inflight
+                if share:
+                    rs[k].render_tiles_device(outs[k].data_ptr(), 8, share[0], share[1], stream=ss[k].cuda_stream)
+                else:
+                    rs[k].render_device(outs[k].data_ptr(), stream=ss[k].cuda_stream)
+            for i in range(2 * a.inflight):
+                frame(i)
+            torch.cuda.synchronize()
+            ts = []
+            nf = 8 * a.inflight
+            for _ in range(a.reps):
+                t = time.perf_counter()
+                for i in range(nf):
+                    frame(i)
+                torch.cuda.synchronize()
+                ts.append((time.perf_counter() - t) * 1e3 / nf)
+            for r in rs:
+                r.close()
+            ts.sort()
+            sha = hashlib.sha1(outs[0].cpu().numpy().tobytes()).hexdigest()[:12]
+            print("%-8s %-40s min %9.3f ms  median %9.3f ms  %8.2f Mpix/s  sha %s  (%d frames in flight, per frame)%s" % (
+                a.scene, o, ts[0], ts[len(ts) // 2], cd.width * cd.height / ts[len(ts) // 2] / 1e3, sha, a.inflight,
+                "  (share %s)" % a.share if share else ""), flush=True)
+            continue
         r = Renderer(sd, cd)              # a fresh context per option set: options do not carry over
         for k, v in opts.items():
             r.set_option(k, v)
