@@ -476,6 +476,12 @@ def main():
                 "kernel_ms_per_frame": round(kern_frame_ms, 4),
                 "kernel_launches_per_frame": kern_launches,
                 "kernel_avg_ms": round(kern_frame_ms / max(1, kern_launches), 4),
+                "kernel_timing": "HIP events around every ray-tree launch of one frame rendered alone on context 0 "
+                                 "(lv_streams %d: %d launches that do not overlap); with frames in flight the "
+                                 "launches of two frames overlap and each one's span stretches, so the matching "
+                                 "rocprofv3 summary is the single-frame run (tools/gpu_session.sh bench: "
+                                 "prof_single = bench.py --inflight 1 --option lv_streams=%d)"
+                                 % (r.get_option("lv_streams"), kern_launches, r.get_option("lv_streams")),
                 "hw": hw,
                 "pmc_source": ({"file": "profiles/pmc_%s.json" % args.workload, "stale": stale,
                                 "source_sha": pm.get("source_sha"), "session": pm.get("session")}

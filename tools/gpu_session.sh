@@ -63,7 +63,10 @@ print(r.engine())") > $OUT/pmc_json.log 2>&1 && \
 bench() {
   timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err && \
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o kt --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-projection > $OUT/prof_bench.log 2>&1
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-projection > $OUT/prof_bench.log 2>&1 && \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_single -o kt --output-format csv -- \
+    python3 bench.py --inflight 1 --option lv_streams=1 --steps 5 --warmup 2 --no-cpu-baseline --no-projection \
+    > $OUT/prof_single.json 2> $OUT/prof_single.err
 }
 bench_c4() {
   timeout -k 10 600 python bench.py --workload c4 --steps 3 --warmup 1 > $OUT/bench_c4.json 2> $OUT/bench_c4.err
