@@ -894,8 +894,12 @@ __device__ __forceinline__ Ray lens_ray(const CameraDev& c, V3 target, int x, in
 // to `leaf(V3)` in light order.  Returns true if any light fired (the ray then
 // stops, ray_tracer.rb:77).  The `&& lit_area(...)` is always truthy in Ruby and
 // is not evaluated.
-template <typename Leaf>
-__device__ __forceinline__ bool highlight_leaves(const SceneDev& S, const Item& it, Leaf&& leaf, uint32_t& err) {
+// att_fn() gives the ray's attenuation, asked for only when a light fires.
+template <typename Att, typename Leaf>
+__device__ __forceinline__ bool highlight_leaves_att(const SceneDev& S, const Ray& ray, Att&& att_fn, Leaf&& leaf,
+                                                     uint32_t& err) {
+  Item it;
+  it.ray = ray;
   uint32_t fired = 0;
   int nfired = 0;
   const RTX_CONST LightDev* lights = cptr(S.light);
@@ -928,12 +932,18 @@ __device__ __forceinline__ bool highlight_leaves(const SceneDev& S, const Item& 
     }
   }
   if (!nfired) return false;
+  it.att = att_fn();
   for (int l = 0; l < S.n_light; l++) {
     if (!(fired >> l & 1)) continue;
     const RTX_CONST LightDev& L = lights[l];
     leaf(vdiv(vmul(it.att, vsc(v3(L.color[0], L.color[1], L.color[2]), L.hl_rate)), (double)nfired));
   }
   return true;
+}
+
+template <typename Leaf>
+__device__ __forceinline__ bool highlight_leaves(const SceneDev& S, const Item& it, Leaf&& leaf, uint32_t& err) {
+  return highlight_leaves_att(S, it.ray, [&] { return it.att; }, leaf, err);
 }
 
 // The same into a running sum.  REDUCE: leaves go through rt_reduce

@@ -658,17 +658,28 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       uint32_t s, off, i;
       bool active = in.item(chunk, s, off, i);
       const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
+      // A staged child's first half needs its origin and direction only: the
+      // attenuation is read if a highlight fires, the root if the ray
+      // overflows the record arena (the second half reloads the rest), so
+      // the walk does not carry them.
+      const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * RAY_DOUBLES);
       Item cur;
       int root = 0, x = 0, y = 0, sample = 0;
       bool alive = false;
       if (active) {
-        bool valid;
-        lv_ray(p, level, slot, cur, root, x, y, sample, valid);
-        if (level == 0) p.lv_redo_of[i] = -1;
+        bool valid = true;
+        if (level == 0) {
+          lv_ray(p, level, slot, cur, root, x, y, sample, valid);
+          p.lv_redo_of[i] = -1;
+        } else {
+          const double2 a = qs[0], b = qs[1], c = qs[2];
+          cur.ray.o = v3(a.x, a.y, b.x);
+          cur.ray.d = v3(b.y, c.x, c.y);
+        }
         active = valid;
         alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // ray_tracer.rb:52
         if (active && base + i >= p.lv_lcap) {
-          lv_redo(p, root);
+          lv_redo(p, level == 0 ? root : (int)(uint32_t)__builtin_bit_cast(uint64_t, qs[5].x));
           active = alive = false;
         }
       }
@@ -678,7 +689,11 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       int nleaf = 0;
       bool fired = false;
       if (alive)
-        fired = highlight_leaves(S, cur, [&](V3 c) {
+        fired = highlight_leaves_att(S, cur.ray, [&] {
+          if (level == 0) return cur.att;
+          const double2 d = qs[3], e = qs[4];
+          return v3(d.x, d.y, e.x);
+        }, [&](V3 c) {
           leafp[3 * nleaf] = c.x;
           leafp[3 * nleaf + 1] = c.y;
           leafp[3 * nleaf + 2] = c.z;

@@ -485,3 +485,23 @@ def test_dead_child_raises_match_lanes_and_oracle(gpu, tmp_path, refl, refr, dep
         assert e.value.kind == "zero_vec", (engine, opts, str(e.value))
         msgs.append(str(e.value))
     assert len(set(msgs)) == 1, msgs
+
+
+def test_frames_in_flight_identical(gpu):
+    """bench.py's two frames in flight: two contexts on two streams render
+    consecutive frames concurrently (one part each); every frame equals the
+    one-context render bit for bit."""
+    import torch
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=480, height=270)
+    ref = _renderer(sd, cd, 1).render(seed=1)
+    rs = [_renderer(sd, cd, 1, lv_streams=1) for _ in range(2)]
+    ss = [torch.cuda.Stream() for _ in range(2)]
+    outs = [torch.zeros((cd.height, cd.width, 3), dtype=torch.float64, device="cuda") for _ in range(2)]
+    for i in range(5):
+        j = i % 2
+        rs[j].render_device(outs[j].data_ptr(), seed=1, stream=ss[j].cuda_stream)
+    torch.cuda.synchronize()
+    for j in range(2):
+        rs[j].sync(ss[j].cuda_stream)
+        assert _same(outs[j].cpu().numpy(), ref), j
+        rs[j].close()
