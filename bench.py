@@ -241,6 +241,13 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    # The frames' streams are this process's first streams, before RCCL makes
+    # its own: HIP maps streams onto its hardware queues in creation order, and
+    # two frame streams that land on one queue run their frames one after the
+    # other.  Created first, they map alike on every rank and
+    # as in the measured 1-GPU run.
+    F = max(1, args.inflight)
+    frame_streams = [torch.cuda.Stream(dev) for _ in range(F)] if F > 1 else None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
@@ -257,7 +264,6 @@ def main():
     # reduction leave idle.  Each context then renders its frame as one part
     # (lv_streams = 1: the overlap comes from the other frame; two parts per
     # frame on top of that measured slower, profiles/r03x).
-    F = max(1, args.inflight)
     rs = []
     for _ in range(F):
         rc = Renderer(scene, cam, device=local_rank)
@@ -272,7 +278,7 @@ def main():
     engine = r.engine()
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
-    streams = [stream] if F == 1 else [torch.cuda.Stream(dev) for _ in range(F)]
+    streams = [stream] if F == 1 else frame_streams
     counter = [0]
 
     def next_ctx():
