@@ -242,10 +242,9 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     # The frames' streams are this process's first streams, before RCCL makes
-    # its own: HIP maps streams onto its hardware queues in creation order, and
-    # two frame streams that land on one queue run their frames one after the
-    # other.  Created first, they map alike on every rank and
-    # as in the measured 1-GPU run.
+    # its own, so every rank sets up its frames exactly as the measured 1-GPU
+    # run does (a second pair of contexts and streams in one
+    # process was measured to run its two frames one after the other).
     F = max(1, args.inflight)
     frame_streams = [torch.cuda.Stream(dev) for _ in range(F)] if F > 1 else None
     if world > 1:

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--share", default="", help="k/N: time rank k's share of N ranks (8-row tiles)")
+    ap.add_argument("--dummy-streams", type=int, default=0,
+                    help="with --inflight: create this many unused streams before each option set's streams")
     ap.add_argument("--inflight", type=int, default=1,
                     help="frames in flight: K contexts on K streams render consecutive frames (throughput per frame)")
     ap.add_argument("opts", nargs="*")
@@ -57,6 +59,7 @@ def main():
         if a.inflight > 1:
             # K independent contexts (own buffers and camera copy), frame i on context/stream i mod K
             rs, ss, outs = [], [], []
+            dummies = [torch.cuda.Stream() for _ in range(a.dummy_streams)]   # (hardware-queue mapping probe)
             for _ in range(a.inflight):
                 r = Renderer(sd, cd)
                 for k, v in opts.items():
