@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--share", default="", help="k/N: time rank k's share of N ranks (8-row tiles)")
     ap.add_argument("--dummy-streams", type=int, default=0,
                     help="with --inflight: create this many unused streams before each option set's streams")
+    ap.add_argument("--keep", action="store_true", help="with --inflight: keep every option set's contexts open")
     ap.add_argument("--inflight", type=int, default=1,
                     help="frames in flight: K contexts on K streams render consecutive frames (throughput per frame)")
     ap.add_argument("opts", nargs="*")
@@ -54,6 +55,7 @@ def main():
             r.render_tiles_device(out.data_ptr(), 8, share[0], share[1], stream=s.cuda_stream)
         else:
             r.render_device(out.data_ptr(), stream=s.cuda_stream)
+    kept = []
     for o in (a.opts or ["{}"]):
         opts = json.loads(o)
         if a.inflight > 1:
@@ -84,8 +86,11 @@ def main():
                     frame(i)
                 torch.cuda.synchronize()
                 ts.append((time.perf_counter() - t) * 1e3 / nf)
-            for r in rs:
-                r.close()
+            if a.keep:
+                kept.extend(rs)
+            else:
+                for r in rs:
+                    r.close()
             ts.sort()
             sha = hashlib.sha1(outs[0].cpu().numpy().tobytes()).hexdigest()[:12]
             print("%-8s %-40s min %9.3f ms  median %9.3f ms  %8.2f Mpix/s  sha %s  (%d frames in flight, per frame)%s" % (
