@@ -505,3 +505,37 @@ def test_frames_in_flight_identical(gpu):
         rs[j].sync(ss[j].cuda_stream)
         assert _same(outs[j].cpu().numpy(), ref), j
         rs[j].close()
+
+
+def test_first_raise_in_render_sync_order(gpu, tmp_path):
+    """Two raise sites in one frame: pixel (0, 3) meets a glowing sphere
+    (color greater than 1) and pixel (2, 2) meets the pane head-on (zero
+    vector).  render_sync walks x outer, y inner (camera.rb:102-103), so the
+    call reports (0, 3)'s raise, which a row-major order would not."""
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import RtxError
+    from oracle.c_oracle import Oracle
+    w, c = tmp_path / "w.yml", tmp_path / "c.yml"
+    w.write_text(HEADON_WORLD % ("0.5, 0.5, 0.5", "0.0, 0.0, 0.0") + """  - type: Sphere
+    properties:
+      name: glow
+      center: [3.0, 1.5, -0.75]
+      radius: 0.2
+      refractive_rate: 1.5
+      diffuse_rate: [0.5, 0.5, 0.5]
+      ambient: [2.0, 2.0, 2.0]
+      reflective_attenuation: [0.0, 0.0, 0.0]
+      refractive_attenuation: [0.0, 0.0, 0.0]
+""")
+    c.write_text(HEADON_CAMERA % 2)
+    sd, cd = config.load_scene(str(w), str(c))
+    _, status, rc = Oracle(sd, cd).render()
+    assert status[3, 0] == 2 and status[2, 2] == 1, status   # color > 1 at (0, 3), zero vector at (2, 2)
+    assert rc == 2                                            # the oracle reports in render_sync order too
+    msgs = []
+    for engine, opts in ((0, {}), (1, {}), (1, dict(lv_split=1))):
+        with pytest.raises(RtxError) as e:
+            _renderer(sd, cd, engine, **opts).render()
+        assert e.value.kind == "color_gt1", (engine, opts, str(e.value))
+        msgs.append(str(e.value))
+    assert len(set(msgs)) == 1, msgs
