@@ -192,6 +192,9 @@ def main():
                     help="frames in flight: F contexts, each on its own stream, render consecutive frames "
                          "(frame i on context i mod F; every frame complete, and gathered, inside the timed "
                          "region); 1 = one frame at a time")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="run the multi-GPU step (tile shares, RCCL gather to rank 0, pipelined) even with one "
+                         "rank: a 1-rank RCCL group (evidence that the C3 path runs on ROCm)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # CPU test of the rank plumbing
     args = ap.parse_args()
 
@@ -220,6 +223,9 @@ def main():
         METRIC = "Mpixels/sec at 3840×2160, 8× AA, depth 8 (C4, 4096 spheres)"
 
     emulate = None
+    if args.force_collective and args.emulate_rank:
+        print("bench.py: --force-collective and --emulate-rank exclude each other", file=sys.stderr)
+        sys.exit(2)
     if args.emulate_rank:
         k, n = (int(v) for v in args.emulate_rank.split("/"))
         if world != 1 or not (0 <= k < n):
@@ -237,7 +243,7 @@ def main():
 
     from raytracing_rb_amd import config, roofline
     from raytracing_rb_amd.runtime import Renderer
-    from raytracing_rb_amd.tiles import DistributedFrame, rows_per_rank
+    from raytracing_rb_amd.tiles import PipelinedTiles, rows_per_rank
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -247,8 +253,15 @@ def main():
     # process was measured to run its two frames one after the other).
     F = max(1, args.inflight)
     frame_streams = [torch.cuda.Stream(dev) for _ in range(F)] if F > 1 else None
-    if world > 1:
+    if world > 1 or args.force_collective:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:                     # the multi-rank step under a 1-rank RCCL group
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            if "MASTER_PORT" not in os.environ:
+                with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+                    so.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(so.getsockname()[1])
         dist.init_process_group("nccl", device_id=dev)
         if dist.get_world_size() != args.gpus:
             print("bench.py: process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus),
@@ -297,53 +310,30 @@ def main():
     def share_step(k, n):
         share_render(k, n, next_ctx())
 
+    dist_step = world > 1 or args.force_collective
     if world == 1 and emulate is None:
         frames = [torch.empty((H, W, 3), dtype=torch.float64, device=dev) for _ in range(F)]
 
         def render_full(j):
             rs[j].render_device(frames[j].data_ptr(), seed=1, stream=streams[j].cuda_stream)
 
+    if world == 1 and emulate is None and not dist_step:
         def step():
             render_full(next_ctx())
-    elif world == 1:
+    elif world == 1 and emulate is not None:
         def step():
             share_step(*emulate)
     else:
-        # Frame i renders on context / stream / packed buffer j = i mod F; the
-        # current stream waits for it, finishes frame i - 1's gather (rank 0
-        # unpacks it; buffer j' may be rendered into again after that), then
-        # starts frame i's gather asynchronously, so it overlaps frame i + 1's
-        # render.  drain() finishes the last one before the timed region
-        # closes: all K frames are rendered AND gathered inside it.
-        df = DistributedFrame(W, H, TILE_ROWS, rank, world, dev, buffers=F)
-        pending = []
-        free_ev = [None] * F
+        # Frame i renders on context / stream / packed buffer j = i mod F; its
+        # gather overlaps frame i + 1's render (tiles.PipelinedTiles); drain()
+        # finishes the last one before the timed region closes: all K frames
+        # are rendered AND gathered inside it.
+        pipe = PipelinedTiles(rs, streams, W, H, TILE_ROWS, rank, world, dev, seed=1,
+                              force_collective=args.force_collective)
+        df = pipe.df
+        step, drain = pipe.step, pipe.drain
 
-        def finish_one():
-            h, jj = pending.pop(0)
-            df.gather_finish(h)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            free_ev[jj] = ev
-
-        def step():
-            j = next_ctx()
-            if free_ev[j] is not None:
-                streams[j].wait_event(free_ev[j])
-            rs[j].render_tiles_device(df.bufs[j].data_ptr(), TILE_ROWS, rank, world, seed=1,
-                                      stream=streams[j].cuda_stream)
-            done = torch.cuda.Event()
-            done.record(streams[j])
-            while pending:
-                finish_one()
-            stream.wait_event(done)
-            pending.append((df.gather_start(df.bufs[j]), j))
-
-        def drain():
-            while pending:
-                finish_one()
-
-    if world == 1:
+    if not dist_step:
         def drain():
             pass
 
@@ -376,6 +366,16 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     check_raises()
+
+    # ---- the gathered frame equals one whole-frame render, bit for bit (rank 0)
+    gather_check = None
+    if dist_step and rank == 0:
+        full = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+        rs[0].render_device(full.data_ptr(), seed=1, stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        rs[0].sync(stream.cuda_stream)
+        gather_check = "bit-identical" if torch.equal(full, df.frame) else "MISMATCH"
+        del full
 
     # ---- one frame alone (latency; F = 1 semantics), outside the timed region
     latency_ms = None
@@ -445,8 +445,11 @@ def main():
         n_share = emulate[1] if emulate else world
         px_frame = W * H if n_share == 1 else W * H / n_share
         ops_frame = roofline.algorithmic_ops(counts) / n_share
-        ref_rate_tf = ops_frame / (kern_frame_ms * 1e-3) / 1e12
-        wr_gbs = px_frame * roofline.FRAMEBUFFER_BYTES_PER_PX / (kern_frame_ms * 1e-3) / 1e9
+        # whole-frame rates over the timed step (every launch of the frame: level
+        # kernels, resets, re-render, tree reduction), not the level kernels alone
+        step_s = elapsed / args.steps
+        ref_rate_tf = ops_frame / step_s / 1e12
+        wr_gbs = px_frame * roofline.FRAMEBUFFER_BYTES_PER_PX / step_s / 1e9
         value = W * H * args.steps / elapsed / 1e6 if emulate is None else None
         pm, stale = pmc_profile(args.workload, engine) if (world == 1 and emulate is None) else (None, None)
         hw = roofline.hw_fp64(pm, kern_frame_ms) if pm else None
@@ -467,8 +470,9 @@ def main():
             "data": "synthetic",
             "config": {"workload": WORKLOAD, "width": W, "height": H, "samples_per_pixel": cam.pre_sample_times,
                        "trace_depth": cam.trace_depth, "objects": scene.n_objects, "seed": 1, "engine": engine,
-                       "parallelism": "tiles%d-rr x %d ranks, 1 RCCL gather/frame" % (TILE_ROWS, world)
-                       if world > 1 else "1 GPU"},
+                       "parallelism": "tiles%d-rr x %d ranks, 1 RCCL gather/frame%s"
+                       % (TILE_ROWS, world, " (1-rank group, --force-collective)" if world == 1 else "")
+                       if dist_step else "1 GPU"},
             "roofline": {
                 "bound": "valu_fp64",
                 "unit": "TFLOP/s",
@@ -481,7 +485,8 @@ def main():
                 "kernel_ms_per_frame": round(kern_frame_ms, 4),
                 "kernel_launches_per_frame": kern_launches,
                 "kernel_avg_ms": round(kern_frame_ms / max(1, kern_launches), 4),
-                "kernel_timing": "HIP events around every ray-tree launch of one frame rendered alone on context 0 "
+                "kernel_timing": "level kernels only (achieved/frac are the dominant kernel's: its FLOP over its own "
+                                 "launches); HIP events around every ray-tree launch of one frame rendered alone on context 0 "
                                  "(lv_streams %d: %d launches that do not overlap); with frames in flight the "
                                  "launches of two frames overlap and each one's span stretches, so the matching "
                                  "rocprofv3 summary is the single-frame run (tools/gpu_session.sh bench: "
@@ -498,16 +503,19 @@ def main():
                 "reference_work_rate": {"achieved_tflops": round(ref_rate_tf, 4),
                                         "algorithmic_fp64_ops_per_frame": int(ops_frame),
                                         "note": "the brute-force reference algorithm's ops (device-counted events "
-                                                "x frozen cost table, raytracing_rb_amd/roofline.py) per kernel "
-                                                "second: a work rate, not a utilisation (the exact culls and the "
-                                                "hierarchy skip most of these ops)"},
+                                                "x frozen cost table, raytracing_rb_amd/roofline.py) per second of "
+                                                "the timed step (whole frame): a work rate, not a utilisation (the "
+                                                "exact culls and the hierarchy skip most of these ops)"},
                 "hbm_write": {"achieved": round(wr_gbs, 3), "peak": roofline.HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(wr_gbs / roofline.HBM_PEAK_GBS, 7),
-                              "bytes_per_px": roofline.FRAMEBUFFER_BYTES_PER_PX},
+                              "bytes_per_px": roofline.FRAMEBUFFER_BYTES_PER_PX,
+                              "time": "ms_per_step (the whole frame)"},
             },
             "cpu_baseline": cpu,
             "work_counts": counts,
         }
+        if gather_check is not None:
+            line["gather_check"] = gather_check
         if emulate:
             line["emulate_rank"] = {"rank": emulate[0], "nranks": emulate[1],
                                     "rank_ms_per_frame": round(elapsed / args.steps * 1e3, 4)}
@@ -516,9 +524,11 @@ def main():
         print(json.dumps(line), flush=True)
     for rc in rs:
         rc.close()
-    if world > 1:
+    if dist_step:
         dist.barrier(device_ids=[local_rank])
         dist.destroy_process_group()
+    if gather_check == "MISMATCH":
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -156,7 +156,11 @@ rtx_status rtx_camera_set(rtx_context* ctx, const rtx_camera_desc* camera);
 /* Camera#render_sync: pixels [x0,x1) x [y0,y1) into the caller-owned host
  * buffer out_rgb (row-major; out_rgb[(y-y0)*row_stride + (x-x0)*3 + c]) in final
  * image orientation (row = y = top row first), before quantization.
- * Synchronous.  RNG key: seed (main.rb:10 uses Random.srand(1)). */
+ * Synchronous.  RNG key: seed (main.rb:10 uses Random.srand(1)).
+ * The synchronous host-buffer calls (rtx_render, rtx_render_at,
+ * rtx_render_tiles, rtx_render_multi) start by discarding raises that earlier
+ * asynchronous *_device calls on the same context(s) recorded and nobody
+ * collected: call rtx_sync first to read those. */
 rtx_status rtx_render(rtx_context* ctx, int32_t x0, int32_t y0, int32_t x1, int32_t y1,
                       uint64_t seed, double* out_rgb, size_t row_stride);
 
@@ -190,8 +194,10 @@ rtx_status rtx_render_tiles(rtx_context* ctx, int32_t tile_rows, int32_t rank, i
  * gathered to ctxs[0]'s device with ONE grouped RCCL ncclSend/ncclRecv over
  * xGMI (device copies instead when several contexts share a device),
  * unpacked there and copied into the caller's host buffer out_rgb (layout of
- * rtx_render).  Synchronous.  RTX_ERCCL when the collective fails; a rank's
- * reference raise is returned as in rtx_render. */
+ * rtx_render).  Synchronous.  RTX_ERCCL when the collective fails (the group
+ * is always closed and the cached communicators are re-created by the next
+ * call).  The ranks' reference raises are merged: the one returned is the
+ * first over the whole frame in render_sync order, as in rtx_render. */
 rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, uint64_t seed,
                             double* out_rgb, size_t row_stride);
 
@@ -199,7 +205,11 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
 int32_t    rtx_device_count(void);
 
 /* Wait for `hip_stream` and report the first reference raise recorded by the
- * device since the last rtx_sync (RTX_OK if none); details in rtx_last_error. */
+ * device since the last rtx_sync (RTX_OK if none); details in rtx_last_error.
+ * "First" is the reference's order: pixels in render_sync order (x outer, y
+ * inner, camera.rb:101-103), within a pixel its pre samples before its extra
+ * samples and samples in order (camera.rb:72-97), within a sample trace_sync's
+ * order; rays (rtx_trace) by index. */
 rtx_status rtx_sync(rtx_context* ctx, void* hip_stream);
 
 /* Camera#render_at(x, y): the averaged colour of one pixel. */
@@ -247,7 +257,9 @@ rtx_status rtx_count_work(rtx_context* ctx, uint64_t seed, uint64_t counts[RTX_N
 
 /* Device time of the ray-tree kernel launches of the last render call on this
  * context (HIP events recorded on the launch stream around each launch; needs
- * option "kernel_events" = 1 before the call).  Waits for those events. */
+ * option "kernel_events" = 1 before the call).  Waits for those events.
+ * Bounce-level engine: the level launches only (k_level / k_level_c, the split
+ * kernels), not the per-batch reset, re-render or tree reduction. */
 rtx_status rtx_kernel_time(rtx_context* ctx, double* total_ms, int32_t* launches);
 
 /* Bounce-level engine statistics of the last render call (summed over its
@@ -259,7 +271,10 @@ rtx_status rtx_level_stats(rtx_context* ctx, int64_t* out, int32_t n);
 /* Kernel-variant control for experiments; 0 = default. */
 rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
 rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
-/* keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
+/* read-only key: "engine_effective" (the engine the next render of the uploaded scene and camera runs:
+         "engine", except that the bounce-level engine falls back to the lanes engine for trace_depth > 64,
+         monte_carlo_diffusion_times > 14 or more than 255 lights).
+   keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
          2 always; every choice renders the same bits), "bvh_min" [32], "bvh_sah" (1 [default] binned-SAH hierarchy
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
          staging, 1 scalar loads), "lds_stack" (ray-stack entries per lane kept in LDS,

@@ -400,8 +400,14 @@ void rtx_context_destroy(rtx_context* c) {
   delete c;
 }
 
+static bool levels_engine(const rtx_context* c);
+
 rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
   if (!c || !key || !value) return RTX_EINVAL;
+  if (!strcmp(key, "engine_effective")) {   // read-only: the engine the next render of this camera runs
+    *value = c->have_cam && c->have_scene ? (levels_engine(c) ? 1 : 0) : c->opt_engine;
+    return RTX_OK;
+  }
   const struct { const char* k; int64_t v; } tab[] = {
       {"engine", c->opt_engine},       {"force_stack", c->opt_force_stack}, {"bvh", c->opt_bvh},
       {"bvh_sah", c->opt_bvh_sah},     {"bvh_min", c->opt_bvh_min},         {"postpone", c->opt_postpone},
@@ -1095,30 +1101,44 @@ rtx_status rtx_kernel_time(rtx_context* c, double* total_ms, int32_t* launches) 
   return RTX_OK;
 }
 
-rtx_status rtx_sync(rtx_context* c, void* stream) {
-  if (!c) return RTX_EINVAL;
+// Waits for `stream`, moves the device's raise record into `e` and resets it.
+static rtx_status take_errors(rtx_context* c, void* stream, ErrState* e) {
   hipSetDevice(c->device);
-  ErrState e;
   HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-  HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof e, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(e, c->d_err, sizeof *e, hipMemcpyDeviceToHost));
   HIPCHK(c, hipMemset(c->d_err, 0, 8));
   HIPCHK(c, hipMemset(((char*)c->d_err) + 8, 0xFF, sizeof(ErrState) - 8));
   HIPCHK(c, hipDeviceSynchronize());
+  return RTX_OK;
+}
+
+// The first raise the reference would meet: the smallest key over the codes.
+static rtx_status report_errors(rtx_context* c, const ErrState& e) {
   if (!e.flags) return RTX_OK;
   // device ERR_ code -> rtx_status (index = ERR_ code, rtx_vec3.h)
   static const rtx_status status_of[5] = {RTX_OK, RTX_EZERO_VEC, RTX_ECOLOR_GT1, RTX_EDOMAIN, RTX_ETYPE};
   rtx_status first = RTX_OK;
-  unsigned long long pix = ~0ull;
+  unsigned long long key = ~0ull;
   for (int code = 1; code < 5; code++)
-    if ((e.flags >> code & 1) && e.first[code] < pix) {
-      pix = e.first[code];
+    if ((e.flags >> code & 1) && e.first[code] < key) {
+      key = e.first[code];
       first = status_of[code];
     }
   const char* more = __builtin_popcount(e.flags) > 1 ? " (and other errors)" : "";
-  if (c->err_keys_rays) return fail(c, first, "%s at ray %llu%s", rtx_status_string(first), pix, more);
-  // pixel keys are x * height + y: render_sync's x-outer, y-inner order (camera.rb:102-103)
+  if (c->err_keys_rays) return fail(c, first, "%s at ray %llu%s", rtx_status_string(first), key, more);
+  // pixel keys are (x * height + y) * 2 + phase: render_sync's x-outer, y-inner
+  // order (camera.rb:102-103), pre samples before extra samples (px_key)
   const unsigned long long H = c->have_cam ? (unsigned long long)c->cam.height : 1;
+  const unsigned long long pix = key >> 1;
   return fail(c, first, "%s at pixel (%llu,%llu)%s", rtx_status_string(first), pix / H, pix % H, more);
+}
+
+rtx_status rtx_sync(rtx_context* c, void* stream) {
+  if (!c) return RTX_EINVAL;
+  ErrState e;
+  const rtx_status s = take_errors(c, stream, &e);
+  if (s) return s;
+  return report_errors(c, e);
 }
 
 static rtx_status ensure_scratch(rtx_context* c, size_t bytes) {
@@ -1176,12 +1196,6 @@ static rtx_status grow(rtx_context* c, double** buf, size_t* cap, size_t bytes) 
   return RTX_OK;
 }
 
-#define NCCLCHK(c, expr)                                                                      \
-  do {                                                                                        \
-    ncclResult_t r_ = (expr);                                                                 \
-    if (r_ != ncclSuccess) return fail(c, RTX_ERCCL, "%s: %s", #expr, ncclGetErrorString(r_)); \
-  } while (0)
-
 rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, uint64_t seed, double* out,
                             size_t row_stride) {
   if (!ctxs || n < 1 || !ctxs[0]) return RTX_EINVAL;
@@ -1199,7 +1213,9 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
   if (row_stride < (size_t)W * 3) return fail(c0, RTX_EINVAL, "row_stride too small");
   const int R = rtx_tiles_rows_per_rank(H, tile_rows, n);
   const size_t count = (size_t)R * W * 3;                      // doubles per rank
-  for (int k = 0; k < n; k++) (void)rtx_sync(ctxs[k], nullptr);   // clear stale device errors
+  // clear stale device errors (as rtx_render: unsynced raises of earlier
+  // asynchronous calls on these contexts are discarded, include/rtx.h)
+  for (int k = 0; k < n; k++) (void)rtx_sync(ctxs[k], nullptr);
   // every rank renders its tiles on its own device; the devices run concurrently
   for (int k = 0; k < n; k++) {
     rtx_context* c = ctxs[k];
@@ -1226,18 +1242,43 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
       }
       c0->comms.assign(n, nullptr);
       c0->comm_devs.clear();
-      NCCLCHK(c0, ncclCommInitAll(c0->comms.data(), n, devs.data()));
+      const ncclResult_t ri = ncclCommInitAll(c0->comms.data(), n, devs.data());
+      if (ri != ncclSuccess) {
+        c0->comms.clear();                       // nothing to destroy later
+        return fail(c0, RTX_ERCCL, "ncclCommInitAll: %s", ncclGetErrorString(ri));
+      }
       c0->comm_devs = devs;
     }
-    NCCLCHK(c0, ncclGroupStart());
-    for (int k = 0; k < n; k++) {
-      hipSetDevice(devs[k]);
-      NCCLCHK(c0, ncclSend(ctxs[k]->d_multi, count, ncclFloat64, 0, c0->comms[k], nullptr));
+    // Every call between GroupStart and GroupEnd is made and GroupEnd always
+    // runs, so a failure never leaves this thread inside an open RCCL group;
+    // after one the cached communicators are torn down (the next call
+    // re-initialises them).
+    ncclResult_t r = ncclGroupStart();
+    const char* what = r != ncclSuccess ? "ncclGroupStart" : nullptr;
+    if (r == ncclSuccess) {
+      for (int k = 0; k < n; k++) {
+        hipSetDevice(devs[k]);
+        const ncclResult_t rk = ncclSend(ctxs[k]->d_multi, count, ncclFloat64, 0, c0->comms[k], nullptr);
+        if (rk != ncclSuccess && !what) r = rk, what = "ncclSend";
+      }
+      hipSetDevice(devs[0]);
+      for (int k = 0; k < n; k++) {
+        const ncclResult_t rk = ncclRecv(gathered + (size_t)k * count, count, ncclFloat64, k, c0->comms[0], nullptr);
+        if (rk != ncclSuccess && !what) r = rk, what = "ncclRecv";
+      }
+      const ncclResult_t re = ncclGroupEnd();
+      if (re != ncclSuccess && !what) r = re, what = "ncclGroupEnd";
     }
-    hipSetDevice(devs[0]);
-    for (int k = 0; k < n; k++)
-      NCCLCHK(c0, ncclRecv(gathered + (size_t)k * count, count, ncclFloat64, k, c0->comms[0], nullptr));
-    NCCLCHK(c0, ncclGroupEnd());
+    if (what) {
+      for (size_t k = 0; k < c0->comms.size(); k++) {
+        hipSetDevice(c0->comm_devs[k]);
+        ncclCommDestroy(c0->comms[k]);
+      }
+      c0->comms.clear();
+      c0->comm_devs.clear();
+      hipSetDevice(devs[0]);
+      return fail(c0, RTX_ERCCL, "%s: %s", what, ncclGetErrorString(r));
+    }
   } else {
     // several ranks on one device (more workers than GPUs): device copies
     for (int k = 0; k < n; k++) {
@@ -1251,11 +1292,21 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
   HIPCHK(c0, launch_unpack(gathered, W, H, tile_rows, n, R, frame, (size_t)W * 3, nullptr));
   HIPCHK(c0, hipMemcpy2D(out, row_stride * sizeof(double), frame, (size_t)W * 3 * sizeof(double),
                          (size_t)W * 3 * sizeof(double), H, hipMemcpyDeviceToHost));
-  for (int k = 0; k < n; k++) {                 // the ranks' reference raises
-    const rtx_status e = rtx_sync(ctxs[k], nullptr);
-    if (e) return fail(c0, e, "rank %d: %s", k, rtx_last_error(ctxs[k]));
+  // the ranks' reference raises, merged: the first in render_sync order over
+  // the whole frame (pixel keys do not depend on the rank that rendered them)
+  ErrState all;
+  all.flags = 0;
+  for (int code = 0; code < 5; code++) all.first[code] = ~0ull;
+  for (int k = 0; k < n; k++) {
+    ErrState e;
+    const rtx_status st = take_errors(ctxs[k], nullptr, &e);
+    if (st) return fail(c0, st, "rank %d: %s", k, rtx_last_error(ctxs[k]));
+    all.flags |= e.flags;
+    for (int code = 0; code < 5; code++)
+      if (e.first[code] < all.first[code]) all.first[code] = e.first[code];
   }
-  return RTX_OK;
+  hipSetDevice(devs[0]);
+  return report_errors(c0, all);
 }
 
 int32_t rtx_device_count(void) {

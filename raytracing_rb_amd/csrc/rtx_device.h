@@ -957,15 +957,17 @@ __device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3
   }, err);
 }
 
-// `key` orders the raise sites as the reference meets them: x * height + y for
-// pixels (render_sync runs x in the outer loop, y in the inner one,
-// camera.rb:102-103), the ray index for rtx_trace.
+// `key` orders the raise sites as the reference meets them: (x * height + y) * 2
+// + phase for pixels (render_sync runs x in the outer loop, y in the inner one,
+// camera.rb:102-103; within a pixel render_at traces the pre samples before the
+// extra ones, camera.rb:72-97, so a pre-sample raise (phase 0) comes before an
+// extra-sample raise (phase 1) whatever their codes), the ray index for rtx_trace.
 __device__ __forceinline__ void record_error(ErrState* e, uint32_t code, unsigned long long key) {
   atomicOr(&e->flags, 1u << code);
   atomicMin(&e->first[code], key);
 }
-__device__ __forceinline__ unsigned long long px_key(int x, int y, int H) {
-  return (unsigned long long)x * (unsigned long long)H + (unsigned long long)y;
+__device__ __forceinline__ unsigned long long px_key(int x, int y, int H, int phase = 0) {
+  return ((unsigned long long)x * (unsigned long long)H + (unsigned long long)y) << 1 | (unsigned long long)phase;
 }
 
 __device__ __forceinline__ int row_to_y(const KParams& p, int row) {

@@ -493,7 +493,9 @@ __global__ __launch_bounds__(256) void k_finalize(KParams p, int phase) {
   o[0] = avg.x;
   o[1] = avg.y;
   o[2] = avg.z;
-  if (err) record_error(p.err, err, px_key(x, y, cam.height));
+  // phase 1: err is the pre-sample raise (already recorded by phase 0 with the
+  // smaller phase-0 key) or else the first extra-sample raise
+  if (err) record_error(p.err, err, px_key(x, y, cam.height, phase));
 }
 
 // ----------------------------------------------------------------- tile order

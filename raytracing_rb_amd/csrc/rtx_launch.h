@@ -13,7 +13,7 @@ namespace rtx {
 struct ErrState {
   unsigned int flags;              // bit (1 << code) for every code raised
   unsigned int pad;
-  unsigned long long first[5];     // per ERR_ code (rtx_vec3.h): min key (pixels: x*H + y, render_sync order; rays: index)
+  unsigned long long first[5];     // per ERR_ code (rtx_vec3.h): min key (pixels: (x*H + y)*2 + phase, render_sync order; rays: index)
 };
 
 // Bounce-level engine: one launch per tree level (or three,

@@ -1455,7 +1455,9 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
   o[0] = r.x;
   o[1] = r.y;
   o[2] = r.z;
-  if (err) record_error(p.err, err, px_key(x, y, cam.height));
+  // an extra sample's raise: after any pre-sample raise of this pixel, which
+  // pass 0 recorded with phase 0 (render_at traces the pre samples first)
+  if (err) record_error(p.err, err, px_key(x, y, cam.height, 1));
 }
 
 // Per batch: the control block (count0 = the batch's level-0 items, pass 1:

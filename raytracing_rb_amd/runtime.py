@@ -132,8 +132,10 @@ class Renderer:
     ENGINES = {0: "lanes", 1: "levels"}
 
     def engine(self):
-        """Name of the ray-tree engine the next render uses (option "engine")."""
-        return self.ENGINES[self.get_option("engine")]
+        """Name of the ray-tree engine the next render of this scene and camera
+        runs (read-only option "engine_effective": "engine", except that the
+        bounce-level engine hands cameras it cannot take to the lanes engine)."""
+        return self.ENGINES[self.get_option("engine_effective")]
 
     def level_stats(self):
         """Bounce-level engine statistics of the last render call: {"redo", "dropped", "rays": [per level]}."""

@@ -75,10 +75,13 @@ class DistributedFrame:
     the gather of frame i + 1 is issued (a collective waits for the stream it
     is issued from), so the single receive buffer is never overwritten early."""
 
-    def __init__(self, width, height, tile_rows, rank, nranks, device, buffers=1):
+    def __init__(self, width, height, tile_rows, rank, nranks, device, buffers=1, force_collective=False):
         import torch
         self.width, self.height = width, height
         self.tile_rows, self.rank, self.nranks = tile_rows, rank, nranks
+        # force_collective: issue the gather even with one rank (the GPU test of
+        # the multi-rank path runs it under a 1-rank RCCL group)
+        self.collective = nranks > 1 or force_collective
         self.rows = rows_per_rank(height, tile_rows, nranks)
         self.bufs = [torch.zeros((self.rows, width, 3), dtype=torch.float64, device=device)
                      for _ in range(max(1, buffers))]
@@ -101,7 +104,7 @@ class DistributedFrame:
         advance = buf is None
         buf = self.packed if buf is None else buf
         work = None
-        if self.nranks > 1:
+        if self.collective:
             chunks = list(self.gathered.chunk(self.nranks, 0)) if self.rank == 0 else None
             work = dist.gather(buf, chunks, dst=0, async_op=True)
         if advance:
@@ -116,7 +119,7 @@ class DistributedFrame:
         if work is not None:
             work.wait()
         if self.rank == 0:
-            src = buf if self.nranks == 1 else self.gathered
+            src = self.gathered if self.collective else buf
             self.frame.index_copy_(0, self.dst, src.index_select(0, self.src))
             return self.frame
         return None
@@ -124,3 +127,62 @@ class DistributedFrame:
     def gather(self):
         """ONE collective: every rank's packed tiles to rank 0; rank 0 returns the frame."""
         return self.gather_finish(self.gather_start())
+
+
+class PipelinedTiles:
+    """The multi-GPU frame step of bench.py (C3), frames pipelined: F renderers
+    (contexts) on F streams, frame i on context j = i mod F renders this rank's
+    tiles into packed buffer j; the current stream waits for it, finishes frame
+    i - 1's gather (rank 0 unpacks it; buffer j' may be rendered into again
+    after that, ``free_ev``), then starts frame i's gather asynchronously, so it
+    overlaps frame i + 1's render.  ``drain()`` finishes the last gather.
+
+    renderers: raytracing_rb_amd.runtime.Renderer, one per frame in flight;
+    streams: torch.cuda.Stream per renderer; on_frame(i, frame): rank 0's
+    callback with frame i (the DistributedFrame's frame tensor, reused)."""
+
+    def __init__(self, renderers, streams, width, height, tile_rows, rank, nranks, device, seed=1,
+                 force_collective=False, on_frame=None):
+        import torch
+        self.rs, self.streams = renderers, streams
+        self.F = len(renderers)
+        assert len(streams) == self.F
+        self.tile_rows, self.rank, self.nranks, self.seed = tile_rows, rank, nranks, seed
+        self.stream = torch.cuda.current_stream(device)
+        self.df = DistributedFrame(width, height, tile_rows, rank, nranks, device, buffers=self.F,
+                                   force_collective=force_collective)
+        self.pending = []
+        self.free_ev = [None] * self.F
+        self.on_frame = on_frame
+        self.i = 0              # frames started
+        self.done = 0           # frames gathered
+
+    def _finish_one(self):
+        import torch
+        h, jj = self.pending.pop(0)
+        frame = self.df.gather_finish(h)
+        if self.on_frame is not None and self.rank == 0:
+            self.on_frame(self.done, frame)
+        self.done += 1
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        self.free_ev[jj] = ev
+
+    def step(self):
+        import torch
+        j = self.i % self.F
+        self.i += 1
+        if self.free_ev[j] is not None:
+            self.streams[j].wait_event(self.free_ev[j])
+        self.rs[j].render_tiles_device(self.df.bufs[j].data_ptr(), self.tile_rows, self.rank, self.nranks,
+                                       seed=self.seed, stream=self.streams[j].cuda_stream)
+        done = torch.cuda.Event()
+        done.record(self.streams[j])
+        while self.pending:
+            self._finish_one()
+        self.stream.wait_event(done)
+        self.pending.append((self.df.gather_start(self.df.bufs[j]), j))
+
+    def drain(self):
+        while self.pending:
+            self._finish_one()

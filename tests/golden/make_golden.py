@@ -10,6 +10,8 @@ Fixtures (numpy .npz, data only):
   vectors.npz       counter-RNG values, Camera#lens_func rays, trace_sync colours
   c2_full_columns64.npz  every 64th column of the full-size C2 frame, by the C
                     restatement (the GPU test renders the whole frame)
+  c4_full_columns256.npz every 256th column of the full-size C4 frame (3840x2160,
+                    8xAA, depth 8, 4096 spheres), by the C restatement
   frame_c4_48x27.npz the 4096-sphere C4 scene: rendered by the C restatement
                     (oracle/rt_oracle.c, bit-checked against rt_ref.py on the other
                     frames and on sampled C4 pixels in tests/test_oracle.py), since
@@ -108,6 +110,26 @@ def c2_columns(stride=64, nprocs=8):
     print("c2 columns", cols.size, full[:, cols].mean(axis=(0, 1)))
 
 
+def c4_columns(stride=256, nprocs=8):
+    """C4 (the LDS scene-staging stress config) at its full 3840x2160, 8xAA,
+    depth 8 over 4,097 objects: every `stride`-th column (15 columns, 32,400
+    pixels) by the C restatement in forked column bands (rto_render_fork, the
+    fork_jobs counterpart, camera.rb:41-68).  The world file is generated
+    (tools/make_scenes.py ensure_c4, seeded), so its sha is kept to detect drift."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_scenes
+    from oracle.c_oracle import Oracle
+    from raytracing_rb_amd import config
+    world = make_scenes.ensure_c4()
+    sd, cd = config.load_scene(world, os.path.join(SC, "c4_camera.yml"))
+    full = Oracle(sd, cd).render_fork(nprocs, stride)
+    cols = np.arange(0, cd.width, stride)
+    np.savez_compressed(os.path.join(HERE, "c4_full_columns%d.npz" % stride), columns=cols,
+                        frame=full[:, cols, :], scene_sha=sha(world),
+                        camera_sha=sha(os.path.join(SC, "c4_camera.yml")), seed=1, source="rt_oracle.c")
+    print("c4 columns", cols.size, full[:, cols].mean(axis=(0, 1)))
+
+
 def main(only=None):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import make_scenes
@@ -130,6 +152,8 @@ def main(only=None):
         print(name, fb.shape, "errors", int((st != 0).sum()), "mean", fb.mean(axis=(0, 1)))
     if not only or "c2_columns" in only:
         c2_columns()
+    if not only or "c4_columns" in only:
+        c4_columns()
     if not only or "vectors" in only:
         np.savez_compressed(os.path.join(HERE, "vectors.npz"), **vectors())
         print("vectors")

@@ -539,3 +539,94 @@ def test_first_raise_in_render_sync_order(gpu, tmp_path):
         assert e.value.kind == "color_gt1", (engine, opts, str(e.value))
         msgs.append(str(e.value))
     assert len(set(msgs)) == 1, msgs
+
+
+PRE_EXTRA_WORLD = """max_distance: 10000
+soft_shadow_exponent: 2
+lights:
+  - type: Spot
+    properties:
+      name: side
+      position: [2.0, -30.0, 4.0]
+      radius: 0.0
+      color: [1.0, 1.0, 1.0]
+      high_light_rate: 1.0
+      high_light_angle: 0.5
+world_objects:
+  - type: Plane
+    properties:
+      name: wall
+      point: [5.0, 0, 0]
+      front: [-1, 0, 0]
+      up: [0, 0, 1]
+      u_unit: 1.0
+      v_unit: 1.0
+      diffuse_rate: [0.3, 0.3, 0.3]
+      ambient: [0.02, 0.02, 0.02]
+      reflective_attenuation: [0.0, 0.0, 0.0]
+      texture_file_path: %s
+      texture_horizontal_scale: 0.0
+      texture_vertical_scale: 0.0
+  - type: Sphere
+    properties:
+      name: glow
+      center: [3.0, 1.597, 1.51]
+      radius: 0.012
+      refractive_rate: 1.5
+      diffuse_rate: [0.5, 0.5, 0.5]
+      ambient: [2.0, 2.0, 2.0]
+      reflective_attenuation: [0.0, 0.0, 0.0]
+      refractive_attenuation: [0.0, 0.0, 0.0]
+"""
+PRE_EXTRA_CAMERA = """position: [0.0, 0.0, 0.0]
+up: [0.0, 0.0, 1.0]
+front: [1.0, 0.0, 0.0]
+retina_width: 0.5
+retina_height: 0.5
+aperture_radius: 0.1
+image_distance: 1.0
+focal_distance: 0.990099
+width: 1
+height: 1
+pre_sample_times: 1
+max_sample_times: 8
+variant_threshold: 0.0
+trace_depth: 2
+monte_carlo_diffusion_times: 1
+"""
+
+
+def test_pre_sample_raise_before_extra_sample_raise(gpu, tmp_path):
+    """One pixel, two raise codes: its pre sample meets the wall, whose texture
+    scale 0 makes Texture#color's to_i raise FloatDomainError (texture.rb:24,
+    code 3); an extra sample (the lens aperture moves it) meets a glowing sphere
+    first (color greater than 1, code 2).  render_at traces the pre samples
+    before the extra ones (camera.rb:72-97), so the reference raises the domain
+    error although its code is the larger one: both engines, split phases and
+    no compaction report "domain" as the oracle does (a tie on the
+    pixel key used to go to the smaller code)."""
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import RtxError
+    from oracle.c_oracle import Oracle
+    w, c = tmp_path / "w.yml", tmp_path / "c.yml"
+    w.write_text(PRE_EXTRA_WORLD % os.path.join(SCENES, "textures", "checker.png"))
+    c.write_text(PRE_EXTRA_CAMERA)
+    sd, cd = config.load_scene(str(w), str(c))
+    o = Oracle(sd, cd)
+    keys = np.array([[0, 0, j] for j in range(8)], np.int32)
+    chosen = None
+    for seed in range(1, 200):              # a seed whose samples raise: 3, then 2 before any other 3
+        rays = np.array([o.lens(0, 0, j, seed) for j in range(8)])
+        _, st, _ = o.trace(rays, keys, seed)
+        extra = [int(s) for s in st[1:] if s]
+        if st[0] == 3 and extra and extra[0] == 2:
+            chosen = seed
+            break
+    assert chosen is not None
+    _, status, rc = o.render(seed=chosen)
+    assert rc == 3 and status[0, 0] == 3
+    for engine, opts in ((0, {}), (1, {}), (1, dict(lv_split=1)), (1, dict(lv_compact=0))):
+        with pytest.raises(RtxError) as e:
+            _renderer(sd, cd, engine, **opts).render(seed=chosen)
+        assert e.value.kind == "domain", (engine, opts, str(e.value))
+        assert "pixel (0,0)" in str(e.value)

@@ -81,6 +81,19 @@ def test_c1_full_size_bit_exact(gpu):
     rms, exact = _check(fb, ref, min_exact=0.999)
 
 
+def test_c0_configured_size_vs_oracle(gpu):
+    """C0 (BASELINE configs[0]: the reference's config/world.yml at
+    scenes/c0_camera.yml's 320x240, no AA, depth 1) at its configured size, every
+    pixel against the C oracle rendered live."""
+    from oracle.c_oracle import Oracle
+    sd, cd = _scene("c0_world.yml", "c0_camera.yml")
+    assert (cd.width, cd.height) == (320, 240)
+    fb = _renderer(sd, cd).render()
+    ref, st, rc = Oracle(sd, cd).render()
+    assert rc == 0 and not st.any()
+    _check(fb, ref, min_exact=0.99)
+
+
 def test_c2_full_size_vs_oracle_columns(gpu):
     """C2 (the metric config) at full 1920x1080, 4xAA, depth 5: the whole frame on
     the GPU; every 64th column (32,400 pixels) against the C oracle's committed
