@@ -99,6 +99,7 @@ struct KParams {
   int32_t lds_ring;                // k_level (compacting): LDS byte offset of the per-wave hit rings
   int32_t lv_grid_div;             // level launches: persistent grid = resident workgroups / this (option lv_grid_div)
   int32_t lv_fin_cap;              // tree reduction: records of a tile gathered into LDS (0: walk from global memory)
+  int32_t lv_fin_tiles;            // tree reduction pass 0: tiles of the batch (grid-stride loop when the grid is smaller)
   int32_t lv_redo_blocks;          // the lanes-engine re-render of overflowed samples: at most this many workgroups (0: all resident)
 };
 

@@ -1139,9 +1139,8 @@ __device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, 
 // render_at's per-pixel stage of pass 0 (camera.rb:70-99) once a tile's
 // 64 x pre sample colours / raises are in LDS (scol, serr): 64 threads, one
 // per pixel of the tile.
-__device__ __forceinline__ void lv_tile_pixels(const KParams& p, const double* scol, const uint32_t* serr) {
+__device__ __forceinline__ void lv_tile_pixels(const KParams& p, const double* scol, const uint32_t* serr, int slot) {
   const int pre = p.pre;
-  const int slot = blockIdx.x;
   const int l = (int)threadIdx.x;
   if (l >= 64) return;
   const int tiles_x = (p.nx + 7) >> 3;
@@ -1202,29 +1201,36 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
   extern __shared__ uint32_t lds_fin[];
   uint32_t* pex = lds_fin;
   const unsigned long long ts0 = RTX_STAMPS ? stamp() : 0ull;   // RTX_STAMPS diagnostic build only
-  lv_layout(p, nlev, base, pex);
+  lv_layout(p, nlev, base, pex);               // once per block: every tile of the batch shares it
   const unsigned long long ts1 = RTX_STAMPS ? stamp() : 0ull;
   const int pre = p.pre;
-  const int slot = blockIdx.x;                 // tile of the batch
   uint32_t* lo = lds_fin + nlev * 64 + threadIdx.x;
   uint32_t* hi = lo + SD * 256;
   double* scol = reinterpret_cast<double*>(lds_fin + nlev * 64 + (SD > 16 ? 0 : 2 * SD * 256));   // 64 * pre * 3
   uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
   uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];  // deep trees: private stack
   const int n_items = 64 * pre;
-  const int item0 = slot * n_items;
-  for (int it = (int)threadIdx.x; it < n_items; it += 256) {
-    const ItemPos ip = decode_item(p, item0 + it);
-    if (!ip.valid) continue;
-    uint32_t e = 0;
-    const V3 c = SD > 16 ? lv_sample(p, base, pex, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
-                         : lv_sample(p, base, pex, item0 + it, nlev, lo, hi, 256, SD, e);
-    scol[3 * it] = c.x;
-    scol[3 * it + 1] = c.y;
-    scol[3 * it + 2] = c.z;
-    serr[it] = e;
+  // one block per tile, or (lv_fin_tiles > gridDim.x) a grid-stride loop over
+  // the batch's tiles, so the layout above is read once per block
+  const int n_tiles = p.lv_fin_tiles > (int)gridDim.x ? p.lv_fin_tiles : (int)gridDim.x;
+  for (int slot = blockIdx.x; slot < n_tiles; slot += gridDim.x) {
+    const int item0 = slot * n_items;
+    for (int it = (int)threadIdx.x; it < n_items; it += 256) {
+      const ItemPos ip = decode_item(p, item0 + it);
+      if (!ip.valid) continue;
+      uint32_t e = 0;
+      const V3 c = SD > 16 ? lv_sample(p, base, pex, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
+                           : lv_sample(p, base, pex, item0 + it, nlev, lo, hi, 256, SD, e);
+      scol[3 * it] = c.x;
+      scol[3 * it + 1] = c.y;
+      scol[3 * it + 2] = c.z;
+      serr[it] = e;
+    }
+    __syncthreads();
+    lv_tile_pixels(p, scol, serr, slot);
+    __syncthreads();                           // scol / serr are reused by the next tile
   }
-  if (RTX_STAMPS) {                           // layout / walks (wave lifetime parts), waves
+  if (RTX_STAMPS) {                           // layout / walks + pixels (wave lifetime parts), waves
     const unsigned long long ts2 = stamp();
     if (__lane_id() == 0) {
       atomicAdd(&rtx_stamps[11], ts1 - ts0);
@@ -1232,8 +1238,6 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
       atomicAdd(&rtx_stamps[13], 1ull);
     }
   }
-  __syncthreads();
-  lv_tile_pixels(p, scol, serr);
 }
 
 // The same reduction with the tile's trees gathered into LDS first (option
@@ -1417,7 +1421,7 @@ __global__ __launch_bounds__(256) void k_tree_finalize_g(KParams p, int nlev) {
     }
   }
   __syncthreads();
-  lv_tile_pixels(p, scol, serr);
+  lv_tile_pixels(p, scol, serr, blockIdx.x);
 }
 
 // Pass 1: one thread per extra-list entry of the batch: (pre mean * pre +
@@ -1610,7 +1614,16 @@ static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStrea
   const size_t stack = (size_t)nlev * 64 * 4 + (SD > 16 ? 0 : (size_t)SD * 2 * 256 * 4);
   if (q.lv_pass == 0) {                        // n = tiles of the batch
     const size_t lds = ((stack + 7) & ~(size_t)7) + (size_t)64 * q.pre * 28;
-    hipLaunchKernelGGL(k_tree_finalize<SD>, dim3((unsigned)n), dim3(256), lds, s, q, nlev);
+    KParams r = q;
+    long grid = n;
+    if (q.lv_fin_tiles > 0) {                  // lv_fin_grid blocks per CU, grid-stride over the tiles
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+        grid = std::min<long>(n, (long)cus * q.lv_fin_tiles);
+    }
+    r.lv_fin_tiles = n;
+    hipLaunchKernelGGL(k_tree_finalize<SD>, dim3((unsigned)grid), dim3(256), lds, s, r, nlev);
   } else {                                     // n = extra-list entries of the batch
     hipLaunchKernelGGL(k_tree_finalize_extra<SD>, dim3((unsigned)((n + 255) / 256)), dim3(256), stack, s, q, nlev);
   }

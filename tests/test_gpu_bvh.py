@@ -225,9 +225,21 @@ def test_c4_full_size_vs_oracle_columns_and_strip_bvh_equals_linear(gpu, c4_worl
     r = Renderer(sd, cd)
     fb = r.render(seed=int(z["seed"]))
     assert fb.shape == (2160, 3840, 3)
-    # 8 samples x depth 8: more ocml-vs-glibc ulp differences per pixel than C2
-    # (as test_c4_bvh_matches_golden_and_linear); same RMS / max-abs bounds.
-    _check(fb[:, z["columns"], :], z["frame"], min_exact=0.8)
+    # 8 samples x depth 8 over 4,096 spheres: more ocml-vs-glibc ulp differences
+    # per pixel than C2 (sin/cos/asin/acos are the only functions that differ,
+    # DESIGN.md §2), carried through up to 8 bounces.  Measured (r05a) max |diff|
+    # 1.9e-8 on these 32,400 pixels: the size a 1-ulp difference takes after an
+    # ill-conditioned step such as the penumbra's acos near 1 (sphere.rb:43-46,
+    # d acos/dx = -1/sqrt(1 - x^2)).  The north-star bound (per-channel RMS <=
+    # 1e-4) is the test; max |diff| is bounded at 1e-6 here.
+    d = fb[:, z["columns"], :] - z["frame"]
+    rms = np.sqrt((d.reshape(-1, 3) ** 2).mean(axis=0))
+    exact = np.mean(np.all(d == 0, axis=-1))
+    print("C4 full-size columns: per-channel RMS %s, max |diff| %.3g, bit-exact pixels %.4f, pixels > 1e-9: %d"
+          % (rms, np.abs(d).max(), exact, int((np.abs(d).max(axis=-1) > 1e-9).sum())))
+    assert (rms <= 1e-4).all(), rms
+    assert np.abs(d).max() <= 1e-6, np.abs(d).max()
+    assert exact >= 0.8, exact
     assert np.isfinite(fb).all() and (fb >= 0).all() and (fb <= 1).all()
     assert fb.mean() > 0.01
     lin = Renderer(sd, cd)

@@ -13,6 +13,8 @@
 #       stamps         = phase stamps of the levels engine (diagnostic build _variants/librtx_stamps.so):
 #                        bash tools/gpu_session.sh TAG stamps SCENE OPT...   (OPT as key=value)
 # ENGINE: rtx engine option for the PMC passes (0 lanes, 1 levels; default: the library default)
+# WL (environment): workload of the pmc / pmcbench modes, c2 (default) or c4
+#       pmcbench       = PMC passes + the workload's bench line + its single-frame kernel-trace summary
 # Every GPU step has its own time limit; steps are chained with && (stop at the first failure).
 set -o pipefail
 export TMPDIR=/tmp
@@ -24,6 +26,7 @@ if [ "$MODE" != timing ] && [ "$MODE" != stamps ]; then ENGINE=${1:-}; fi
 OUT=gpurun_out/$TAG
 mkdir -p $OUT profiles
 ENGOPT='{}'
+WL=${WL:-c2}
 ENGNAME=$(python3 -c "import sys; sys.path.insert(0,'.'); print({'0':'lanes','1':'levels'}.get('$ENGINE','default'))")
 if [ -n "$ENGINE" ]; then ENGOPT="{\"engine\": $ENGINE}"; fi
 
@@ -36,7 +39,7 @@ smoke() {
 pmcpass() {  # name counters...   (one rocprofv3 run per pass; 1 warm-up + 3 timed frames)
   local n=$1; shift
   timeout -k 5 -s KILL 180 rocprofv3 --pmc "$@" --kernel-trace -d $OUT/pmc_$n -o $n --output-format csv -- \
-    python3 tools/timing.py --scene c2 --reps 3 "$ENGOPT" > $OUT/pmc_$n.log 2>&1
+    python3 tools/timing.py --scene $WL --reps 3 "$ENGOPT" > $OUT/pmc_$n.log 2>&1
 }
 pmc() {
   (timeout -k 5 -s KILL 60 rocprofv3 -L > $OUT/rocprof_counters.txt 2>&1 || true) && \
@@ -48,17 +51,17 @@ pmc() {
   { if grep -q "SQ_INST_CYCLES_VALU" $OUT/rocprof_counters.txt; then pmcpass e SQ_INST_CYCLES_VALU SQ_INSTS_VALU; else true; fi; } && \
   DIRS="$OUT/pmc_a $OUT/pmc_b $OUT/pmc_c $OUT/pmc_d $OUT/pmc_f" && \
   { [ -d $OUT/pmc_e ] && DIRS="$DIRS $OUT/pmc_e"; true; } && \
-  python3 tools/pmc_json.py $OUT/pmc_c2.json $DIRS --workload c2 --frames 4 --skip 1 --session $TAG \
+  python3 tools/pmc_json.py $OUT/pmc_$WL.json $DIRS --workload $WL --frames 4 --skip 1 --session $TAG \
     --engine $(python3 -c "
 import sys; sys.path.insert(0,'.')
 from raytracing_rb_amd import config
 from raytracing_rb_amd.runtime import Renderer
 import json
-sd, cd = config.load_scene('scenes/c2_world.yml', 'scenes/c2_camera.yml', camera_overrides={'width': 8, 'height': 8})
+sd, cd = config.load_scene('scenes/c2_world.yml', 'scenes/${WL}_camera.yml', camera_overrides={'width': 8, 'height': 8})
 r = Renderer(sd, cd)
 for k, v in json.loads('$ENGOPT').items(): r.set_option(k, v)
 print(r.engine())") > $OUT/pmc_json.log 2>&1 && \
-  cp $OUT/pmc_c2.json profiles/pmc_c2.json
+  cp $OUT/pmc_$WL.json profiles/pmc_$WL.json
 }
 bench() {
   timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err && \
@@ -70,6 +73,11 @@ bench() {
 }
 bench_c4() {
   timeout -k 10 600 python bench.py --workload c4 --steps 3 --warmup 1 > $OUT/bench_c4.json 2> $OUT/bench_c4.err
+}
+bench_c4_single() {   # the C4 roofline's kernel time: one frame alone, one context (as prof_single for C2)
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_single_c4 -o kt --output-format csv -- \
+    python3 bench.py --workload c4 --inflight 1 --option lv_streams=1 --steps 2 --warmup 1 --no-cpu-baseline \
+    --no-projection > $OUT/prof_single_c4.json 2> $OUT/prof_single_c4.err
 }
 
 levels() {
@@ -99,6 +107,7 @@ case $MODE in
   full)  tests && smoke && pmc && bench && bench_c4 ;;
   quick) tests && timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err ;;
   pmc)   pmc && bench ;;
+  pmcbench) if [ "$WL" = c4 ]; then pmc && bench_c4 && bench_c4_single; else pmc && bench; fi ;;
   bench) bench ;;
   *) echo "unknown mode $MODE"; false ;;
 esac
