@@ -50,6 +50,10 @@ constexpr int RAY_DOUBLES = 12;          // staging ray record: o, d, att, path,
 constexpr int HIT_DOUBLES = 8;           // split hit record: hit, hit + delta, {ray, object | in}, {slot, raises}
 static_assert(RAY_DOUBLES * 8 == (int)RAY_BYTES && HIT_DOUBLES * 8 == (int)LV_HIT_BYTES, "record sizes");
 
+// Diagnostic builds: the level kernels' phases per tree level (levels >= 7
+// summed into row 7): 6 phases, chunks, lanes with a hit.
+static __device__ unsigned long long rtx_stamps_lv[8 * 8];
+
 int levels_rec_bytes(int n_light) {
   const int nl = n_light > 1 ? n_light : 1;
   return (8 + 24 * nl + 15) & ~15;       // {meta, first child} + one leaf per fired light
@@ -591,6 +595,10 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
     atomicAdd(&rtx_stamps[8], nA);
     atomicAdd(&rtx_stamps[9], nE);
     atomicAdd(&rtx_stamps[10], nS);
+    unsigned long long* lv = rtx_stamps_lv + 8 * (level < 7 ? level : 7);
+    for (int k = 0; k < 6; k++) atomicAdd(&lv[k], tS[k]);
+    atomicAdd(&lv[6], nchunks);
+    atomicAdd(&lv[7], nS);
   }
 }
 
@@ -832,6 +840,10 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     atomicAdd(&rtx_stamps[8], nA);
     atomicAdd(&rtx_stamps[9], nE);
     atomicAdd(&rtx_stamps[10], nS);
+    unsigned long long* lv = rtx_stamps_lv + 8 * (level < 7 ? level : 7);
+    for (int k = 0; k < 6; k++) atomicAdd(&lv[k], tS[k]);
+    atomicAdd(&lv[6], nchunks);
+    atomicAdd(&lv[7], nS);
   }
 }
 
@@ -1511,6 +1523,15 @@ int read_level_stamps(unsigned long long* out, int reset) {
   if (reset) {
     unsigned long long z[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(rtx_stamps), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+
+extern "C" int rtxdbg_read_level_stamps(unsigned long long* out, int reset) {   // diagnostic builds: [8 levels][8]
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtx_stamps_lv), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[64] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtx_stamps_lv), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;
 }

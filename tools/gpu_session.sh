@@ -10,7 +10,7 @@
 #                        (SHARE = k/N for one rank's share, or - for the whole frame; each OPT a JSON
 #                        option set; output $OUT/timing_SCENE[_shareN].log)
 #       baseline       = BASELINE.md's table (tools/baseline_table.py: CPU restatement + 1-GPU + projections)
-#       stamps         = phase stamps of the levels engine (diagnostic build _variants/librtx_stamps.so):
+#       stamps         = phase stamps of the levels engine (diagnostic build diag/librtx_stamps.so):
 #                        bash tools/gpu_session.sh TAG stamps SCENE OPT...   (OPT as key=value)
 # ENGINE: rtx engine option for the PMC passes (0 lanes, 1 levels; default: the library default)
 # WL (environment): workload of the pmc / pmcbench modes, c2 (default) or c4
@@ -91,7 +91,7 @@ timing() {  # SCENE REPS SHARE OPT...
 }
 stamps() {  # SCENE OPT...
   local scene=$1; shift
-  RTX_LIB=_variants/librtx_stamps.so timeout -k 10 120 python3 tools/stamps_levels.py $scene "$@" \
+  RTX_LIB=${STAMPS_LIB:-diag/librtx_stamps.so} timeout -k 10 120 python3 tools/stamps_levels.py $scene "$@" \
     > $OUT/stamps_${scene}_$(echo "$@" | tr ' =' '_-').log 2>&1
 }
 

@@ -25,9 +25,12 @@ lib = _abi.load_library()
 out = torch.empty((cd.height, cd.width, 3), dtype=torch.float64, device="cuda")
 r.render_device(out.data_ptr()); r.sync()
 st = (ctypes.c_ulonglong * 16)()
+lv = (ctypes.c_ulonglong * 64)()
 lib.rtxdbg_read_stamps(st, 1)
+lib.rtxdbg_read_level_stamps(lv, 1)
 r.render_device(out.data_ptr()); r.sync()
 lib.rtxdbg_read_stamps(st, 1)
+lib.rtxdbg_read_level_stamps(lv, 1)
 v = list(st)
 tot = sum(v[:6])
 names = ["A claim/load/lens/highlight", "B EXTEND walk", "C hit_info/normal/cos", "D SHADOW walks + lights",
@@ -42,3 +45,12 @@ if v[13]:
     print("k_tree_finalize: %d waves, per wave %.0f cycles slice layout + %.0f cycles tree walks"
           " (of which LDS gather %.0f)" % (v[13], v[11] / v[13], v[12] / v[13], v[14] / v[13]))
 
+
+print("per level: cycles per chunk by phase A-F, chunks, hit lanes per chunk")
+for d in range(8):
+    row = list(lv[8 * d: 8 * d + 8])
+    if not row[6]:
+        continue
+    c = row[6]
+    print("  level %d%s: chunks %8d  hit %5.1f  total %7.0f  A %6.0f B %6.0f C %6.0f D %6.0f E %6.0f F %6.0f" % (
+        d, "+" if d == 7 else " ", c, row[7] / c, sum(row[:6]) / c, *[x / c for x in row[:6]]))
