@@ -277,7 +277,7 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
    keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
          2 always; every choice renders the same bits), "bvh_min" [32], "bvh_sah" (1 [default] binned-SAH hierarchy
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
-         staging, 1 scalar loads), "lds_stack" (ray-stack entries per lane kept in LDS,
+         staging, 1 scalar loads, 2 nodes in LDS and leaves global), "lds_stack" (ray-stack entries per lane kept in LDS,
          -1 = as many as fit), "force_stack" (per-lane ray-stack bucket), "postpone" (hierarchy walks
          still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never), "tile_order" (1 expensive
          8x8 tiles first by a primary-hit probe, 0 row-major, -1 [default] = 1 up to 512 spheres; the order
@@ -292,12 +292,16 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          rest claimed from sharded counters; -1 [default] = 100 up to 512 spheres, else 50; same bits),
          "lv_compact" (bounce levels: 1 park the rays that hit something in a per-wave LDS ring and run the
          shadow walks and shading on full waves, 0 off, -1 [default] = on whenever the rings fit the walk's
-         LDS; same bits), "lv_streams" (bounce levels: the region's 8x8 tiles in this many interleaved parts,
+         LDS; a hierarchy too large for the full ring next to it gets the compact ring (hit point and ids only,
+         the ray re-derived); 2 = the compact ring always; same bits), "lv_streams" (bounce levels: the region's 8x8 tiles in this many interleaved parts,
          1..4, rendered at once on as many HIP streams, parts 1.. on streams the context owns; one part's level
          tails and reductions overlap the others' work; 2 [default]; same bits), "lv_grid_div" (bounce levels:
          level grids = resident workgroups / this, 1 [default]), "lv_redo_blocks" (bounce levels: at most this
          many workgroups for the lanes-engine re-render of overflowed samples, launched after every batch and
-         nearly always empty; 8 [default], 0 = every resident workgroup; same bits). */
+         nearly always empty; 8 [default], 0 = every resident workgroup; same bits), "lv_fin_grid" (bounce levels:
+         0 [default] one tree-reduction block per 8x8 tile, k > 0 k blocks per CU looping over the tiles; measured
+         neutral on C2), "sphere_src" also 2 (hierarchy nodes staged in LDS, leaf records read from global memory:
+         leaves room for the hit rings; bounce-level engine). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

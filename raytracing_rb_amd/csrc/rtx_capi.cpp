@@ -517,8 +517,8 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_lv_streams = value;
     return RTX_OK;
   }
-  if (!strcmp(key, "lv_compact")) {        // bounce levels: hit compaction in k_level, -1 auto
-    if (value < -1 || value > 1) return fail(c, RTX_EINVAL, "lv_compact must be -1, 0 or 1");
+  if (!strcmp(key, "lv_compact")) {        // bounce levels: hit compaction in k_level, -1 auto, 2 compact ring
+    if (value < -1 || value > 2) return fail(c, RTX_EINVAL, "lv_compact must be -1, 0, 1 or 2");
     c->opt_lv_compact = value;
     return RTX_OK;
   }
@@ -526,8 +526,8 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_kernel_events = value != 0;
     return RTX_OK;
   }
-  if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads
-    if (value < 0 || value > 1) return fail(c, RTX_EINVAL, "sphere_src must be 0 or 1");
+  if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads; 2: hierarchy nodes in LDS, leaves global
+    if (value < 0 || value > 2) return fail(c, RTX_EINVAL, "sphere_src must be 0, 1 or 2");
     c->opt_sphere_src = value;
     return RTX_OK;
   }
@@ -804,7 +804,8 @@ static int required_stack(const rtx_context* c) {
 // loads when the records exceed the LDS budget.
 static int sph_mode(const rtx_context* c) {
   const bool bvh = c->opt_bvh == 2 || (c->opt_bvh == 1 && c->scene.n_sphere >= c->opt_bvh_min);
-  if (bvh && c->scene.bvh_root != BVH_NONE) return c->opt_sphere_src ? SPH_BVH_GLOBAL : SPH_BVH_LDS;
+  if (bvh && c->scene.bvh_root != BVH_NONE)
+    return c->opt_sphere_src == 2 ? SPH_BVH_MIX : c->opt_sphere_src ? SPH_BVH_GLOBAL : SPH_BVH_LDS;
   return c->opt_sphere_src ? SPH_LIN_SCALAR : SPH_LIN_LDS;
 }
 

@@ -84,6 +84,12 @@ enum { SRC_PIXELS = 0, SRC_RAYS = 1, SRC_EXTRA = 2, SRC_LIST = 3 };
 #define RTX_LVL_WPS 2        // waves per SIMD k_level is compiled for
 #endif
 static __device__ unsigned long long rtx_stamps[16];   // one per translation unit (no -fgpu-rdc)
+#ifndef RTX_WALKSTATS
+#define RTX_WALKSTATS 0      // diagnostic build only: lane occupancy of the hierarchy walk's loops
+#endif
+// [0] wave iterations of the inner-node loop, [1] lanes in them, [2] leaf
+// visits (wave), [3] lanes in them; [4..7] the same for SHADOW walks
+static __device__ unsigned long long rtx_walkstats[8];
 __device__ __forceinline__ unsigned long long wall() {   // 100 MHz constant clock, same on every XCD
 #if RTX_STAMPS
   return __builtin_amdgcn_s_memrealtime();
@@ -519,9 +525,15 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
     }
   }
 
+  unsigned long long ws_ni = 0, ws_nl = 0, ws_li = 0, ws_ll = 0;   // RTX_WALKSTATS only
   while (ref != BVH_NONE) {
     // ---- inner nodes: slab-test the four child boxes, descend into the nearest
     while (ref >= 0 && ref != BVH_NONE) {
+      if (RTX_WALKSTATS) {
+        const unsigned long long am = __ballot(1);
+        ws_nl++;
+        if ((int)__lane_id() == __builtin_ctzll(am)) ws_ni++;
+      }
       float key[4];
       int ch[4];
 #pragma unroll
@@ -557,6 +569,11 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
     }
     if (ref == BVH_NONE) break;
     // ---- leaf: pre-test its spheres, exact test for those not ruled out
+    if (RTX_WALKSTATS) {
+      const unsigned long long am = __ballot(1);
+      ws_ll++;
+      if ((int)__lane_id() == __builtin_ctzll(am)) ws_li++;
+    }
     {
       const int v = ~ref;
       const int slot0 = (v >> 2) * BVH_LEAF;
@@ -610,6 +627,13 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
     }
     ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
     if (PP && __popcll(__ballot(ref != BVH_NONE)) < postpone && ref != BVH_NONE) return false;
+  }
+  if (RTX_WALKSTATS) {
+    unsigned long long* w = rtx_walkstats + (ext ? 0 : 4);
+    atomicAdd(&w[0], ws_ni);
+    atomicAdd(&w[1], ws_nl);
+    atomicAdd(&w[2], ws_li);
+    atomicAdd(&w[3], ws_ll);
   }
   if (!ext) {
     total = 1.0;
@@ -1027,15 +1051,15 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   const SceneDev& S = p.scene;
   size_t off = 0;
   if (mode == SPH_LIN_LDS) off = (size_t)(S.n_sphere + 4) * 16;
-  if (mode == SPH_BVH_LDS) {
+  if (mode == SPH_BVH_LDS || mode == SPH_BVH_MIX) {
     off = (size_t)S.n_nodes * sizeof(Bvh4Node);
     p.lds_leaf = (int32_t)off;
-    off += (size_t)S.n_slots * 16;
+    if (mode == SPH_BVH_LDS) off += (size_t)S.n_slots * 16;
   }
   off = (off + 15) & ~(size_t)15;
   p.lds_stack = (int32_t)off;
   p.lds_cov = (int32_t)off;
-  if (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL) {
+  if (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL || mode == SPH_BVH_MIX) {
     off += (size_t)S.bvh_stack * bs * 4;
     off = (off + 15) & ~(size_t)15;
     p.lds_cov = (int32_t)off;
@@ -1044,7 +1068,8 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   // the bottom of every lane's ray stack, as many entries as fit the budget
   off = (off + 15) & ~(size_t)15;
   p.lds_items = (int32_t)off;
-  const size_t budget = (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL) ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
+  const size_t budget =
+      (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL || mode == SPH_BVH_MIX) ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
   const size_t per = (size_t)ITEM_WORDS * 8 * bs;
   int slots = budget > off ? (int)((budget - off) / per) : 0;
   if (slots > p.stk_slots_max) slots = p.stk_slots_max;

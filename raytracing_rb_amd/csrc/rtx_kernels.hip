@@ -665,6 +665,11 @@ size_t bvh_lds_bytes(int n_nodes, int n_slots, int bvh_stack) {
 size_t bvh_lds_budget() { return LDS_TOTAL_BYTES; }
 
 int resolve_mode(const SceneDev& S, int mode) {
+  if (mode == SPH_BVH_MIX) {                   // nodes in LDS, leaves global: needs room for the nodes
+    const size_t need = (size_t)S.n_nodes * sizeof(Bvh4Node) + (size_t)S.bvh_stack * BS_BVH * 4 +
+                        (size_t)COVER_K * BS_BVH * 12 + 64;
+    return need > LDS_TOTAL_BYTES ? SPH_BVH_GLOBAL : SPH_BVH_MIX;
+  }
   if (mode == SPH_LIN_LDS && (size_t)(S.n_sphere + 4) * 16 > LDS_SPHERE_BYTES) return SPH_LIN_SCALAR;
   if (mode == SPH_BVH_LDS && bvh_lds_bytes(S.n_nodes, S.n_slots, S.bvh_stack) > LDS_TOTAL_BYTES)
     return SPH_BVH_GLOBAL;
@@ -755,6 +760,7 @@ hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t 
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   if (tiles == 0) return hipSuccess;
   KevScope kscope(count ? nullptr : kev);
+  if (mode == SPH_BVH_MIX) mode = SPH_BVH_LDS;   // (the lanes engine stages the whole hierarchy or none)
   if (count) mode = (mode == SPH_LIN_LDS || mode == SPH_BVH_LDS) ? SPH_LIN_LDS : SPH_LIN_SCALAR;
   mode = resolve_mode(p.scene, mode);
   hipError_t e = hipMemsetAsync(p.extra_count, 0, sizeof(int32_t), s);
@@ -786,6 +792,7 @@ hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t 
 // could not hold (SRC_LIST; k_level_begin already zeroed its work counter).
 hipError_t launch_redo(const KParams& q, int mode, int maxs, int n, hipStream_t s) {
   g_work_zeroed = true;
+  if (mode == SPH_BVH_MIX) mode = resolve_mode(q.scene, SPH_BVH_LDS);   // (see launch_render)
   const hipError_t e = launch_src<SRC_LIST>(q, mode, false, maxs, n, s);
   g_work_zeroed = false;
   return e;
@@ -793,6 +800,7 @@ hipError_t launch_redo(const KParams& q, int mode, int maxs, int n, hipStream_t 
 
 hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s) {
   if (p.nrays == 0) return hipSuccess;
+  if (mode == SPH_BVH_MIX) mode = SPH_BVH_LDS;   // (see launch_render)
   mode = resolve_mode(p.scene, mode);
   switch (maxs) {
     case 8: return launch_mode<false, 8, SRC_RAYS>(p, mode, p.nrays, s);

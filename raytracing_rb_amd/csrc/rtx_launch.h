@@ -95,7 +95,7 @@ struct KParams {
   int32_t lv_static_pct;           // % of a level launch's chunks scheduled statically (the rest: sharded claims)
   double* lv_hit;                  // split: hit queue, LV_HIT_BYTES per hit, LV_SLICES << lv_hslice_log2 slots
   double* lv_area;                 // split: {1 - covers, raise} per (hit, light)
-  int32_t lv_compact;              // k_level: park hits in an LDS ring, shade full waves (-1 auto, 0 off, 1 on)
+  int32_t lv_compact;              // k_level: park hits in an LDS ring, shade full waves (-1 auto, 0 off, 1 on, 2 compact ring)
   int32_t lds_ring;                // k_level (compacting): LDS byte offset of the per-wave hit rings
   int32_t lv_grid_div;             // level launches: persistent grid = resident workgroups / this (option lv_grid_div)
   int32_t lv_fin_cap;              // tree reduction: records of a tile gathered into LDS (0: walk from global memory)
@@ -109,6 +109,9 @@ enum SphMode : int {
   SPH_LIN_SCALAR = 1,    // ordered linear walk, records by scalar loads
   SPH_BVH_LDS = 2,       // four-wide ball hierarchy, nodes + leaf records staged in LDS
   SPH_BVH_GLOBAL = 3,    // four-wide ball hierarchy, nodes + leaf records by scalar loads
+  SPH_BVH_MIX = 4,       // four-wide ball hierarchy, nodes staged in LDS, leaf records from global memory
+                         // (bounce-level engine only: room for the hit rings of k_level_c; the lanes
+                         // engine walks it as SPH_BVH_LDS)
 };
 
 // HIP event pairs recorded on the launch stream around every ray-tree kernel

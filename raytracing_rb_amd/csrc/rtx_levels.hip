@@ -254,11 +254,13 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
   if (SPH == SPH_LIN_LDS) {
     for (int i = threadIdx.x; i < S.n_sphere + 4; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
     __syncthreads();
-  } else if (SPH == SPH_BVH_LDS) {
+  } else if (SPH == SPH_BVH_LDS || SPH == SPH_BVH_MIX) {
     const int nn = S.n_nodes * (int)(sizeof(Bvh4Node) / 16);
     for (int i = threadIdx.x; i < nn; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.bvh)[i];
-    float4* leaf = reinterpret_cast<float4*>(lds + p.lds_leaf);
-    for (int i = threadIdx.x; i < S.n_slots; i += BS) leaf[i] = reinterpret_cast<const float4*>(S.bvh_sph32)[i];
+    if (SPH == SPH_BVH_LDS) {
+      float4* leaf = reinterpret_cast<float4*>(lds + p.lds_leaf);
+      for (int i = threadIdx.x; i < S.n_slots; i += BS) leaf[i] = reinterpret_cast<const float4*>(S.bvh_sph32)[i];
+    }
     __syncthreads();
   }
 }
@@ -281,6 +283,10 @@ __device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V
     bool q_ovf = false;
     if (SPH == SPH_BVH_LDS)
       query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
+                           stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp,
+                           q_ncov, q_ovf, false, 0);
+    else if (SPH == SPH_BVH_MIX)
+      query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(S.bvh_sph32),
                            stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp,
                            q_ncov, q_ovf, false, 0);
     else
@@ -626,12 +632,22 @@ __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level)
 // direction, {dense index, queue slot}, {object | :in << 31, raises}.  The
 // rest of the ray (attenuation, path, RNG key) is reloaded from the level's
 // queue (level 0: the camera sample's item).
+//
+// A compact ring (RF = 5 fields: the hit point, {dense index, queue slot},
+// {object | :in, raises}) is used when the full one does not fit next to the
+// walk's LDS (C4's hierarchy): the second half then re-derives the ray's
+// origin and direction, the same bits either way (level >= 1: reloaded from
+// the queue; level 0: Camera#lens_func re-evaluated for the item's key).
 constexpr int LV_RING = 128;
 constexpr int LV_RING_FIELDS = 11;
+constexpr int LV_RING_FIELDS_SMALL = 5;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
+constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMALL * 8;
 
-template <int SPH, int BS>
+template <int SPH, int BS, int RF>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
+  static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
+  constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
   const SceneDev& S = p.scene;
   extern __shared__ float4 lds_sph[];
   char* lds = reinterpret_cast<char*>(lds_sph);
@@ -644,7 +660,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
   const int slice = sched.wave_id() & (LV_SLICES - 1);
   const int lane = (int)__lane_id();
-  double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * LV_RING_WAVE_BYTES);
+  double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * ((size_t)LV_RING * RF * 8));
   uint32_t head = 0, pend = 0;                // wave-uniform: first parked slot, parked hits
   bool got = true;
 
@@ -733,14 +749,16 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         r[0 * LV_RING] = hit.x;
         r[1 * LV_RING] = hit.y;
         r[2 * LV_RING] = hit.z;
-        r[3 * LV_RING] = cur.ray.o.x;
-        r[4 * LV_RING] = cur.ray.o.y;
-        r[5 * LV_RING] = cur.ray.o.z;
-        r[6 * LV_RING] = cur.ray.d.x;
-        r[7 * LV_RING] = cur.ray.d.y;
-        r[8 * LV_RING] = cur.ray.d.z;
-        r[9 * LV_RING] = __builtin_bit_cast(double, (uint64_t)i | (uint64_t)slot << 32);
-        r[10 * LV_RING] = __builtin_bit_cast(
+        if (RF == LV_RING_FIELDS) {
+          r[3 * LV_RING] = cur.ray.o.x;
+          r[4 * LV_RING] = cur.ray.o.y;
+          r[5 * LV_RING] = cur.ray.o.z;
+          r[6 * LV_RING] = cur.ray.d.x;
+          r[7 * LV_RING] = cur.ray.d.y;
+          r[8 * LV_RING] = cur.ray.d.z;
+        }
+        r[FI * LV_RING] = __builtin_bit_cast(double, (uint64_t)i | (uint64_t)slot << 32);
+        r[(FI + 1) * LV_RING] = __builtin_bit_cast(
             double, (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) | (uint64_t)((errA & 0xffu) | (errL & 0xffu) << 8) << 32);
       }
       pend += (uint32_t)__popcll(hm);
@@ -761,10 +779,12 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     if (shade) {
       const double* r = ring + ((head + (uint32_t)lane) & (LV_RING - 1));
       hit = v3(r[0 * LV_RING], r[1 * LV_RING], r[2 * LV_RING]);
-      cur.ray.o = v3(r[3 * LV_RING], r[4 * LV_RING], r[5 * LV_RING]);
-      cur.ray.d = v3(r[6 * LV_RING], r[7 * LV_RING], r[8 * LV_RING]);
-      const uint64_t is = __builtin_bit_cast(uint64_t, r[9 * LV_RING]);
-      const uint64_t be = __builtin_bit_cast(uint64_t, r[10 * LV_RING]);
+      if (RF == LV_RING_FIELDS) {
+        cur.ray.o = v3(r[3 * LV_RING], r[4 * LV_RING], r[5 * LV_RING]);
+        cur.ray.d = v3(r[6 * LV_RING], r[7 * LV_RING], r[8 * LV_RING]);
+      }
+      const uint64_t is = __builtin_bit_cast(uint64_t, r[FI * LV_RING]);
+      const uint64_t be = __builtin_bit_cast(uint64_t, r[(FI + 1) * LV_RING]);
       i = (uint32_t)is;
       besti = (int)((uint32_t)be & 0x7fffffffu);
       hin = ((uint32_t)be >> 31) != 0;
@@ -778,8 +798,17 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         sample = ip.sample;
         cur.att = v3(1.0, 1.0, 1.0);
         cur.path = 1;
+        if (RF != LV_RING_FIELDS) {             // Camera#lens_func again: the same bits (lv_ray)
+          const CameraDev& cam = *p.cam;
+          cur.ray = lens_ray(cam, lens_target(cam, x, y), x, y, sample, p.seed);
+        }
       } else {                                // the staged child at its queue slot (lv_ray)
         const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)(is >> 32) * RAY_DOUBLES);
+        if (RF != LV_RING_FIELDS) {
+          const double2 a = q[0], b = q[1], c = q[2];
+          cur.ray.o = v3(a.x, a.y, b.x);
+          cur.ray.d = v3(b.y, c.x, c.y);
+        }
         const double2 d = q[3], e = q[4], f = q[5];
         cur.att = v3(d.x, d.y, e.x);
         cur.path = __builtin_bit_cast(uint64_t, e.y);
@@ -847,9 +876,9 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS>
+template <int SPH, int BS, int RF>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
-  k_level_c_body<SPH, BS>(p, level);
+  k_level_c_body<SPH, BS, RF>(p, level);
   lv_level_done(p, level + 1);
 }
 
@@ -1527,6 +1556,15 @@ int read_level_stamps(unsigned long long* out, int reset) {
   return 0;
 }
 
+extern "C" int rtxdbg_read_walkstats(unsigned long long* out, int reset) {   // diagnostic builds (levels unit)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtx_walkstats), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtx_walkstats), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+
 extern "C" int rtxdbg_read_level_stamps(unsigned long long* out, int reset) {   // diagnostic builds: [8 levels][8]
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtx_stamps_lv), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
   if (reset) {
@@ -1571,13 +1609,18 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   size_t lds = lds_layout(q, SPH, BS);
   auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
   if (kind == 0 && q.lv_compact != 0) {        // hit compaction when the rings fit next to the walk's LDS
-    constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL;
-    const size_t ring = (lds + 15) & ~(size_t)15;
+    constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL || SPH == SPH_BVH_MIX;
+    const size_t ring = (lds + 15) & ~(size_t)15, budget = BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
     const size_t need = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES;
-    if (need <= (BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES)) {
+    const size_t need_small = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES_SMALL;
+    if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
-      kern = k_level_c<SPH, BS>;
+      kern = k_level_c<SPH, BS, LV_RING_FIELDS>;
+    } else if (BVH && need_small <= budget) {  // the compact ring (C4-sized hierarchies)
+      q.lds_ring = (int32_t)ring;
+      lds = need_small;
+      kern = k_level_c<SPH, BS, LV_RING_FIELDS_SMALL>;
     }
   }
   if (lds > 64 * 1024)
@@ -1599,7 +1642,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
 template <int SPH>
 static hipError_t launch_level(const KParams& p, int kind, int level, long cap_items, hipStream_t s,
                                KernelEvents* kev) {
-  constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL;
+  constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL || SPH == SPH_BVH_MIX;
   constexpr int FBS = RTX_LV_FUSED_BS ? RTX_LV_FUSED_BS : (BVH ? BS_BVH : BS_LIN);
   if (kind == 0) return launch_level_bs<SPH, FBS>(p, kind, level, cap_items, s, kev);
   if (BVH) {
@@ -1618,6 +1661,7 @@ static hipError_t launch_level_mode(const KParams& p, int mode, int kind, int le
     case SPH_LIN_SCALAR: return launch_level<SPH_LIN_SCALAR>(p, kind, level, cap, s, kev);
     case SPH_BVH_LDS: return launch_level<SPH_BVH_LDS>(p, kind, level, cap, s, kev);
     case SPH_BVH_GLOBAL: return launch_level<SPH_BVH_GLOBAL>(p, kind, level, cap, s, kev);
+    case SPH_BVH_MIX: return launch_level<SPH_BVH_MIX>(p, kind, level, cap, s, kev);
   }
   return hipErrorInvalidValue;
 }

@@ -253,7 +253,7 @@ def test_chunk_schedule_changes_no_bit(gpu, static):
 def test_compaction_bit_identical(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=3)
-    for compact in (0, 1):
+    for compact in (0, 1, 2):                   # 2: the compact ring (the ray re-derived in the second half)
         r = _renderer(sd, cd, 1, lv_compact=compact)
         assert _same(r.render(seed=3), lanes), compact
         st = r.level_stats()
@@ -269,10 +269,11 @@ def test_compaction_bit_identical(gpu, world, camera, ov):
 def test_compaction_batches_overflow_schedule(gpu, opts):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
     lanes = _renderer(sd, cd, 0).render(seed=5)
-    r = _renderer(sd, cd, 1, lv_compact=1, **opts)
-    assert _same(r.render(seed=5), lanes)
-    if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
-        assert r.level_stats()["redo"] > 0
+    for compact in (1, 2):
+        r = _renderer(sd, cd, 1, lv_compact=compact, **opts)
+        assert _same(r.render(seed=5), lanes), compact
+        if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
+            assert r.level_stats()["redo"] > 0
 
 
 def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
@@ -288,16 +289,22 @@ def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
     p.write_text(src)
     sd, cd = config.load_scene(str(p), os.path.join(SCENES, "c1_camera.yml"), camera_overrides=dict(width=24, height=14))
     msgs = []
-    for engine, opts in ((0, {}), (1, dict(lv_compact=1)), (1, dict(lv_compact=0))):
+    for engine, opts in ((0, {}), (1, dict(lv_compact=1)), (1, dict(lv_compact=0)), (1, dict(lv_compact=2))):
         with pytest.raises(RtxError) as e:
             _renderer(sd, cd, engine, **opts).render()
         msgs.append(str(e.value))
-    assert msgs[0] == msgs[1] == msgs[2]
+    assert len(set(msgs)) == 1, msgs
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import make_scenes
     make_scenes.ensure_c4()
     sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=64, height=36)
-    assert _same(_renderer(sd, cd, 1, lv_compact=1).render(seed=2), _renderer(sd, cd, 0).render(seed=2))
+    lanes = _renderer(sd, cd, 0).render(seed=2)
+    assert _same(_renderer(sd, cd, 1, lv_compact=1).render(seed=2), lanes)
+    # the hierarchy's nodes in LDS and its leaves read from global memory
+    # (sphere_src 2) leave room for the compact ring: k_level_c on C4
+    for src in (1, 2):
+        for compact in (0, 1, 2):
+            assert _same(_renderer(sd, cd, 1, sphere_src=src, lv_compact=compact).render(seed=2), lanes), (src, compact)
 
 
 def test_compaction_c2_full_frame(gpu):

@@ -26,11 +26,14 @@ out = torch.empty((cd.height, cd.width, 3), dtype=torch.float64, device="cuda")
 r.render_device(out.data_ptr()); r.sync()
 st = (ctypes.c_ulonglong * 16)()
 lv = (ctypes.c_ulonglong * 64)()
+ws = (ctypes.c_ulonglong * 8)()
 lib.rtxdbg_read_stamps(st, 1)
 lib.rtxdbg_read_level_stamps(lv, 1)
+lib.rtxdbg_read_walkstats(ws, 1)
 r.render_device(out.data_ptr()); r.sync()
 lib.rtxdbg_read_stamps(st, 1)
 lib.rtxdbg_read_level_stamps(lv, 1)
+lib.rtxdbg_read_walkstats(ws, 1)
 v = list(st)
 tot = sum(v[:6])
 names = ["A claim/load/lens/highlight", "B EXTEND walk", "C hit_info/normal/cos", "D SHADOW walks + lights",
@@ -54,3 +57,9 @@ for d in range(8):
     c = row[6]
     print("  level %d%s: chunks %8d  hit %5.1f  total %7.0f  A %6.0f B %6.0f C %6.0f D %6.0f E %6.0f F %6.0f" % (
         d, "+" if d == 7 else " ", c, row[7] / c, sum(row[:6]) / c, *[x / c for x in row[:6]]))
+
+w = list(ws)
+if w[0]:
+    for name, o in (("EXTEND", 0), ("SHADOW", 4)):
+        print("%s walks: inner-node loop %d wave iterations, %.1f lanes each; leaf visits %d wave iterations, %.1f lanes each"
+              % (name, w[o], w[o + 1] / max(1, w[o]), w[o + 2], w[o + 3] / max(1, w[o + 2])))
