@@ -277,7 +277,9 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
    keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
          2 always; every choice renders the same bits), "bvh_min" [32], "bvh_sah" (1 [default] binned-SAH hierarchy
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
-         staging, 1 scalar loads, 2 nodes in LDS and leaves global), "lds_stack" (ray-stack entries per lane kept in LDS,
+         staging, 1 scalar loads, 2 hierarchy nodes in LDS and leaf records from global memory (bounce-level
+         engine; the lanes engine stages all), -1 [default] auto: 0, or 2 for a hierarchy whose staging leaves no
+         LDS for the hit rings; every choice renders the same bits), "lds_stack" (ray-stack entries per lane kept in LDS,
          -1 = as many as fit), "force_stack" (per-lane ray-stack bucket), "postpone" (hierarchy walks
          still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never), "tile_order" (1 expensive
          8x8 tiles first by a primary-hit probe, 0 row-major, -1 [default] = 1 up to 512 spheres; the order
@@ -300,8 +302,7 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          many workgroups for the lanes-engine re-render of overflowed samples, launched after every batch and
          nearly always empty; 8 [default], 0 = every resident workgroup; same bits), "lv_fin_grid" (bounce levels:
          0 [default] one tree-reduction block per 8x8 tile, k > 0 k blocks per CU looping over the tiles; measured
-         neutral on C2), "sphere_src" also 2 (hierarchy nodes staged in LDS, leaf records read from global memory:
-         leaves room for the hit rings; bounce-level engine). */
+         neutral on C2). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

@@ -70,7 +70,7 @@ struct rtx_context {
   int64_t opt_bvh = 1;               // 0: ordered linear walk; 1: hierarchy from opt_bvh_min spheres; 2: always
   int64_t opt_bvh_sah = RTX_BVH_SAH;  // hierarchy splits: 1 binned SAH, 0 median (applies at the next upload)
   int64_t opt_bvh_min = 32;         // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
-  int64_t opt_sphere_src = 0;        // 0: LDS staging (measured faster), 1: scalar loads
+  int64_t opt_sphere_src = -1;       // 0: LDS staging (measured faster), 1: scalar loads, 2: nodes LDS + leaves global, -1 auto
   int64_t opt_postpone = -1;         // query_bvh postponing threshold in lanes (-1: auto by hierarchy size)
   int64_t opt_tile_order = -1;       // 1: expensive tiles first (k_tile_cost/k_tile_sort), 0: natural order, -1: auto
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
@@ -526,8 +526,8 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_kernel_events = value != 0;
     return RTX_OK;
   }
-  if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads; 2: hierarchy nodes in LDS, leaves global
-    if (value < 0 || value > 2) return fail(c, RTX_EINVAL, "sphere_src must be 0, 1 or 2");
+  if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads; 2: hierarchy nodes in LDS, leaves global; -1 auto
+    if (value < -1 || value > 2) return fail(c, RTX_EINVAL, "sphere_src must be -1, 0, 1 or 2");
     c->opt_sphere_src = value;
     return RTX_OK;
   }
@@ -805,8 +805,8 @@ static int required_stack(const rtx_context* c) {
 static int sph_mode(const rtx_context* c) {
   const bool bvh = c->opt_bvh == 2 || (c->opt_bvh == 1 && c->scene.n_sphere >= c->opt_bvh_min);
   if (bvh && c->scene.bvh_root != BVH_NONE)
-    return c->opt_sphere_src == 2 ? SPH_BVH_MIX : c->opt_sphere_src ? SPH_BVH_GLOBAL : SPH_BVH_LDS;
-  return c->opt_sphere_src ? SPH_LIN_SCALAR : SPH_LIN_LDS;
+    return c->opt_sphere_src == 2 ? SPH_BVH_MIX : c->opt_sphere_src == 1 ? SPH_BVH_GLOBAL : SPH_BVH_LDS;
+  return c->opt_sphere_src == 1 ? SPH_LIN_SCALAR : SPH_LIN_LDS;
 }
 
 // Global per-lane regions (ray-stack entries beyond LDS) for every lane a persistent launch can keep resident (512 per CU at
@@ -968,7 +968,13 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   KernelEvents kev{c->ev, 0, rtx_context::MAX_EV};
   if (c->opt_kernel_events && !c->ev[0])
     for (int k = 0; k < 2 * rtx_context::MAX_EV; k++) HIPCHK(c, hipEventCreate(&c->ev[k]));
-  const hipError_t e = launch_levels(p, sph_mode(c), maxs, std::max(1, c->cam.depth), batch_tiles, stream,
+  // sphere_src auto: C4-sized hierarchies keep their nodes in LDS and read
+  // their leaves from global memory, which leaves room for the hit rings
+  // (r05b: C4 410 -> 386 ms, same bits)
+  const int mode = c->opt_sphere_src == -1 ? levels_auto_mode(c->scene, sph_mode(c), (int)c->opt_lv_compact,
+                                                              (int)c->opt_lv_split)
+                                           : sph_mode(c);
+  const hipError_t e = launch_levels(p, mode, maxs, std::max(1, c->cam.depth), batch_tiles, stream,
                                      c->opt_kernel_events ? &kev : nullptr, parts > 1 ? &aux : nullptr);
   if (c->opt_kernel_events) c->n_ev = kev.n;
   const hipError_t f = hipFreeAsync(buf, stream);

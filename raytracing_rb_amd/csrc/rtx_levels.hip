@@ -1556,6 +1556,17 @@ int read_level_stamps(unsigned long long* out, int reset) {
   return 0;
 }
 
+int levels_auto_mode(const SceneDev& S, int mode, int compact, int split) {
+  if (mode != SPH_BVH_LDS || compact == 0 || split) return mode;
+  const size_t waves = BS_BVH / 64;
+  const size_t walk = (size_t)S.bvh_stack * BS_BVH * 4 + (size_t)COVER_K * BS_BVH * 12 + 64;
+  const size_t nodes = (size_t)S.n_nodes * sizeof(Bvh4Node), leaves = (size_t)S.n_slots * 16;
+  if (nodes + leaves + walk + waves * LV_RING_WAVE_BYTES <= LDS_TOTAL_BYTES) return mode;   // LDS + full ring
+  if (nodes + leaves + walk + waves * LV_RING_WAVE_BYTES_SMALL <= LDS_TOTAL_BYTES) return mode;   // + compact ring
+  if (nodes + walk + waves * LV_RING_WAVE_BYTES_SMALL <= LDS_TOTAL_BYTES) return SPH_BVH_MIX;
+  return mode;
+}
+
 extern "C" int rtxdbg_read_walkstats(unsigned long long* out, int reset) {   // diagnostic builds (levels unit)
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtx_walkstats), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
   if (reset) {

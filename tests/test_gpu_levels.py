@@ -277,8 +277,10 @@ def test_compaction_batches_overflow_schedule(gpu, opts):
 
 
 def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
-    """Raise sites keep their order through the ring; C4's hierarchy leaves no
-    LDS for the rings, so the option falls back to k_level (same bits)."""
+    """Raise sites keep their order through the ring (full and compact); C4's
+    staged hierarchy leaves no LDS for a ring: with sphere_src 0 the option
+    falls back to k_level, with the default (auto: nodes in LDS, leaves from
+    global memory) k_level_c runs with the compact ring; the same bits."""
     import sys
     from raytracing_rb_amd import config
     from raytracing_rb_amd.runtime import RtxError
@@ -300,6 +302,7 @@ def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
     sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=64, height=36)
     lanes = _renderer(sd, cd, 0).render(seed=2)
     assert _same(_renderer(sd, cd, 1, lv_compact=1).render(seed=2), lanes)
+    assert _same(_renderer(sd, cd, 1, lv_compact=1, sphere_src=0).render(seed=2), lanes)
     # the hierarchy's nodes in LDS and its leaves read from global memory
     # (sphere_src 2) leave room for the compact ring: k_level_c on C4
     for src in (1, 2):
