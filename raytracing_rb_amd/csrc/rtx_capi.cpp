@@ -527,7 +527,7 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     return RTX_OK;
   }
   if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads; 2: hierarchy nodes in LDS, leaves global; -1 auto
-    if (value < -1 || value > 2) return fail(c, RTX_EINVAL, "sphere_src must be -1, 0, 1 or 2");
+    if (value < -1 || value > 3) return fail(c, RTX_EINVAL, "sphere_src must be -1, 0, 1, 2 or 3");
     c->opt_sphere_src = value;
     return RTX_OK;
   }
@@ -805,7 +805,10 @@ static int required_stack(const rtx_context* c) {
 static int sph_mode(const rtx_context* c) {
   const bool bvh = c->opt_bvh == 2 || (c->opt_bvh == 1 && c->scene.n_sphere >= c->opt_bvh_min);
   if (bvh && c->scene.bvh_root != BVH_NONE)
-    return c->opt_sphere_src == 2 ? SPH_BVH_MIX : c->opt_sphere_src == 1 ? SPH_BVH_GLOBAL : SPH_BVH_LDS;
+    return c->opt_sphere_src == 3   ? SPH_BVH_LDSX
+           : c->opt_sphere_src == 2 ? SPH_BVH_MIX
+           : c->opt_sphere_src == 1 ? SPH_BVH_GLOBAL
+                                    : SPH_BVH_LDS;
   return c->opt_sphere_src == 1 ? SPH_LIN_SCALAR : SPH_LIN_LDS;
 }
 

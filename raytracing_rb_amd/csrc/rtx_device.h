@@ -445,8 +445,9 @@ __device__ __forceinline__ void push_cover(int* ci, double* cv, int& n, bool& ov
 // resume = true; meanwhile the wave's other lanes shade and start new
 // queries instead of idling.  Every lane visits the same nodes and leaves in
 // the same order either way, so the result is unchanged.
-template <int BS, bool PP, typename NP, typename LP>
-__device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4, int* stk, int* ci, double* cv,
+template <int BS, bool PP, typename NP, typename LP, typename XP, typename OP>
+__device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4, XP x64, OP xobj, int* stk, int* ci,
+                                          double* cv,
                                           bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
                                           V3& bhit, bool& bin, double& total, uint32_t& err, int& ref, int& sp,
                                           int& ncov, bool& ovf, bool resume, int postpone) {
@@ -604,12 +605,12 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
       while (keep) {
         const int u = __builtin_ctz(keep);
         keep &= keep - 1;
-        const Sphere64 sp64 = S.bvh_sph64[slot0 + u];
+        const Sphere64 sp64 = x64[slot0 + u];
         const V3 C = v3(sp64.c[0], sp64.c[1], sp64.c[2]);
         V3 hit;
         bool in;
         if (!sphere_exact(C, sp64.r, o, d, dn, r2, hit, in)) continue;
-        const int obj = S.bvh_obj[slot0 + u];
+        const int obj = xobj[slot0 + u];
         if (ext) {
           const double dist = vr(vsub(o, hit));      // Ray#distance
           if (lex_better(dist, obj, best, besti)) {
@@ -1051,15 +1052,22 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   const SceneDev& S = p.scene;
   size_t off = 0;
   if (mode == SPH_LIN_LDS) off = (size_t)(S.n_sphere + 4) * 16;
-  if (mode == SPH_BVH_LDS || mode == SPH_BVH_MIX) {
+  p.lds_x64 = p.lds_xobj = -1;
+  if (mode == SPH_BVH_LDS || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) {
     off = (size_t)S.n_nodes * sizeof(Bvh4Node);
     p.lds_leaf = (int32_t)off;
-    if (mode == SPH_BVH_LDS) off += (size_t)S.n_slots * 16;
+    if (mode != SPH_BVH_MIX) off += (size_t)S.n_slots * 16;
+    if (mode == SPH_BVH_LDSX) {
+      p.lds_x64 = (int32_t)off;
+      off += (size_t)S.n_slots * sizeof(Sphere64);
+      p.lds_xobj = (int32_t)off;
+      off += (size_t)S.n_slots * 4;
+    }
   }
   off = (off + 15) & ~(size_t)15;
   p.lds_stack = (int32_t)off;
   p.lds_cov = (int32_t)off;
-  if (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL || mode == SPH_BVH_MIX) {
+  if (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) {
     off += (size_t)S.bvh_stack * bs * 4;
     off = (off + 15) & ~(size_t)15;
     p.lds_cov = (int32_t)off;
@@ -1068,8 +1076,9 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   // the bottom of every lane's ray stack, as many entries as fit the budget
   off = (off + 15) & ~(size_t)15;
   p.lds_items = (int32_t)off;
-  const size_t budget =
-      (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL || mode == SPH_BVH_MIX) ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
+  const size_t budget = (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX)
+                            ? LDS_TOTAL_BYTES
+                            : LDS_LIN_BLOCK_BYTES;
   const size_t per = (size_t)ITEM_WORDS * 8 * bs;
   int slots = budget > off ? (int)((budget - off) / per) : 0;
   if (slots > p.stk_slots_max) slots = p.stk_slots_max;

@@ -279,11 +279,13 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
       query<COUNT>(S, sph_k, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, cnt);
     else if (SPH == SPH_BVH_LDS)
       q_resume = !query_bvh<BS, PP>(S, reinterpret_cast<const Bvh4Node*>(lds),
-                                reinterpret_cast<const float4*>(lds + p.lds_leaf), stk, cov_i, cov_v,
+                                reinterpret_cast<const float4*>(lds + p.lds_leaf), S.bvh_sph64, S.bvh_obj, stk,
+                                cov_i, cov_v,
                                 mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, q_ref, q_sp,
                                 q_ncov, q_ovf, q_resume, p.postpone);
     else
-      q_resume = !query_bvh<BS, PP>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), stk, cov_i, cov_v,
+      q_resume = !query_bvh<BS, PP>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, S.bvh_obj,
+                                stk, cov_i, cov_v,
                                 mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, q_ref, q_sp,
                                 q_ncov, q_ovf, q_resume, p.postpone);
     if (RTX_STAMPS) {
@@ -665,6 +667,11 @@ size_t bvh_lds_bytes(int n_nodes, int n_slots, int bvh_stack) {
 size_t bvh_lds_budget() { return LDS_TOTAL_BYTES; }
 
 int resolve_mode(const SceneDev& S, int mode) {
+  if (mode == SPH_BVH_LDSX) {                  // the staged hierarchy plus its exact records
+    const size_t need = bvh_lds_bytes(S.n_nodes, S.n_slots, S.bvh_stack) + (size_t)S.n_slots * (sizeof(Sphere64) + 4);
+    if (need <= LDS_TOTAL_BYTES) return mode;
+    mode = SPH_BVH_LDS;
+  }
   if (mode == SPH_BVH_MIX) {                   // nodes in LDS, leaves global: needs room for the nodes
     const size_t need = (size_t)S.n_nodes * sizeof(Bvh4Node) + (size_t)S.bvh_stack * BS_BVH * 4 +
                         (size_t)COVER_K * BS_BVH * 12 + 64;
@@ -760,7 +767,7 @@ hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t 
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   if (tiles == 0) return hipSuccess;
   KevScope kscope(count ? nullptr : kev);
-  if (mode == SPH_BVH_MIX) mode = SPH_BVH_LDS;   // (the lanes engine stages the whole hierarchy or none)
+  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) mode = SPH_BVH_LDS;   // (the lanes engine stages the whole hierarchy or none)
   if (count) mode = (mode == SPH_LIN_LDS || mode == SPH_BVH_LDS) ? SPH_LIN_LDS : SPH_LIN_SCALAR;
   mode = resolve_mode(p.scene, mode);
   hipError_t e = hipMemsetAsync(p.extra_count, 0, sizeof(int32_t), s);
@@ -792,7 +799,7 @@ hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t 
 // could not hold (SRC_LIST; k_level_begin already zeroed its work counter).
 hipError_t launch_redo(const KParams& q, int mode, int maxs, int n, hipStream_t s) {
   g_work_zeroed = true;
-  if (mode == SPH_BVH_MIX) mode = resolve_mode(q.scene, SPH_BVH_LDS);   // (see launch_render)
+  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) mode = resolve_mode(q.scene, SPH_BVH_LDS);   // (see launch_render)
   const hipError_t e = launch_src<SRC_LIST>(q, mode, false, maxs, n, s);
   g_work_zeroed = false;
   return e;
@@ -800,7 +807,7 @@ hipError_t launch_redo(const KParams& q, int mode, int maxs, int n, hipStream_t 
 
 hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s) {
   if (p.nrays == 0) return hipSuccess;
-  if (mode == SPH_BVH_MIX) mode = SPH_BVH_LDS;   // (see launch_render)
+  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) mode = SPH_BVH_LDS;   // (see launch_render)
   mode = resolve_mode(p.scene, mode);
   switch (maxs) {
     case 8: return launch_mode<false, 8, SRC_RAYS>(p, mode, p.nrays, s);

@@ -57,6 +57,7 @@ struct KParams {
   int32_t nrays;
   // dynamic LDS layout (bytes), filled by launch_render/launch_trace
   int32_t lds_leaf, lds_stack, lds_cov, lds_items;
+  int32_t lds_x64, lds_xobj;       // SPH_BVH_LDSX: staged Sphere64 records / object indices per leaf slot
   int32_t stk_slots;               // ray-stack entries per lane kept in LDS (set by the launcher)
   int32_t stk_slots_max;           // cap (option "lds_stack"; the stack bucket by default)
   double* stk_glb;                 // per-lane regions: MAXS * 12 doubles of ray stack
@@ -112,6 +113,9 @@ enum SphMode : int {
   SPH_BVH_MIX = 4,       // four-wide ball hierarchy, nodes staged in LDS, leaf records from global memory
                          // (bounce-level engine only: room for the hit rings of k_level_c; the lanes
                          // engine walks it as SPH_BVH_LDS)
+  SPH_BVH_LDSX = 5,      // as SPH_BVH_LDS, and the binary64 sphere records of the exact test with their
+                         // object indices staged too (bounce-level engine only, small hierarchies: no
+                         // global load inside the walk; the lanes engine walks it as SPH_BVH_LDS)
 };
 
 // HIP event pairs recorded on the launch stream around every ray-tree kernel

@@ -254,12 +254,18 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
   if (SPH == SPH_LIN_LDS) {
     for (int i = threadIdx.x; i < S.n_sphere + 4; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
     __syncthreads();
-  } else if (SPH == SPH_BVH_LDS || SPH == SPH_BVH_MIX) {
+  } else if (SPH == SPH_BVH_LDS || SPH == SPH_BVH_MIX || SPH == SPH_BVH_LDSX) {
     const int nn = S.n_nodes * (int)(sizeof(Bvh4Node) / 16);
     for (int i = threadIdx.x; i < nn; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.bvh)[i];
-    if (SPH == SPH_BVH_LDS) {
+    if (SPH != SPH_BVH_MIX) {
       float4* leaf = reinterpret_cast<float4*>(lds + p.lds_leaf);
       for (int i = threadIdx.x; i < S.n_slots; i += BS) leaf[i] = reinterpret_cast<const float4*>(S.bvh_sph32)[i];
+    }
+    if (SPH == SPH_BVH_LDSX) {
+      float4* x = reinterpret_cast<float4*>(lds + p.lds_x64);
+      for (int i = threadIdx.x; i < 2 * S.n_slots; i += BS) x[i] = reinterpret_cast<const float4*>(S.bvh_sph64)[i];
+      int32_t* o = reinterpret_cast<int32_t*>(lds + p.lds_xobj);
+      for (int i = threadIdx.x; i < S.n_slots; i += BS) o[i] = S.bvh_obj[i];
     }
     __syncthreads();
   }
@@ -283,15 +289,21 @@ __device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V
     bool q_ovf = false;
     if (SPH == SPH_BVH_LDS)
       query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
-                           stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp,
-                           q_ncov, q_ovf, false, 0);
+                           S.bvh_sph64, S.bvh_obj, stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total,
+                           err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
+    else if (SPH == SPH_BVH_LDSX)
+      query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
+                           reinterpret_cast<const Sphere64*>(lds + p.lds_x64),
+                           reinterpret_cast<const int32_t*>(lds + p.lds_xobj), stk, cov_i, cov_v, ext, o, d, L, rad,
+                           best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
     else if (SPH == SPH_BVH_MIX)
       query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(S.bvh_sph32),
-                           stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp,
-                           q_ncov, q_ovf, false, 0);
+                           S.bvh_sph64, S.bvh_obj, stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total,
+                           err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
     else
-      query_bvh<BS, false>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), stk, cov_i, cov_v, ext, o, d, L,
-                           rad, best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
+      query_bvh<BS, false>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, S.bvh_obj, stk, cov_i,
+                           cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf,
+                           false, 0);
   }
 }
 
@@ -1620,7 +1632,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   size_t lds = lds_layout(q, SPH, BS);
   auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
   if (kind == 0 && q.lv_compact != 0) {        // hit compaction when the rings fit next to the walk's LDS
-    constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL || SPH == SPH_BVH_MIX;
+    constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL || SPH == SPH_BVH_MIX || SPH == SPH_BVH_LDSX;
     const size_t ring = (lds + 15) & ~(size_t)15, budget = BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
     const size_t need = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES;
     const size_t need_small = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES_SMALL;
@@ -1653,7 +1665,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
 template <int SPH>
 static hipError_t launch_level(const KParams& p, int kind, int level, long cap_items, hipStream_t s,
                                KernelEvents* kev) {
-  constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL || SPH == SPH_BVH_MIX;
+  constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL || SPH == SPH_BVH_MIX || SPH == SPH_BVH_LDSX;
   constexpr int FBS = RTX_LV_FUSED_BS ? RTX_LV_FUSED_BS : (BVH ? BS_BVH : BS_LIN);
   if (kind == 0) return launch_level_bs<SPH, FBS>(p, kind, level, cap_items, s, kev);
   if (BVH) {
@@ -1673,6 +1685,7 @@ static hipError_t launch_level_mode(const KParams& p, int mode, int kind, int le
     case SPH_BVH_LDS: return launch_level<SPH_BVH_LDS>(p, kind, level, cap, s, kev);
     case SPH_BVH_GLOBAL: return launch_level<SPH_BVH_GLOBAL>(p, kind, level, cap, s, kev);
     case SPH_BVH_MIX: return launch_level<SPH_BVH_MIX>(p, kind, level, cap, s, kev);
+    case SPH_BVH_LDSX: return launch_level<SPH_BVH_LDSX>(p, kind, level, cap, s, kev);
   }
   return hipErrorInvalidValue;
 }

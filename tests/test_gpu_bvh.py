@@ -58,7 +58,7 @@ def c4_world():
 def test_bvh_bit_identical_to_ordered_walk(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lin = _render(sd, cd, BVH_OFF)
-    for src in (0, 1, 2):                       # hierarchy staged in LDS / scalar loads / nodes LDS + leaves global
+    for src in (0, 1, 2, 3):                    # staged in LDS / scalar loads / nodes LDS + leaves global / all + exact records
         assert _same_bits(_render(sd, cd, BVH_ALWAYS, src), lin), src
 
 
@@ -164,7 +164,7 @@ def test_bvh_edge_scenes_bit_identical(gpu, tmp_path):
     for name, world in _edge_scenes(tmp_path).items():
         sd, cd = _scene(world, "c2_camera.yml", width=160, height=90, pre_sample_times=2, max_sample_times=2)
         lin = _render(sd, cd, BVH_OFF)
-        for src in (0, 1, 2):
+        for src in (0, 1, 2, 3):
             assert _same_bits(_render(sd, cd, BVH_ALWAYS, src), lin), (name, src)
 
 

@@ -254,8 +254,9 @@ def test_compaction_bit_identical(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=3)
     for compact in (0, 1, 2):                   # 2: the compact ring (the ray re-derived in the second half)
-        r = _renderer(sd, cd, 1, lv_compact=compact)
-        assert _same(r.render(seed=3), lanes), compact
+        for src in (-1, 3):                     # 3: the exact sphere records staged in LDS too
+            r = _renderer(sd, cd, 1, lv_compact=compact, sphere_src=src)
+            assert _same(r.render(seed=3), lanes), (compact, src)
         st = r.level_stats()
         assert st["redo"] == 0 and st["dropped"] == 0
 
