@@ -279,7 +279,8 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
          staging, 1 scalar loads, 2 hierarchy nodes in LDS and leaf records from global memory, 3 the hierarchy and
          the binary64 records of the exact sphere test in LDS (2 and 3: bounce-level engine; the lanes engine
-         stages as 0), -1 [default] auto: 0, or 2 for a hierarchy whose staging leaves no LDS for the hit rings;
+         stages as 0), -1 [default] auto: 3 when that and the hit ring fit LDS, 2 for a hierarchy whose staging leaves
+         no LDS for a hit ring, else 0;
          every choice renders the same bits), "lds_stack" (ray-stack entries per lane kept in LDS,
          -1 = as many as fit), "force_stack" (per-lane ray-stack bucket), "postpone" (hierarchy walks
          still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never), "tile_order" (1 expensive

@@ -155,9 +155,10 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
                          KernelEvents* kev = nullptr, const LvAux* aux = nullptr);
 // Tree-record bytes for a scene with n_light lights (one leaf per fired light).
 int levels_rec_bytes(int n_light);
-// The bounce-level engine's sphere mode for sphere_src auto: SPH_BVH_LDS,
-// unless the staged hierarchy leaves no LDS for k_level_c's hit rings while
-// the hierarchy's nodes alone with the compact ring fit (C4): SPH_BVH_MIX.
+// The bounce-level engine's sphere mode for sphere_src auto: SPH_BVH_LDSX
+// when the hierarchy, its exact records and the full hit ring fit LDS (C2);
+// SPH_BVH_MIX when the staged hierarchy leaves no LDS for a hit ring while
+// the hierarchy's nodes alone with the compact ring fit (C4); else SPH_BVH_LDS.
 int levels_auto_mode(const SceneDev& S, int mode, int compact, int split);
 constexpr size_t RAY_BYTES = 96;                // staged ray record of the bounce-level engine
 constexpr size_t LV_HIT_BYTES = 64;             // split phases: hit-queue record

@@ -1573,6 +1573,9 @@ int levels_auto_mode(const SceneDev& S, int mode, int compact, int split) {
   const size_t waves = BS_BVH / 64;
   const size_t walk = (size_t)S.bvh_stack * BS_BVH * 4 + (size_t)COVER_K * BS_BVH * 12 + 64;
   const size_t nodes = (size_t)S.n_nodes * sizeof(Bvh4Node), leaves = (size_t)S.n_slots * 16;
+  const size_t exact = (size_t)S.n_slots * (sizeof(Sphere64) + 4);
+  // C2: the exact test's records staged too (r05d: 4.91-4.94 -> 4.85 ms, same bits)
+  if (nodes + leaves + exact + walk + waves * LV_RING_WAVE_BYTES <= LDS_TOTAL_BYTES) return SPH_BVH_LDSX;
   if (nodes + leaves + walk + waves * LV_RING_WAVE_BYTES <= LDS_TOTAL_BYTES) return mode;   // LDS + full ring
   if (nodes + leaves + walk + waves * LV_RING_WAVE_BYTES_SMALL <= LDS_TOTAL_BYTES) return mode;   // + compact ring
   if (nodes + walk + waves * LV_RING_WAVE_BYTES_SMALL <= LDS_TOTAL_BYTES) return SPH_BVH_MIX;
