@@ -527,9 +527,23 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
   }
 
   unsigned long long ws_ni = 0, ws_nl = 0, ws_li = 0, ws_ll = 0;   // RTX_WALKSTATS only
-  while (ref != BVH_NONE) {
+  // Speculative traversal (without postponing): a lane that reaches a leaf
+  // while other lanes of its wave still search holds it (`pend`) and keeps
+  // descending; the leaves are tested once every searching lane holds one.
+  // The visiting order changes, the result cannot (order independence, above).
+#ifndef RTX_SPEC
+#define RTX_SPEC 1             // speculative traversal (diagnostic builds may turn it off to compare)
+#endif
+  constexpr bool SPEC = !PP && RTX_SPEC;
+  int pend = BVH_NONE;
+  while (ref != BVH_NONE || pend != BVH_NONE) {
+    if (SPEC && ref < 0 && pend == BVH_NONE) {    // hold the leaf, search on
+      pend = ref;
+      ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
+    }
     // ---- inner nodes: slab-test the four child boxes, descend into the nearest
     while (ref >= 0 && ref != BVH_NONE) {
+      if (SPEC && !__ballot(pend == BVH_NONE)) break;   // every searching lane holds a leaf
       if (RTX_WALKSTATS) {
         const unsigned long long am = __ballot(1);
         ws_nl++;
@@ -567,16 +581,27 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
         if (key[k] < __builtin_inff()) stk[(sp++) * BS] = ch[k];
       if (key[0] < __builtin_inff()) ref = ch[0];
       else ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
+      if (SPEC && ref < 0 && pend == BVH_NONE) {  // reached a leaf: hold it, search on
+        pend = ref;
+        ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
+      }
     }
-    if (ref == BVH_NONE) break;
+    int lf;
+    if (SPEC) {
+      lf = pend;                                 // (a lane that found none yet waits here)
+      pend = BVH_NONE;
+    } else {
+      if (ref == BVH_NONE) break;
+      lf = ref;
+    }
     // ---- leaf: pre-test its spheres, exact test for those not ruled out
-    if (RTX_WALKSTATS) {
+    if (RTX_WALKSTATS && lf != BVH_NONE) {
       const unsigned long long am = __ballot(1);
       ws_ll++;
       if ((int)__lane_id() == __builtin_ctzll(am)) ws_li++;
     }
-    {
-      const int v = ~ref;
+    if (lf != BVH_NONE) {
+      const int v = ~lf;
       const int slot0 = (v >> 2) * BVH_LEAF;
       const int cnt = (v & 3) + 1;
       // the leaf's 4 records as {x0..x3}, {y0..y3}, {z0..z3}, {R^2 0..3}: the
@@ -626,8 +651,10 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
         }
       }
     }
-    ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
-    if (PP && __popcll(__ballot(ref != BVH_NONE)) < postpone && ref != BVH_NONE) return false;
+    if (!SPEC) {
+      ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
+      if (PP && __popcll(__ballot(ref != BVH_NONE)) < postpone && ref != BVH_NONE) return false;
+    }
   }
   if (RTX_WALKSTATS) {
     unsigned long long* w = rtx_walkstats + (ext ? 0 : 4);
