@@ -85,7 +85,6 @@ struct rtx_context {
   int64_t opt_lv_grid_div = 1;       // bounce levels: persistent level grids = resident workgroups / this
   int64_t opt_lv_fin_cap = 0;        // bounce levels: tree records per tile gathered into LDS by the reduction (0: off; measured slower)
   int64_t opt_lv_fin_grid = 0;       // bounce levels: tree reduction blocks per CU (grid-stride over tiles), 0 = one block per tile
-  int64_t opt_lv_fin_ilp = 0;        // bounce levels: tree walks in flight per thread in the reduction (0 / 2 / 4)
   int64_t opt_lv_redo_blocks = 8;    // bounce levels: workgroups of the overflow re-render launch (0: all resident)
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
@@ -419,7 +418,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact},
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
       {"lv_redo_blocks", c->opt_lv_redo_blocks}, {"lv_fin_cap", c->opt_lv_fin_cap},
-      {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_fin_ilp", c->opt_lv_fin_ilp}};
+      {"lv_fin_grid", c->opt_lv_fin_grid}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -496,11 +495,6 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_grid_div")) {       // bounce levels: level grids = resident workgroups / this
     if (value < 1 || value > 8) return fail(c, RTX_EINVAL, "lv_grid_div must be in [1, 8]");
     c->opt_lv_grid_div = value;
-    return RTX_OK;
-  }
-  if (!strcmp(key, "lv_fin_ilp")) {        // bounce levels: reduction tree walks in flight per thread (0, 2, 4)
-    if (value != 0 && value != 2 && value != 4) return fail(c, RTX_EINVAL, "lv_fin_ilp must be 0, 2 or 4");
-    c->opt_lv_fin_ilp = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_fin_grid")) {       // bounce levels: reduction blocks per CU (grid-stride), 0 = one per tile
@@ -935,7 +929,6 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_redo_blocks = (int32_t)c->opt_lv_redo_blocks;
   p.lv_fin_cap = (int32_t)c->opt_lv_fin_cap;   // the launcher turns it off when the rings do not fit LDS
   p.lv_fin_tiles = (int32_t)c->opt_lv_fin_grid;   // (blocks per CU here; the launcher sets the tile count)
-  p.lv_fin_ilp = (int32_t)c->opt_lv_fin_ilp;
   // Static chunks cost no atomics; dynamic claims balance rays of very
   // different cost.  Auto: all static while the sphere records fit one walk
   // workgroup's LDS with room to spare (C2: 5.35 vs 5.9 ms at 50 %), half

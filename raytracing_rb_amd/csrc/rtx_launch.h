@@ -101,8 +101,6 @@ struct KParams {
   int32_t lv_grid_div;             // level launches: persistent grid = resident workgroups / this (option lv_grid_div)
   int32_t lv_fin_cap;              // tree reduction: records of a tile gathered into LDS (0: walk from global memory)
   int32_t lv_fin_tiles;            // tree reduction pass 0: tiles of the batch (grid-stride loop when the grid is smaller)
-  int32_t lv_fin_ilp;              // tree reduction pass 0: tree walks in flight per thread (0: one, the plain kernel)
-  int32_t lv_fin_tpb;              // tree reduction with several walks per thread: tiles per block (launcher)
   int32_t lv_redo_blocks;          // the lanes-engine re-render of overflowed samples: at most this many workgroups (0: all resident)
 };
 

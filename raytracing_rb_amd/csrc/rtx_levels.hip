@@ -1192,10 +1192,9 @@ __device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, 
 // render_at's per-pixel stage of pass 0 (camera.rb:70-99) once a tile's
 // 64 x pre sample colours / raises are in LDS (scol, serr): 64 threads, one
 // per pixel of the tile.
-__device__ __forceinline__ void lv_tile_pixels(const KParams& p, const double* scol, const uint32_t* serr, int slot,
-                                               int l = -1) {
+__device__ __forceinline__ void lv_tile_pixels(const KParams& p, const double* scol, const uint32_t* serr, int slot) {
   const int pre = p.pre;
-  if (l < 0) l = (int)threadIdx.x;
+  const int l = (int)threadIdx.x;
   if (l >= 64) return;
   const int tiles_x = (p.nx + 7) >> 3;
   const int tile = p.lv_t0 + slot * p.lv_tstride;
@@ -1292,151 +1291,6 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
       atomicAdd(&rtx_stamps[13], 1ull);
     }
   }
-}
-
-// The same reduction with K trees walked at once per thread (option
-// lv_fin_ilp = K; r05).  Each walk step is one dependent global load (the
-// next record is known only once the current one has arrived), and the plain
-// kernel already runs at the CU's 32-wave limit, so the reduction waits on
-// load latency.  Here a thread keeps K independent walks and advances them in
-// lock step: the K records of a step are requested together, then consumed.
-// A block of 256 threads takes T = K * 256 / (64 * pre) tiles (1..4); the
-// walk stack lives in registers (one pending child range per level below the
-// root; the stack index is the visited record's level).  Same walks, same
-// additions in the same order per tree: the same bits.
-template <int SD>
-struct LvWalk {
-  V3 sum;
-  uint32_t err, q;
-  int lev;
-  bool gt1, act;
-  uint32_t lo[SD], hi[SD];
-};
-template <int SD>
-__device__ __forceinline__ uint32_t lv_sget(const uint32_t (&a)[SD], int i) {
-  uint32_t v = 0;
-#pragma unroll
-  for (int k = 0; k < SD; k++) v = k == i ? a[k] : v;
-  return v;
-}
-template <int SD>
-__device__ __forceinline__ void lv_sset(uint32_t (&a)[SD], int i, uint32_t v) {
-#pragma unroll
-  for (int k = 0; k < SD; k++) a[k] = k == i ? v : a[k];
-}
-
-template <int SD, int K>
-__global__ __launch_bounds__(256) void k_tree_finalize_ilp(KParams p, int nlev) {
-  __shared__ uint32_t base[LV_MAXL + 1];
-  extern __shared__ uint32_t lds_fin[];
-  uint32_t* pex = lds_fin;
-  lv_layout(p, nlev, base, pex);
-  const int pre = p.pre, n_items = 64 * pre;
-  const int T = p.lv_fin_tpb;
-  double* scol = reinterpret_cast<double*>(lds_fin + ((nlev * 64 + 1) & ~1));   // T * n_items colours
-  uint32_t* serr = reinterpret_cast<uint32_t*>(scol + (size_t)T * n_items * 3);
-  const int tile0 = blockIdx.x * T;
-  const int ntile = min(T, p.lv_fin_tiles - tile0);
-  const int total = ntile * n_items;
-  const uint32_t log2cap = (uint32_t)p.lv_slice_log2, smask = (1u << log2cap) - 1u;
-  const size_t rb = (size_t)p.lv_rec_bytes;
-  for (int g = (int)threadIdx.x; g < total; g += 256 * K) {
-    LvWalk<SD> w[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const int li = g + k * 256;               // block-local item: tile (li / n_items), sample li % n_items
-      w[k].act = false;
-      w[k].lev = 0;                             // (an idle walk's record address stays in range)
-      w[k].q = 0;
-      if (li >= total) continue;
-      const int item = tile0 * n_items + li;
-      if (!decode_item(p, item).valid) continue;
-      const int r = p.lv_redo_of[item];
-      if (r >= 0) {                             // re-rendered whole by the lanes engine
-        const double* q = p.lv_redo_smp + (size_t)r * 4;
-        scol[3 * li] = q[0];
-        scol[3 * li + 1] = q[1];
-        scol[3 * li + 2] = q[2];
-        serr[li] = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
-        continue;
-      }
-      w[k].act = true;
-      w[k].q = (uint32_t)item;
-      w[k].lev = 0;
-      w[k].err = 0;
-      w[k].gt1 = false;
-      w[k].sum = v3(0.0, 0.0, 0.0);
-    }
-    uint32_t pf = 0;
-    while (true) {
-      bool any = false;
-#pragma unroll
-      for (int k = 0; k < K; k++) any = any || w[k].act;
-      if (!any) break;
-      // the K records of this step, requested together
-      uint2 H[K];
-      double2 A[K];
-      double B[K];
-      const char* R[K];
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        R[k] = p.lv_rec + (size_t)(base[w[k].act ? w[k].lev : 0] + w[k].q) * rb;
-        if (w[k].act) {
-          H[k] = *reinterpret_cast<const uint2*>(R[k]);
-          A[k] = *reinterpret_cast<const double2*>(R[k] + 8);
-          B[k] = *reinterpret_cast<const double*>(R[k] + 24);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        if (!w[k].act) continue;
-        LvWalk<SD>& W = w[k];
-        const uint2 hdr = H[k];
-        if (!W.err) W.err = hdr.x & 0xffu;
-        const int nleaf = (int)(hdr.x >> 8 & 0xffu);
-        if (nleaf > 0) {                        // rt_reduce (ray_tracer.rb:292-298), in emission order
-          W.sum = vadd(W.sum, v3(A[k].x, A[k].y, B[k]));
-          if (!(W.sum.x <= 1 && W.sum.y <= 1 && W.sum.z <= 1)) W.gt1 = true;
-          const double* lf = reinterpret_cast<const double*>(R[k] + 8);
-          for (int j = 1; j < nleaf; j++) {
-            W.sum = vadd(W.sum, v3(lf[3 * j], lf[3 * j + 1], lf[3 * j + 2]));
-            if (!(W.sum.x <= 1 && W.sum.y <= 1 && W.sum.z <= 1)) W.gt1 = true;
-          }
-        }
-        int sp = W.lev;                         // pending ranges: one per level 1..lev
-        const uint32_t nch = (uint32_t)__popc(hdr.x >> 16);
-        if (nch && W.lev + 1 < nlev && sp < SD) {
-          const uint32_t c0 = pex[(W.lev + 1) * 64 + (hdr.y >> log2cap)] + (hdr.y & smask);
-          lv_sset<SD>(W.lo, sp, c0);
-          lv_sset<SD>(W.hi, sp, c0 + nch);
-          sp++;
-          const char* r0 = p.lv_rec + (size_t)(base[W.lev + 1] + c0) * rb;   // the children, fetched early
-          pf += *reinterpret_cast<const uint32_t*>(r0) + *reinterpret_cast<const uint32_t*>(r0 + (nch - 1) * rb);
-        }
-        // next: the last unvisited child of the deepest pending range (LIFO pop)
-        while (sp > 0 && lv_sget<SD>(W.hi, sp - 1) == lv_sget<SD>(W.lo, sp - 1)) sp--;
-        if (sp == 0) {
-          W.act = false;
-          const int li = g + k * 256;
-          scol[3 * li] = W.sum.x;
-          scol[3 * li + 1] = W.sum.y;
-          scol[3 * li + 2] = W.sum.z;
-          serr[li] = W.err ? W.err : (W.gt1 ? (uint32_t)ERR_COLOR_GT1 : 0u);
-        } else {
-          const uint32_t h = lv_sget<SD>(W.hi, sp - 1) - 1u;
-          lv_sset<SD>(W.hi, sp - 1, h);
-          W.q = h;
-          W.lev = sp;
-        }
-      }
-    }
-    asm volatile("" : : "v"(pf));             // the prefetches' values, consumed
-  }
-  __syncthreads();
-  const int t = (int)threadIdx.x;
-  if (t < ntile * 64)
-    lv_tile_pixels(p, scol + (size_t)(t >> 6) * n_items * 3, serr + (size_t)(t >> 6) * n_items, tile0 + (t >> 6),
-                   t & 63);
 }
 
 // The same reduction with the tile's trees gathered into LDS first (option
@@ -1891,25 +1745,7 @@ static hipError_t launch_finalize_g(KParams q, int nlev, int n, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int SD, int K>
-static hipError_t launch_finalize_ilp(KParams q, int nlev, int n, hipStream_t s) {
-  const int n_items = 64 * q.pre;
-  const int T = std::max(1, std::min(4, K * 256 / n_items));
-  q.lv_fin_tpb = T;
-  q.lv_fin_tiles = n;
-  const size_t lds = (size_t)((nlev * 64 + 1) & ~1) * 4 + (size_t)T * n_items * 28;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tree_finalize_ilp<SD, K>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((k_tree_finalize_ilp<SD, K>), dim3((unsigned)((n + T - 1) / T)), dim3(256), lds, s, q, nlev);
-  return hipGetLastError();
-}
-
 static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t s) {
-  if (q.lv_pass == 0 && q.lv_fin_ilp > 0 && q.lv_fin_cap <= 0 && nlev <= 9) {   // K walks per thread (nlev - 1 <= SD)
-    if (q.lv_fin_ilp >= 4) return nlev <= 5 ? launch_finalize_ilp<4, 4>(q, nlev, n, s) : launch_finalize_ilp<8, 4>(q, nlev, n, s);
-    return nlev <= 5 ? launch_finalize_ilp<4, 2>(q, nlev, n, s) : launch_finalize_ilp<8, 2>(q, nlev, n, s);
-  }
   if (q.lv_pass == 0 && q.lv_fin_cap > 0) {
     if (nlev <= 5) return launch_finalize_g<4>(q, nlev, n, s);
     if (nlev <= 9) return launch_finalize_g<8>(q, nlev, n, s);

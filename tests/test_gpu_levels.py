@@ -425,42 +425,6 @@ def test_gathered_reduction_with_overflow(gpu):
         r.close()
 
 
-# ---- tree reduction with several walks in flight per thread (option lv_fin_ilp)
-@pytest.mark.parametrize("world,camera,ov", [
-    ("c2_world.yml", "c2_camera.yml", dict(width=120, height=70)),                 # ragged tiles, T = K tiles/block
-    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, monte_carlo_diffusion_times=3, trace_depth=6)),
-    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, pre_sample_times=2, max_sample_times=5,
-                                             variant_threshold=0.0)),               # 2 lights: 2 leaves / record
-    ("mix_world.yml", "mix_camera.yml", dict(width=33, height=17, pre_sample_times=9, max_sample_times=9,
-                                             trace_depth=8)),                       # n_items > 256 K, 8 levels
-])
-def test_ilp_reduction_changes_no_bit(gpu, world, camera, ov):
-    """lv_fin_ilp: K = 2 / 4 tree walks advanced in lock step per thread, K x 256
-    trees per block, the walk stacks in registers: the same bits as the lanes
-    engine and the one-walk reduction."""
-    sd, cd = _scene(world, camera, **ov)
-    lanes = _renderer(sd, cd, 0).render(seed=4)
-    for k in (0, 2, 4):
-        r = _renderer(sd, cd, 1, lv_fin_ilp=k)
-        assert _same(r.render(seed=4), lanes), k
-        r.close()
-
-
-def test_ilp_reduction_with_overflow_and_full_frame(gpu):
-    """Re-rendered samples inside multi-walk blocks; C2 at full size."""
-    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
-    lanes = _renderer(sd, cd, 0).render(seed=6)
-    for k in (2, 4):
-        r = _renderer(sd, cd, 1, lv_fin_ilp=k, lv_stage_pct=5, lv_floor=0)
-        assert _same(r.render(seed=6), lanes), k
-        assert r.level_stats()["redo"] > 0
-        r.close()
-    sd, cd = _scene("c2_world.yml", "c2_camera.yml")
-    plain = _renderer(sd, cd, 1).render()
-    for k in (2, 4):
-        assert _same(_renderer(sd, cd, 1, lv_fin_ilp=k).render(), plain), k
-
-
 # ---- raises of children the cutoff drops (lv_finish builds only their normalize tests)
 HEADON_WORLD = """max_distance: 10000
 soft_shadow_exponent: 2
