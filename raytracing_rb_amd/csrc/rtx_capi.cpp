@@ -517,8 +517,8 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_lv_streams = value;
     return RTX_OK;
   }
-  if (!strcmp(key, "lv_compact")) {        // bounce levels: hit compaction in k_level, -1 auto, 2 compact ring, 3 binned
-    if (value < -1 || value > 3) return fail(c, RTX_EINVAL, "lv_compact must be -1, 0, 1, 2 or 3");
+  if (!strcmp(key, "lv_compact")) {        // bounce levels: hit compaction in k_level, -1 auto, 2 compact ring
+    if (value < -1 || value > 2) return fail(c, RTX_EINVAL, "lv_compact must be -1, 0, 1 or 2");
     c->opt_lv_compact = value;
     return RTX_OK;
   }
@@ -726,11 +726,6 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   HIPCHK(c, up(bb.slot64.data(), bb.slot64.size() * sizeof(Sphere64), &ptr)); S.bvh_sph64 = (const Sphere64*)ptr;
   HIPCHK(c, up(bb.slot_obj.data(), bb.slot_obj.size() * sizeof(int32_t), &ptr)); S.bvh_obj = (const int32_t*)ptr;
   HIPCHK(c, up(sph_obj.data(), sph_obj.size() * sizeof(int32_t), &ptr)); S.sph_obj = (const int32_t*)ptr;
-  std::vector<uint8_t> cls(mat.size());      // k_level_c's binned rings (lv_compact 3)
-  for (size_t i = 0; i < mat.size(); i++)
-    cls[i] = (mat[i].type == OBJ_SPHERE || mat[i].has_rr) &&
-             (mat[i].refr_att[0] != 0 || mat[i].refr_att[1] != 0 || mat[i].refr_att[2] != 0);
-  HIPCHK(c, up(cls.data(), cls.size(), &ptr));                           S.obj_class = (const uint8_t*)ptr;
   HIPCHK(c, up(lights.data(), lights.size() * sizeof(LightDev), &ptr));  S.light = (const LightDev*)ptr;
   HIPCHK(c, up(tex.data(), tex.size() * sizeof(TexDev), &ptr));          S.tex = (const TexDev*)ptr;
   HIPCHK(c, up(texels.data(), texels.size(), &ptr));                     S.texels = (const uint8_t*)ptr;

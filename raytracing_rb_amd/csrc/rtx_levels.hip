@@ -656,22 +656,10 @@ constexpr int LV_RING_FIELDS_SMALL = 5;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
 constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMALL * 8;
 
-// Binned rings (BIN, lv_compact 3; r05): the hits whose object may spawn a
-// refraction child (refractive attenuation != 0) and the others are parked
-// apart, as two stacks growing towards each other in one buffer of
-// LV_RING_BIN compact slots, and the second half pops 64 hits of one class:
-// the refraction's asin / cos and the refracted ray run on waves of glass
-// hits only.  Hits are independent, so the order they are shaded in changes
-// no bit.  Each stack is popped whenever it holds 64 (before the next chunk
-// is claimed), so each holds at most 63 + 64 and the two never meet.
-constexpr int LV_RING_BIN = 256;
-
-template <int SPH, int BS, int RF, bool BIN = false>
+template <int SPH, int BS, int RF>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
-  static_assert(!BIN || RF == LV_RING_FIELDS_SMALL, "binned rings are compact");
   constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
-  constexpr int RS = BIN ? LV_RING_BIN : LV_RING;      // slots per wave (field stride)
   const SceneDev& S = p.scene;
   extern __shared__ float4 lds_sph[];
   char* lds = reinterpret_cast<char*>(lds_sph);
@@ -684,9 +672,8 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
   const int slice = sched.wave_id() & (LV_SLICES - 1);
   const int lane = (int)__lane_id();
-  double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * ((size_t)RS * RF * 8));
+  double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * ((size_t)LV_RING * RF * 8));
   uint32_t head = 0, pend = 0;                // wave-uniform: first parked slot, parked hits
-  uint32_t n0 = 0, n1 = 0;                    // BIN: hits parked per class (stack 0 up from slot 0, 1 down from RS-1)
   bool got = true;
 
   unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
@@ -699,13 +686,9 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
   while (true) {
     uint32_t chunk = 0;
-    bool fresh = false;                         // a chunk claimed in this iteration
-    if (got && (!BIN || (n0 < 64 && n1 < 64))) {
-      got = sched.claim(in.chunks, chunk);      // (never again once exhausted)
-      fresh = got;
-    }
+    if (got) got = sched.claim(in.chunks, chunk);   // (never again once exhausted)
     if (RTX_STAMPS) t0 = stamp();
-    if (fresh) {
+    if (got) {
       if (RTX_STAMPS) nchunks++;
       // ---- first half: the ray, rt_map's cutoff, highlights, World#intersect
       uint32_t s, off, i;
@@ -770,61 +753,35 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         const uint32_t err = errA ? errA : errL;
         *reinterpret_cast<uint2*>(rec) = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8), 0u);
       }
-      // park the hits: slot head + pend + (rank among the wave's hits); BIN:
-      // the class's stack top + (rank among the wave's hits of that class)
+      // park the hits: slot head + pend + (rank among the wave's hits)
       const uint64_t hm = __ballot(shade);
-      const bool cls = BIN && shade && p.scene.obj_class[besti] != 0;
-      const uint64_t m1 = BIN ? __ballot(cls) : 0ull, m0 = hm & ~m1;
       if (shade) {
-        const uint64_t below = (1ull << lane) - 1ull;
-        const uint32_t k =
-            !BIN ? (head + pend + (uint32_t)__popcll(hm & below)) & (LV_RING - 1)
-                 : (cls ? (uint32_t)(RS - 1) - (n1 + (uint32_t)__popcll(m1 & below)) : n0 + (uint32_t)__popcll(m0 & below));
+        const uint32_t k = (head + pend + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))) & (LV_RING - 1);
         double* r = ring + k;
-        r[0 * RS] = hit.x;
-        r[1 * RS] = hit.y;
-        r[2 * RS] = hit.z;
+        r[0 * LV_RING] = hit.x;
+        r[1 * LV_RING] = hit.y;
+        r[2 * LV_RING] = hit.z;
         if (RF == LV_RING_FIELDS) {
-          r[3 * RS] = cur.ray.o.x;
-          r[4 * RS] = cur.ray.o.y;
-          r[5 * RS] = cur.ray.o.z;
-          r[6 * RS] = cur.ray.d.x;
-          r[7 * RS] = cur.ray.d.y;
-          r[8 * RS] = cur.ray.d.z;
+          r[3 * LV_RING] = cur.ray.o.x;
+          r[4 * LV_RING] = cur.ray.o.y;
+          r[5 * LV_RING] = cur.ray.o.z;
+          r[6 * LV_RING] = cur.ray.d.x;
+          r[7 * LV_RING] = cur.ray.d.y;
+          r[8 * LV_RING] = cur.ray.d.z;
         }
-        r[FI * RS] = __builtin_bit_cast(double, (uint64_t)i | (uint64_t)slot << 32);
-        r[(FI + 1) * RS] = __builtin_bit_cast(
+        r[FI * LV_RING] = __builtin_bit_cast(double, (uint64_t)i | (uint64_t)slot << 32);
+        r[(FI + 1) * LV_RING] = __builtin_bit_cast(
             double, (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) | (uint64_t)((errA & 0xffu) | (errL & 0xffu) << 8) << 32);
       }
-      if (BIN) {
-        n0 += (uint32_t)__popcll(m0);
-        n1 += (uint32_t)__popcll(m1);
-      } else {
-        pend += (uint32_t)__popcll(hm);
-      }
+      pend += (uint32_t)__popcll(hm);
       RTX_LV_STAMP(4)
     }
-    uint32_t take, first;                      // hits popped; BIN: the slot of lane 0's hit
-    if (!BIN) {
-      if (pend < 64 && (got || pend == 0)) {
-        if (!got) break;                      // no chunk left and nothing parked
-        continue;                             // not a full wave of hits yet
-      }
-      take = pend < 64 ? pend : 64u;
-      first = 0;
-    } else {
-      if (n0 < 64 && n1 < 64 && (got || (n0 == 0 && n1 == 0))) {
-        if (!got) break;
-        continue;
-      }
-      const bool c1 = n0 >= 64 ? false : (n1 >= 64 ? true : n0 == 0);   // a full stack, else flush 0 then 1
-      const uint32_t avail = c1 ? n1 : n0;
-      take = avail < 64 ? avail : 64u;
-      first = c1 ? (uint32_t)RS - n1 : n0 - take;   // the stack's top `take` slots
-      if (c1) n1 -= take;
-      else n0 -= take;
+    if (pend < 64 && (got || pend == 0)) {
+      if (!got) break;                        // no chunk left and nothing parked
+      continue;                               // not a full wave of hits yet
     }
     // ---- second half on up to 64 parked hits (64, except the final flush)
+    const uint32_t take = pend < 64 ? pend : 64u;
     const bool shade = (uint32_t)lane < take;
     Item cur;
     V3 hit = v3(0.0, 0.0, 0.0);
@@ -832,14 +789,14 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     int besti = 0, root = 0, x = 0, y = 0, sample = 0;
     bool hin = true;
     if (shade) {
-      const double* r = ring + (BIN ? first + (uint32_t)lane : (head + (uint32_t)lane) & (LV_RING - 1));
-      hit = v3(r[0 * RS], r[1 * RS], r[2 * RS]);
+      const double* r = ring + ((head + (uint32_t)lane) & (LV_RING - 1));
+      hit = v3(r[0 * LV_RING], r[1 * LV_RING], r[2 * LV_RING]);
       if (RF == LV_RING_FIELDS) {
-        cur.ray.o = v3(r[3 * RS], r[4 * RS], r[5 * RS]);
-        cur.ray.d = v3(r[6 * RS], r[7 * RS], r[8 * RS]);
+        cur.ray.o = v3(r[3 * LV_RING], r[4 * LV_RING], r[5 * LV_RING]);
+        cur.ray.d = v3(r[6 * LV_RING], r[7 * LV_RING], r[8 * LV_RING]);
       }
-      const uint64_t is = __builtin_bit_cast(uint64_t, r[FI * RS]);
-      const uint64_t be = __builtin_bit_cast(uint64_t, r[(FI + 1) * RS]);
+      const uint64_t is = __builtin_bit_cast(uint64_t, r[FI * LV_RING]);
+      const uint64_t be = __builtin_bit_cast(uint64_t, r[(FI + 1) * LV_RING]);
       i = (uint32_t)is;
       besti = (int)((uint32_t)be & 0x7fffffffu);
       hin = ((uint32_t)be >> 31) != 0;
@@ -874,10 +831,8 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         y = (int)(xy >> 32);
       }
     }
-    if (!BIN) {
-      head = (head + take) & (LV_RING - 1);
-      pend -= take;
-    }
+    head = (head + take) & (LV_RING - 1);
+    pend -= take;
     char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
     RTX_LV_STAMP(4)
     V3 delta = hit, nrm = hit, nn = hit;
@@ -933,9 +888,9 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS, int RF, bool BIN = false>
+template <int SPH, int BS, int RF>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
-  k_level_c_body<SPH, BS, RF, BIN>(p, level);
+  k_level_c_body<SPH, BS, RF>(p, level);
   lv_level_done(p, level + 1);
 }
 
@@ -1684,12 +1639,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
     const size_t ring = (lds + 15) & ~(size_t)15, budget = BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
     const size_t need = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES;
     const size_t need_small = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES_SMALL;
-    const size_t need_bin = ring + (size_t)(BS / 64) * LV_RING_BIN * LV_RING_FIELDS_SMALL * 8;
-    if (q.lv_compact == 3 && need_bin <= budget) {   // binned compact rings
-      q.lds_ring = (int32_t)ring;
-      lds = need_bin;
-      kern = k_level_c<SPH, BS, LV_RING_FIELDS_SMALL, true>;
-    } else if (need <= budget && q.lv_compact != 2) {   // the full ring
+    if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
       kern = k_level_c<SPH, BS, LV_RING_FIELDS>;

@@ -107,7 +107,6 @@ struct SceneDev {
   const Sphere64* bvh_sph64; // binary64 record per slot
   const int32_t* bvh_obj; // slot -> global (YAML) object index (-1 = padding)
   const int32_t* sph_obj; // sphere record -> global (YAML) object index
-  const uint8_t* obj_class; // per object: 1 = its hits may spawn refraction children (refractive attenuation != 0)
   const LightDev* light;
   const TexDev* tex;
   const uint8_t* texels;

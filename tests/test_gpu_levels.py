@@ -253,7 +253,7 @@ def test_chunk_schedule_changes_no_bit(gpu, static):
 def test_compaction_bit_identical(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=3)
-    for compact in (0, 1, 2, 3):                # 2: the compact ring (the ray re-derived), 3: binned by class
+    for compact in (0, 1, 2):                   # 2: the compact ring (the ray re-derived in the second half)
         for src in (-1, 3):                     # 3: the exact sphere records staged in LDS too
             r = _renderer(sd, cd, 1, lv_compact=compact, sphere_src=src)
             assert _same(r.render(seed=3), lanes), (compact, src)
@@ -270,7 +270,7 @@ def test_compaction_bit_identical(gpu, world, camera, ov):
 def test_compaction_batches_overflow_schedule(gpu, opts):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
     lanes = _renderer(sd, cd, 0).render(seed=5)
-    for compact in (1, 2, 3):
+    for compact in (1, 2):
         r = _renderer(sd, cd, 1, lv_compact=compact, **opts)
         assert _same(r.render(seed=5), lanes), compact
         if "lv_stage_pct" in opts or "lv_rec_pct" in opts:
@@ -292,8 +292,7 @@ def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
     p.write_text(src)
     sd, cd = config.load_scene(str(p), os.path.join(SCENES, "c1_camera.yml"), camera_overrides=dict(width=24, height=14))
     msgs = []
-    for engine, opts in ((0, {}), (1, dict(lv_compact=1)), (1, dict(lv_compact=0)), (1, dict(lv_compact=2)),
-                         (1, dict(lv_compact=3))):
+    for engine, opts in ((0, {}), (1, dict(lv_compact=1)), (1, dict(lv_compact=0)), (1, dict(lv_compact=2))):
         with pytest.raises(RtxError) as e:
             _renderer(sd, cd, engine, **opts).render()
         msgs.append(str(e.value))
@@ -315,10 +314,9 @@ def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
 def test_compaction_c2_full_frame(gpu):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml")
     plain = _renderer(sd, cd, 1, lv_compact=0).render()
-    for compact in (1, 3):
-        r = _renderer(sd, cd, 1, lv_compact=compact)
-        assert _same(r.render(), plain), compact
-        assert r.level_stats()["redo"] == 0
+    r = _renderer(sd, cd, 1, lv_compact=1)
+    assert _same(r.render(), plain)
+    assert r.level_stats()["redo"] == 0
 
 
 # ---- two halves on two streams (option lv_streams = 2, the default)
