@@ -105,4 +105,19 @@ def hw_fp64(pm, kernel_ms_per_frame):
             "active_lanes": round(lanes, 2), "active_lanes_from": how,
             "valu_wave_instrs_per_frame": pf.get("SQ_INSTS_VALU"),
             "f64_share_of_valu": round(sum(pf[k] for k in F64_FLOP) / pf["SQ_INSTS_VALU"], 4)
-            if pf.get("SQ_INSTS_VALU") else None}
+            if pf.get("SQ_INSTS_VALU") else None,
+            "valu_busy": valu_busy(pm)}
+
+
+def valu_busy(pm):
+    """rocprofv3's VALUBusy for the dominant kernel (profiles/gfx950_counters.txt:
+    100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE): the share of the
+    CUs' active cycles in which the vector ALU issues.  The issue-rate view of
+    the same kernel beside the FP64 FLOP rate (an FP64 FMA, an FP32 compare
+    and an integer add each occupy an issue slot)."""
+    pf = pm.get("per_frame") or {}
+    cus = pm.get("cu_num") or 256
+    if not pf.get("GRBM_GUI_ACTIVE") or not pf.get("SQ_ACTIVE_INST_VALU"):
+        return None
+    return {"percent": round(100.0 * pf["SQ_ACTIVE_INST_VALU"] / cus / pf["GRBM_GUI_ACTIVE"], 2),
+            "from": "100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE (rocprofv3 VALUBusy), per frame"}

@@ -45,7 +45,7 @@ pmc() {
   (timeout -k 5 -s KILL 60 rocprofv3 -L > $OUT/rocprof_counters.txt 2>&1 || true) && \
   pmcpass a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY && \
   pmcpass b SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR && \
-  pmcpass c FETCH_SIZE && \
+  pmcpass c FETCH_SIZE GRBM_GUI_ACTIVE && \
   pmcpass d WRITE_SIZE && \
   pmcpass f SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY && \
   { if grep -q "SQ_INST_CYCLES_VALU" $OUT/rocprof_counters.txt; then pmcpass e SQ_INST_CYCLES_VALU SQ_INSTS_VALU; else true; fi; } && \

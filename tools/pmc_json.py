@@ -42,7 +42,10 @@ def dispatch_values(d, kernel, seen=None):
                 seen.add(short.split("::")[-1])
             key = int(r["Dispatch_Id"])
             per.setdefault(r["Counter_Name"], {}).setdefault(key, 0.0)
-            per[r["Counter_Name"]][key] += float(r["Counter_Value"])
+            if r["Counter_Name"].startswith("GRBM_"):   # per-instance copies of one clock: max, as VALUBusy's reduce
+                per[r["Counter_Name"]][key] = max(per[r["Counter_Name"]][key], float(r["Counter_Value"]))
+            else:
+                per[r["Counter_Name"]][key] += float(r["Counter_Value"])
     return {c: [v[k] for k in sorted(v)] for c, v in per.items()}
 
 
