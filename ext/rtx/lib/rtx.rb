@@ -59,6 +59,7 @@ module RTX
   extern 'char* rtx_last_error(void*)'
   extern 'char* rtx_status_string(int)'
   extern 'int rtx_abi_version()'
+  extern 'char* rtx_build_id()'
   # ---- World.new / Camera.new
   extern 'int rtx_scene_upload(void*, void*)'
   extern 'int rtx_camera_set(void*, void*)'

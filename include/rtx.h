@@ -147,6 +147,10 @@ void        rtx_context_destroy(rtx_context* ctx);
 const char* rtx_last_error(const rtx_context* ctx);
 const char* rtx_status_string(rtx_status s);
 int32_t     rtx_abi_version(void);
+/* Identity of the build: the first 16 hex digits of the sha256 over the device
+ * sources, headers and compiler flags it was built from (the host layer checks
+ * it against the tree before use; the PMC profiles carry the same value). */
+const char* rtx_build_id(void);
 
 /* ---- scene / camera (World.new, Camera.new) ----------------------------- */
 rtx_status rtx_scene_upload(rtx_context* ctx, const rtx_scene_desc* scene);

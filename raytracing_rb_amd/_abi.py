@@ -77,6 +77,7 @@ SIGNATURES = [
     ("rtx_last_error", C.c_char_p, [_P]),
     ("rtx_status_string", C.c_char_p, [_I]),
     ("rtx_abi_version", _I, []),
+    ("rtx_build_id", C.c_char_p, []),
     ("rtx_scene_upload", _I, [_P, C.POINTER(SceneDesc)]),
     ("rtx_camera_set", _I, [_P, C.POINTER(CameraDesc)]),
     ("rtx_render", _I, [_P, _I, _I, _I, _I, _U64, _DP, _SZ]),
@@ -142,6 +143,15 @@ def load_library(path=None):
         fn.argtypes = args
     if lib.rtx_abi_version() != 1:
         raise RtxLibraryMissing("librtx ABI version mismatch")
+    if p == os.path.join(_HERE, "librtx.so"):
+        # the in-tree library must be the build of the sources beside it: a
+        # stale binary would be tested and benchmarked in place of the code
+        from . import _build
+        built, tree = lib.rtx_build_id().decode(), _build.source_sha()
+        if built != tree:
+            raise RtxLibraryMissing(
+                "stale librtx.so: built from sources %s, the tree holds %s — rebuild with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`" % (built, tree))
     if path is None:
         _lib = lib
     return lib

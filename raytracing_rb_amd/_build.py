@@ -46,6 +46,18 @@ def build_cli(force=False, verbose=False):
     return CLI_OUT
 
 
+def source_sha():
+    """Identity of the kernel build: sha256 over the device sources, headers and
+    build flags (embedded in librtx.so as rtx_build_id, checked at load)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
 def stale():
     if not os.path.exists(OUT):
         return True
@@ -68,12 +80,16 @@ def build(force=False, verbose=False, out=None, defines=()):
     with open(tag, "w") as f:
         f.write(" ".join(FLAGS + dflags))
     newest_dep = max(os.path.getmtime(p) for p in HEADERS + [__file__])
+    sha = source_sha()
     for src in SOURCES:
         obj = os.path.join(odir, os.path.basename(src) + ".o")
         objs.append(obj)
-        if same and os.path.exists(obj) and os.path.getmtime(obj) > max(newest_dep, os.path.getmtime(src)):
+        ident = []
+        if src.endswith("rtx_capi.cpp"):          # the build identity, always current (a quick unit)
+            ident = ['-DRTX_SOURCE_SHA="%s"' % sha]
+        elif same and os.path.exists(obj) and os.path.getmtime(obj) > max(newest_dep, os.path.getmtime(src)):
             continue
-        cmd = [HIPCC] + FLAGS + dflags + ["-c", "-o", obj, src]
+        cmd = [HIPCC] + FLAGS + dflags + ident + ["-c", "-o", obj, src]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((subprocess.Popen(cmd), cmd))

@@ -324,6 +324,11 @@ extern "C" {
 
 int32_t rtx_abi_version(void) { return RTX_ABI_VERSION; }
 
+#ifndef RTX_SOURCE_SHA
+#define RTX_SOURCE_SHA "unknown"
+#endif
+const char* rtx_build_id(void) { return RTX_SOURCE_SHA; }
+
 const char* rtx_status_string(rtx_status s) {
   switch (s) {
     case RTX_OK: return "ok";

@@ -49,15 +49,10 @@ F64_FLOP = {"SQ_INSTS_VALU_FMA_F64": 2, "SQ_INSTS_VALU_ADD_F64": 1, "SQ_INSTS_VA
 
 
 def kernel_source_sha():
-    """Identity of the kernel build: sha256 over the device sources and build flags."""
-    import hashlib
-    h = hashlib.sha256()
+    """Identity of the kernel build: sha256 over the device sources and build flags
+    (the value librtx.so embeds, rtx_build_id)."""
     from . import _build
-    for f in _build.SOURCES + _build.HEADERS:
-        with open(f, "rb") as fh:
-            h.update(fh.read())
-    h.update(" ".join(_build.FLAGS).encode())
-    return h.hexdigest()[:16]
+    return _build.source_sha()
 
 
 def active_lanes(per_frame):

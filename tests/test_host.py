@@ -336,3 +336,11 @@ def test_bench_refuses_mismatched_world_size():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub", "--gpus", "2"],
                          capture_output=True, text=True, timeout=120, env=env)
     assert out.returncode == 2 and "refusing" in out.stderr
+
+
+def test_library_is_the_build_of_this_tree():
+    """librtx.so embeds the sha of the sources it was built from (rtx_build_id);
+    the loader refuses an in-tree library built from other sources."""
+    from raytracing_rb_amd import _abi, _build
+    lib = _abi.load_library()
+    assert lib.rtx_build_id().decode() == _build.source_sha()
