@@ -30,6 +30,9 @@
 // so it changes no bit of any result.
 #include "rtx_device.h"
 
+#include <mutex>
+#include <vector>
+
 namespace rtx {
 
 
@@ -687,6 +690,41 @@ int resolve_mode(const SceneDev& S, int mode) {
 static thread_local KernelEvents* g_kev = nullptr;   // set by launch_render for its launches
 static thread_local bool g_work_zeroed = false;      // launch_one: the work counter is already zero
 
+// Occupancy of a persistent launch, cached per (kernel, block size, LDS
+// bytes, device): CUs and resident blocks per CU, the kernel's dynamic-LDS
+// limit raised the first time.  Querying the runtime on every launch cost host
+// time per level launch, which small frames (one rank's share) feel.
+hipError_t launch_fit(const void* kern, int bs, size_t lds, int& cus, int& per_cu) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  struct Ent {
+    const void* k;
+    int bs;
+    size_t lds;
+    int dev, cus, per_cu;
+  };
+  static std::mutex mu;
+  static std::vector<Ent> cache;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (const Ent& c : cache)
+      if (c.k == kern && c.bs == bs && c.lds == lds && c.dev == dev) {
+        cus = c.cus;
+        per_cu = c.per_cu;
+        return hipSuccess;
+      }
+  }
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, bs, lds);
+  if (e != hipSuccess) return e;
+  if (per_cu < 1) per_cu = 1;
+  std::lock_guard<std::mutex> g(mu);
+  cache.push_back({kern, bs, lds, dev, cus, per_cu});
+  return hipSuccess;
+}
+
 // Persistent launch: as many workgroups as can be resident at once (the
 // occupancy API; an over-estimate only leaves blocks that start after the
 // pool is empty and exit at once), never more than the work needs.
@@ -695,15 +733,9 @@ static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
   const size_t lds = lds_layout(p, SPH, BS);
   auto kern = k_render<COUNT, MAXS, RTX_WPS, SPH, SRC, BS, PP>;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  int dev = 0, cus = 0, per_cu = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BS, lds);
+  int cus = 0, per_cu = 0;
+  hipError_t e = launch_fit(reinterpret_cast<const void*>(kern), BS, lds, cus, per_cu);
   if (e != hipSuccess) return e;
-  if (per_cu < 1) per_cu = 1;
   const long need = ((long)nwork + BS - 1) / BS;
   long blocks = std::min<long>(need, (long)cus * per_cu);
   blocks = std::min<long>(blocks, (long)p.stk_glb_lanes / BS);   // lanes with a global ray-stack region

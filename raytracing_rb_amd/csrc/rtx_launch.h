@@ -126,6 +126,10 @@ struct KernelEvents {
 };
 
 int stack_bucket(int need);
+// Persistent-launch occupancy (CUs, resident blocks per CU) of `kern`, cached
+// per (kernel, block size, dynamic LDS bytes, device); raises the kernel's
+// dynamic-LDS limit on first use.
+hipError_t launch_fit(const void* kern, int bs, size_t lds, int& cus, int& per_cu);
 // mode: SphMode; a linear mode whose records exceed the LDS budget falls back to
 // SPH_LIN_SCALAR, a BVH mode to SPH_BVH_GLOBAL.  Counting launches always walk
 // linearly (the counters are the reference's brute-force events).

@@ -1602,12 +1602,7 @@ extern "C" int rtxdbg_read_level_stamps(unsigned long long* out, int reset) {   
 
 // ----------------------------------------------------------------- bounce-level launchers
 static hipError_t cus_and_fit(const void* kern, int bs, size_t lds, int& cus, int& per_cu) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, bs, lds);
-  if (per_cu < 1) per_cu = 1;
-  return e;
+  return launch_fit(kern, bs, lds, cus, per_cu);   // cached (rtx_kernels.hip)
 }
 
 template <typename K>
@@ -1649,10 +1644,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
       kern = k_level_c<SPH, BS, LV_RING_FIELDS_SMALL>;
     }
   }
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  int cus = 0, per_cu = 0;
+  int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)
   const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(kern), BS, lds, cus, per_cu);
   if (e != hipSuccess) return e;
   const long grid = std::max<long>(1, (long)cus * per_cu / std::max(1, q.lv_grid_div));
