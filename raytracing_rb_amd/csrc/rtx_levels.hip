@@ -674,14 +674,6 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   const int lane = (int)__lane_id();
   double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * ((size_t)LV_RING * RF * 8));
   uint32_t head = 0, pend = 0;                // wave-uniform: first parked slot, parked hits
-  // Merged flush: once the launch's chunks are exhausted every wave has < 64
-  // hits parked; instead of one partly empty second half per wave, the
-  // workgroup's leftovers are numbered across its waves' rings (wave order,
-  // then ring order) and shaded in blocks of 64, block b by wave b mod waves.
-  constexpr int NW = BS / 64;
-  __shared__ uint32_t fl_head[NW], fl_pend[NW];
-  bool merged = false;
-  uint32_t mtotal = 0, mblk = 0;
   bool got = true;
 
   unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
@@ -784,36 +776,12 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       pend += (uint32_t)__popcll(hm);
       RTX_LV_STAMP(4)
     }
-    if (!merged && pend < 64) {
-      if (got) continue;                      // not a full wave of hits yet
-      // chunks exhausted: publish this wave's leftovers, then shade the
-      // workgroup's in full blocks (every wave of the block comes here once)
-      if (lane == 0) {
-        fl_head[threadIdx.x >> 6] = head;
-        fl_pend[threadIdx.x >> 6] = pend;
-      }
-      __syncthreads();
-      for (int v = 0; v < NW; v++) mtotal += fl_pend[v];
-      merged = true;
-      mblk = threadIdx.x >> 6;
+    if (pend < 64 && (got || pend == 0)) {
+      if (!got) break;                        // no chunk left and nothing parked
+      continue;                               // not a full wave of hits yet
     }
-    // ---- second half on up to 64 parked hits: 64 from this wave's ring, or
-    // a block of the workgroup's merged leftovers
-    uint32_t take;
-    const double* rp;                         // this lane's parked hit
-    if (!merged) {
-      take = 64u;
-      rp = ring + ((head + (uint32_t)lane) & (LV_RING - 1));
-    } else {
-      if (mblk * 64u >= mtotal) break;        // (uniform per wave)
-      const uint32_t g = mblk * 64u + (uint32_t)lane;
-      take = mtotal - mblk * 64u < 64u ? mtotal - mblk * 64u : 64u;
-      mblk += NW;
-      uint32_t v = 0, off = g;                // hit g of the merged order: wave v, its j-th leftover
-      while (v + 1 < (uint32_t)NW && off >= fl_pend[v]) off -= fl_pend[v++];
-      rp = reinterpret_cast<const double*>(lds + p.lds_ring + (size_t)v * ((size_t)LV_RING * RF * 8)) +
-           ((fl_head[v] + off) & (LV_RING - 1));
-    }
+    // ---- second half on up to 64 parked hits (64, except the final flush)
+    const uint32_t take = pend < 64 ? pend : 64u;
     const bool shade = (uint32_t)lane < take;
     Item cur;
     V3 hit = v3(0.0, 0.0, 0.0);
@@ -821,7 +789,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     int besti = 0, root = 0, x = 0, y = 0, sample = 0;
     bool hin = true;
     if (shade) {
-      const double* r = rp;
+      const double* r = ring + ((head + (uint32_t)lane) & (LV_RING - 1));
       hit = v3(r[0 * LV_RING], r[1 * LV_RING], r[2 * LV_RING]);
       if (RF == LV_RING_FIELDS) {
         cur.ray.o = v3(r[3 * LV_RING], r[4 * LV_RING], r[5 * LV_RING]);
@@ -863,10 +831,8 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         y = (int)(xy >> 32);
       }
     }
-    if (!merged) {
-      head = (head + take) & (LV_RING - 1);
-      pend -= take;
-    }
+    head = (head + take) & (LV_RING - 1);
+    pend -= take;
     char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
     RTX_LV_STAMP(4)
     V3 delta = hit, nrm = hit, nn = hit;
