@@ -240,6 +240,10 @@ def test_c4_full_size_vs_oracle_columns_and_strip_bvh_equals_linear(gpu, c4_worl
     assert (rms <= 1e-4).all(), rms
     assert np.abs(d).max() <= 1e-6, np.abs(d).max()
     assert exact >= 0.8, exact
+    from raytracing_rb_amd.runtime import quantize        # max abs u8 difference
+    qg = quantize(np.ascontiguousarray(fb[:, z["columns"], :]), png_gem_blend=False)[..., :3].astype(int)
+    qr = quantize(np.ascontiguousarray(z["frame"]), png_gem_blend=False)[..., :3].astype(int)
+    assert int(np.abs(qg - qr).max()) <= 1
     assert np.isfinite(fb).all() and (fb >= 0).all() and (fb <= 1).all()
     assert fb.mean() > 0.01
     lin = Renderer(sd, cd)

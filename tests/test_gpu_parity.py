@@ -106,6 +106,15 @@ def test_c2_full_size_vs_oracle_columns(gpu):
     fb = _renderer(sd, cd).render()
     _check(fb[:, z["columns"], :], z["frame"])
     assert np.isfinite(fb).all() and (fb >= 0).all() and (fb <= 1).all()
+    # SURVEY.md §8(d) also asks for the max abs u8 difference after
+    # array_to_color (camera.rb:153-156): quantized by librtx for both frames
+    from raytracing_rb_amd.runtime import quantize
+    qg = quantize(np.ascontiguousarray(fb[:, z["columns"], :]), png_gem_blend=False)[..., :3].astype(int)
+    qr = quantize(np.ascontiguousarray(z["frame"]), png_gem_blend=False)[..., :3].astype(int)
+    u8 = int(np.abs(qg - qr).max())
+    print("C2 full-size columns: max abs u8 difference %d, u8-identical pixels %.6f"
+          % (u8, np.mean(np.all(qg == qr, axis=-1))))
+    assert u8 <= 1, u8
 
 
 def test_sharded_tiles_reassemble_bit_exactly(gpu):
