@@ -109,10 +109,19 @@ def valu_busy(pm):
     100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE): the share of the
     CUs' active cycles in which the vector ALU issues.  The issue-rate view of
     the same kernel beside the FP64 FLOP rate (an FP64 FMA, an FP32 compare
-    and an integer add each occupy an issue slot)."""
+    and an integer add each occupy an issue slot).
+
+    rocprofv3 on gfx950 reports GRBM_GUI_ACTIVE as the sum over the 8 XCDs'
+    clocks (MI355X_MICROARCH.md, DVFS note: effective clock = GRBM_GUI_ACTIVE / 8
+    / wall time), and the counter_defs.yaml expression, written for one graphics
+    engine, divides by that sum: its figure is 8x low.  `percent` divides by one
+    XCD's clock; `rocprof_formula` keeps the literal expression's value."""
     pf = pm.get("per_frame") or {}
     cus = pm.get("cu_num") or 256
+    xcds = pm.get("xcd_num") or 8
     if not pf.get("GRBM_GUI_ACTIVE") or not pf.get("SQ_ACTIVE_INST_VALU"):
         return None
-    return {"percent": round(100.0 * pf["SQ_ACTIVE_INST_VALU"] / cus / pf["GRBM_GUI_ACTIVE"], 2),
-            "from": "100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE (rocprofv3 VALUBusy), per frame"}
+    lit = 100.0 * pf["SQ_ACTIVE_INST_VALU"] / cus / pf["GRBM_GUI_ACTIVE"]
+    return {"percent": round(lit * xcds, 2), "rocprof_formula": round(lit, 2),
+            "from": "100 * SQ_ACTIVE_INST_VALU / CU_NUM / (GRBM_GUI_ACTIVE / %d XCDs), per frame "
+                    "(rocprofv3 VALUBusy with GRBM_GUI_ACTIVE taken per XCD)" % xcds}

@@ -42,7 +42,7 @@ def dispatch_values(d, kernel, seen=None):
                 seen.add(short.split("::")[-1])
             key = int(r["Dispatch_Id"])
             per.setdefault(r["Counter_Name"], {}).setdefault(key, 0.0)
-            if r["Counter_Name"].startswith("GRBM_"):   # per-instance copies of one clock: max, as VALUBusy's reduce
+            if r["Counter_Name"].startswith("GRBM_"):   # one row per dispatch, already summed over the 8 XCDs by rocprofv3 (roofline.valu_busy)
                 per[r["Counter_Name"]][key] = max(per[r["Counter_Name"]][key], float(r["Counter_Value"]))
             else:
                 per[r["Counter_Name"]][key] += float(r["Counter_Value"])
