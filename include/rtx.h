@@ -277,7 +277,8 @@ rtx_status rtx_set_option(rtx_context* ctx, const char* key, int64_t value);
 rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
 /* read-only key: "engine_effective" (the engine the next render of the uploaded scene and camera runs:
          "engine", except that the bounce-level engine falls back to the lanes engine for trace_depth > 64,
-         monte_carlo_diffusion_times > 14 or more than 255 lights).
+         monte_carlo_diffusion_times > 14 or more than 255 lights), "lv_ray_bytes_effective" (80 or 96: the
+         staged ray record of the next bounce-level render).
    keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
          2 always; every choice renders the same bits), "bvh_min" [32], "bvh_sah" (1 [default] binned-SAH hierarchy
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
@@ -308,7 +309,10 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          many workgroups for the lanes-engine re-render of overflowed samples, launched after every batch and
          nearly always empty; 8 [default], 0 = every resident workgroup; same bits), "lv_fin_grid" (bounce levels:
          0 [default] one tree-reduction block per 8x8 tile, k > 0 k blocks per CU looping over the tiles; measured
-         neutral on C2). */
+         neutral on C2), "lv_ray_bytes" (bounce levels: staged ray record, 80 = origin, direction, attenuation,
+         {path, root} with the RNG key decoded from the root, 96 = with a 64-bit path and the key stored; 0 [default]
+         = 80 whenever (monte_carlo_diffusion_times + 3)^trace_depth <= 2^32, else 96; 80 for a camera whose paths
+         do not fit fails the render with RTX_EINVAL; same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

@@ -87,6 +87,7 @@ struct rtx_context {
   int64_t opt_lv_fin_grid = 0;       // bounce levels: tree reduction blocks per CU (grid-stride over tiles), 0 = one block per tile
   int64_t opt_lv_redo_blocks = 8;    // bounce levels: workgroups of the overflow re-render launch (0: all resident)
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
+  int64_t opt_lv_ray_bytes = 0;      // bounce levels: staged ray record, 0 auto (80 B when every path fits 32 bits), 80, 96
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
@@ -407,11 +408,16 @@ void rtx_context_destroy(rtx_context* c) {
 }
 
 static bool levels_engine(const rtx_context* c);
+static bool lv_paths32(const rtx_context* c);
 
 rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
   if (!c || !key || !value) return RTX_EINVAL;
   if (!strcmp(key, "engine_effective")) {   // read-only: the engine the next render of this camera runs
     *value = c->have_cam && c->have_scene ? (levels_engine(c) ? 1 : 0) : c->opt_engine;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_ray_bytes_effective")) {   // read-only: the staged ray record of the next level render
+    *value = c->opt_lv_ray_bytes == 96 || (c->have_cam && !lv_paths32(c)) ? 96 : 80;
     return RTX_OK;
   }
   const struct { const char* k; int64_t v; } tab[] = {
@@ -423,7 +429,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact},
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
       {"lv_redo_blocks", c->opt_lv_redo_blocks}, {"lv_fin_cap", c->opt_lv_fin_cap},
-      {"lv_fin_grid", c->opt_lv_fin_grid}};
+      {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -510,6 +516,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_fin_cap")) {        // bounce levels: LDS tree records per tile in the reduction, 0 = off
     if (value < 0 || value > 4096) return fail(c, RTX_EINVAL, "lv_fin_cap must be in [0, 4096]");
     c->opt_lv_fin_cap = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_ray_bytes")) {      // bounce levels: staged ray record size (0 auto)
+    if (value != 0 && value != 80 && value != 96) return fail(c, RTX_EINVAL, "lv_ray_bytes must be 0, 80 or 96");
+    c->opt_lv_ray_bytes = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_redo_blocks")) {    // bounce levels: overflow re-render grid cap, 0 = all resident
@@ -867,6 +878,19 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // The bounce-level engine can take this camera: its levels and child slots.
+// 80-B ray records when a ray's path id fits 32 bits at every level: path
+// < (pt + 3)^trace_depth (the path ids of rtx_device.h emit / lv_finish).
+// lv_ray_bytes 80 asked for a camera whose paths do not fit is refused, not
+// truncated.
+static bool lv_paths32(const rtx_context* c) {
+  uint64_t v = 1;
+  for (int l = 0; l < c->cam.depth; l++) {
+    v *= (uint64_t)c->cam.pt + 3;
+    if (v > (1ull << 32)) return false;
+  }
+  return true;
+}
+
 static bool levels_engine(const rtx_context* c) {
   return c->opt_engine == 1 && c->cam.depth <= LV_MAXL && c->cam.pt + 2 <= 16 && c->scene.n_light <= 255;
 }
@@ -894,6 +918,9 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const size_t scap = (size_t)LV_SLICES << slog2;
   if (scap > UINT32_MAX / 2 || lcap > UINT32_MAX / 2)
     return fail(c, RTX_EINVAL, "bounce-level buffers exceed 2^31 records: lower lv_batch");
+  const bool path32 = lv_paths32(c);
+  if (c->opt_lv_ray_bytes == 80 && !path32)
+    return fail(c, RTX_EINVAL, "lv_ray_bytes 80: this camera's ray paths need 64 bits ((pt + 3)^trace_depth > 2^32)");
   const int rec_bytes = levels_rec_bytes(c->scene.n_light);
   const size_t sz_ctl = al256(sizeof(LevelCtl)), sz_redo = al256(n0 * 4), sz_smp = al256(n0 * 32),
                sz_stage = al256(scap * RAY_BYTES), sz_rec = al256(lcap * (size_t)rec_bytes),
@@ -946,6 +973,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_hslice_log2 = hlog2;
   p.lv_lcap = (uint32_t)lcap;
   p.lv_rec_bytes = rec_bytes;
+  p.lv_ray_dbl = (c->opt_lv_ray_bytes == 96 || !path32) ? 12 : 10;
   p.lv_acc = c->d_lvstats;
   p.samples = nullptr;
   LvAux aux{};

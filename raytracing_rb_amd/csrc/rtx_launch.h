@@ -102,6 +102,7 @@ struct KParams {
   int32_t lv_fin_cap;              // tree reduction: records of a tile gathered into LDS (0: walk from global memory)
   int32_t lv_fin_tiles;            // tree reduction pass 0: tiles of the batch (grid-stride loop when the grid is smaller)
   int32_t lv_redo_blocks;          // the lanes-engine re-render of overflowed samples: at most this many workgroups (0: all resident)
+  int32_t lv_ray_dbl;              // staged ray record, doubles: 10 (80 B: path < 2^32, RNG key decoded from the root) or 12
 };
 
 // Where the sphere walk reads its records:
@@ -164,7 +165,7 @@ int levels_rec_bytes(int n_light);
 // SPH_BVH_MIX when the staged hierarchy leaves no LDS for a hit ring while
 // the hierarchy's nodes alone with the compact ring fit (C4); else SPH_BVH_LDS.
 int levels_auto_mode(const SceneDev& S, int mode, int compact, int split);
-constexpr size_t RAY_BYTES = 96;                // staged ray record of the bounce-level engine
+constexpr size_t RAY_BYTES = 96;                // staged ray record of the bounce-level engine (at most)
 constexpr size_t LV_HIT_BYTES = 64;             // split phases: hit-queue record
 constexpr int LV_SPLIT_MAX_LIGHTS = 16;         // split phases only up to this many lights (shadow results per hit)
 hipError_t launch_path_trace(KParams p, hipStream_t s);

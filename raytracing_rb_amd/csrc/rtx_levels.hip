@@ -46,7 +46,14 @@ namespace rtx {
 // Capacity.  Children beyond their slice or tree records beyond the record
 // arena are not written; their camera sample is listed (lv_redo_list) and
 // re-rendered whole by the lanes engine (SRC_LIST), exact either way.
-constexpr int RAY_DOUBLES = 12;          // staging ray record: o, d, att, path, root item, sample, x, y (96 B)
+// Staging ray record (p.lv_ray_dbl doubles per slot):
+//   12 (96 B): o, d, att, path, {root item, sample}, {x, y};
+//   10 (80 B): o, d, att, {path, root item} as two 32-bit words.  The host
+//   picks it when every path of the camera's trees fits 32 bits (path < (pt +
+//   3)^trace_depth <= 2^32); the RNG key (x, y, sample), needed only by the
+//   path-tracing children of a level >= 1 ray, is then decoded from the root.
+constexpr int RAY_DOUBLES = 12;
+constexpr int RAY_DOUBLES_SMALL = 10;
 constexpr int HIT_DOUBLES = 8;           // split hit record: hit, hit + delta, {ray, object | in}, {slot, raises}
 static_assert(RAY_DOUBLES * 8 == (int)RAY_BYTES && HIT_DOUBLES * 8 == (int)LV_HIT_BYTES, "record sizes");
 
@@ -71,16 +78,46 @@ __device__ __forceinline__ void lv_redo(const KParams& p, int root) {
 }
 
 // root: the level-0 item of the ray's tree; (x, y, sample): its RNG key.
-__device__ __forceinline__ void lv_store_ray(double* dst, const Ray& r, V3 att, uint64_t path, int root, int x, int y,
-                                             int sample) {
+__device__ __forceinline__ void lv_store_ray(const KParams& p, double* dst, const Ray& r, V3 att, uint64_t path,
+                                             int root, int x, int y, int sample) {
   double2* q = reinterpret_cast<double2*>(dst);
   q[0] = make_double2(r.o.x, r.o.y);
   q[1] = make_double2(r.o.z, r.d.x);
   q[2] = make_double2(r.d.y, r.d.z);
   q[3] = make_double2(att.x, att.y);
+  if (p.lv_ray_dbl == RAY_DOUBLES_SMALL) {
+    q[4] = make_double2(att.z, __builtin_bit_cast(double, (uint64_t)(uint32_t)path | (uint64_t)(uint32_t)root << 32));
+    return;
+  }
   q[4] = make_double2(att.z, __builtin_bit_cast(double, path));
   q[5] = make_double2(__builtin_bit_cast(double, (uint64_t)(uint32_t)root | (uint64_t)(uint32_t)sample << 32),
                       __builtin_bit_cast(double, (uint64_t)(uint32_t)x | (uint64_t)(uint32_t)y << 32));
+}
+
+// A staged ray's path, root item and RNG key from the record's last 16-B
+// words (e = {att.z, .}, f: the 96-B record's last word, unread for 80 B).
+__device__ __forceinline__ void lv_ray_tail(const KParams& p, const double2* q, double2 e, uint64_t& path, int& root,
+                                            int& x, int& y, int& sample) {
+  const uint64_t w = __builtin_bit_cast(uint64_t, e.y);
+  if (p.lv_ray_dbl == RAY_DOUBLES_SMALL) {
+    path = (uint32_t)w;
+    root = (int)(w >> 32);
+    x = y = sample = -1;                       // decoded when needed (lv_ray_key)
+    return;
+  }
+  const double2 f = q[5];
+  path = w;
+  const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
+  root = (int)(uint32_t)rs;
+  sample = (int)(rs >> 32);
+  x = (int)(uint32_t)xy;
+  y = (int)(xy >> 32);
+}
+
+// The root item of the staged ray at `q` (its record-arena overflow).
+__device__ __forceinline__ int lv_ray_root(const KParams& p, const double2* q) {
+  const uint64_t w = __builtin_bit_cast(uint64_t, p.lv_ray_dbl == RAY_DOUBLES_SMALL ? q[4].y : q[5].x);
+  return p.lv_ray_dbl == RAY_DOUBLES_SMALL ? (int)(w >> 32) : (int)(uint32_t)w;
 }
 
 __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
@@ -328,17 +365,22 @@ __device__ __forceinline__ void lv_ray(const KParams& p, int level, uint32_t idx
     }
     return;
   }
-  const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)idx * RAY_DOUBLES);
-  const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
+  const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)idx * p.lv_ray_dbl);
+  const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
   cur.ray.o = v3(a.x, a.y, b.x);
   cur.ray.d = v3(b.y, c.x, c.y);
   cur.att = v3(d.x, d.y, e.x);
-  cur.path = __builtin_bit_cast(uint64_t, e.y);
-  const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
-  root = (int)(uint32_t)rs;
-  sample = (int)(rs >> 32);
-  x = (int)(uint32_t)xy;
-  y = (int)(xy >> 32);
+  lv_ray_tail(p, q, e, cur.path, root, x, y, sample);
+}
+
+// The RNG key (x, y, sample) of a ray of tree `root` (lv_ray_tail leaves it
+// -1 for an 80-B record): decode_item of the root, as lv_ray does at level 0.
+__device__ __forceinline__ void lv_ray_key(const KParams& p, int root, int& x, int& y, int& sample) {
+  if (x >= 0) return;
+  const ItemPos ip = decode_item(p, root);
+  x = p.x0 + ip.px;
+  y = row_to_y(p, ip.row);
+  sample = ip.sample;
 }
 
 // rt_map's tail once the lit areas are known (ray_tracer.rb:80-158): which
@@ -449,8 +491,9 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
     double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
     uint32_t off = off0;
     auto put = [&](const Ray& r, V3 att, uint64_t path) {
-      if (off < cap) lv_store_ray(outs + (size_t)(((uint32_t)slice << log2cap) + off) * RAY_DOUBLES, r, att, path, root,
-                                  x, y, sample);
+      if (off < cap)
+        lv_store_ray(p, outs + (size_t)(((uint32_t)slice << log2cap) + off) * p.lv_ray_dbl, r, att, path, root, x, y,
+                     sample);
       else {
         lv_redo(p, root);
         atomicAdd(&p.lv_ctl->dropped, 1u);
@@ -469,6 +512,7 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
       const V3 up = vcross(nn, left);
       Ray r;
       r.o = vadd(hit, delta);
+      lv_ray_key(p, root, x, y, sample);
       for (int k = 0; k < pt; k++) {
         const double theta = rand01(p.seed, x, y, sample, cur.path, 2 * k) * PI / 2.0;
         const double phi = rand01(p.seed, x, y, sample, cur.path, 2 * k + 1) * PI * 2.0;
@@ -698,7 +742,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       // attenuation is read if a highlight fires, the root if the ray
       // overflows the record arena (the second half reloads the rest), so
       // the walk does not carry them.
-      const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * RAY_DOUBLES);
+      const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
       Item cur;
       int root = 0, x = 0, y = 0, sample = 0;
       bool alive = false;
@@ -715,7 +759,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         active = valid;
         alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // ray_tracer.rb:52
         if (active && base + i >= p.lv_lcap) {
-          lv_redo(p, level == 0 ? root : (int)(uint32_t)__builtin_bit_cast(uint64_t, qs[5].x));
+          lv_redo(p, level == 0 ? root : lv_ray_root(p, qs));
           active = alive = false;
         }
       }
@@ -815,20 +859,15 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
           cur.ray = lens_ray(cam, lens_target(cam, x, y), x, y, sample, p.seed);
         }
       } else {                                // the staged child at its queue slot (lv_ray)
-        const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)(is >> 32) * RAY_DOUBLES);
+        const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)(is >> 32) * p.lv_ray_dbl);
         if (RF != LV_RING_FIELDS) {
           const double2 a = q[0], b = q[1], c = q[2];
           cur.ray.o = v3(a.x, a.y, b.x);
           cur.ray.d = v3(b.y, c.x, c.y);
         }
-        const double2 d = q[3], e = q[4], f = q[5];
+        const double2 d = q[3], e = q[4];
         cur.att = v3(d.x, d.y, e.x);
-        cur.path = __builtin_bit_cast(uint64_t, e.y);
-        const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
-        root = (int)(uint32_t)rs;
-        sample = (int)(rs >> 32);
-        x = (int)(uint32_t)xy;
-        y = (int)(xy >> 32);
+        lv_ray_tail(p, q, e, cur.path, root, x, y, sample);
       }
     }
     head = (head + take) & (LV_RING - 1);

@@ -311,6 +311,38 @@ def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
             assert _same(_renderer(sd, cd, 1, sphere_src=src, lv_compact=compact).render(seed=2), lanes), (src, compact)
 
 
+# ---- staged ray records: 80 B (path and root in one word, the RNG key decoded from the root) or 96 B
+@pytest.mark.parametrize("world,camera,ov", [
+    ("c2_world.yml", "c2_camera.yml", dict(width=160, height=90)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=64, height=36)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=33, height=19, monte_carlo_diffusion_times=3, trace_depth=4)),
+    ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, pre_sample_times=2, max_sample_times=5,
+                                             variant_threshold=0.0)),
+])
+def test_ray_record_layouts_change_no_bit(gpu, world, camera, ov):
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=3)
+    for rb in (0, 80, 96):
+        for opts in (dict(), dict(lv_compact=2), dict(lv_compact=0), dict(lv_split=1), dict(lv_stage_pct=5, lv_floor=0)):
+            r = _renderer(sd, cd, 1, lv_ray_bytes=rb, **opts)
+            assert r.get_option("lv_ray_bytes_effective") == (96 if rb == 96 else 80)
+            assert _same(r.render(seed=3), lanes), (rb, opts)
+
+
+def test_ray_record_64_bit_paths(gpu):
+    """A camera whose ray path ids need more than 32 bits ((pt + 3)^trace_depth
+    > 2^32) keeps the 96-B record; asking for 80 B is refused, not truncated."""
+    from raytracing_rb_amd.runtime import RtxError
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=32, height=18, trace_depth=17)
+    lanes = _renderer(sd, cd, 0).render(seed=3)
+    r = _renderer(sd, cd, 1)
+    assert r.get_option("lv_ray_bytes_effective") == 96
+    assert _same(r.render(seed=3), lanes)
+    with pytest.raises(RtxError) as e:
+        _renderer(sd, cd, 1, lv_ray_bytes=80).render(seed=3)
+    assert e.value.kind == "invalid" and "64 bits" in str(e.value)
+
+
 def test_compaction_c2_full_frame(gpu):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml")
     plain = _renderer(sd, cd, 1, lv_compact=0).render()
