@@ -438,65 +438,63 @@ __device__ __forceinline__ void push_cover(int* ci, double* cv, int& n, bool& ov
   n++;
 }
 
-// Resumable: a lane whose walk is still running when fewer than `postpone`
-// lanes of its wave are is postponed (returns false) with its walk in
-// ref / sp (+ the LDS stack) / ncov / ovf (+ the LDS cover list) and best /
-// besti / bhit / bin, and continues where it stopped at the next call with
-// resume = true; meanwhile the wave's other lanes shade and start new
-// queries instead of idling.  Every lane visits the same nodes and leaves in
-// the same order either way, so the result is unchanged.
-template <int BS, bool PP, typename NP, typename LP, typename XP, typename OP>
-__device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4, XP x64, OP xobj, int* stk, int* ci,
-                                          double* cv,
-                                          bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
-                                          V3& bhit, bool& bin, double& total, uint32_t& err, int& ref, int& sp,
-                                          int& ncov, bool& ovf, bool resume, int postpone) {
-  const double r = vr(d);
-  const double r2 = r * r;                        // front.r2
-  V3 dn = d;
-  if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r); // front.normalize (same bits as the walk)
-  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
-  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
-  const float dd = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
-  const float Sx = fabsf(ox) + fabsf(oy) + fabsf(oz) + S.sph_scale;
-  const float ms2 = CULL_M * Sx * Sx;
-  const float mS = CULL_M * Sx;
-  const float kline = dd * ms2;
-  const float qneg = -CULL_M * Sx * sqrtf(dd);
-  // slab set-up: reciprocal direction and the dilated origin terms
-  const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
-  const float tiny = 1e-20f * l1;
-  const float ex = fabsf(dx) < tiny ? copysignf(tiny, dx) : dx;
-  const float ey = fabsf(dy) < tiny ? copysignf(tiny, dy) : dy;
-  const float ez = fabsf(dz) < tiny ? copysignf(tiny, dz) : dz;
-  const float ix = 1.0f / ex, iy = 1.0f / ey, iz = 1.0f / ez;
-  const float ax = (ox + mS) * ix, ay = (oy + mS) * iy, az = (oz + mS) * iz;   // lo - mS side
-  const float bx = (ox - mS) * ix, by = (oy - mS) * iy, bz = (oz - mS) * iz;   // hi + mS side
-  // packed operands of the slab test: {lo, hi} * {i, i} + {-a, -b} per axis
-  const F2 pix = {ix, ix}, piy = {iy, iy}, piz = {iz, iz};
-  const F2 pax = {-ax, -bx}, pay = {-ay, -by}, paz = {-az, -bz};
-  // A non-finite or zero ray makes no cull (comparisons would be unordered).
-  const bool fin = __builtin_isfinite(dd) && __builtin_isfinite(Sx) && l1 > 0.0f && __builtin_isfinite(ix) &&
-                   __builtin_isfinite(iy) && __builtin_isfinite(iz);
-  if (!fin) {
-    // no float32 cull is valid for this ray: the ordered linear walk (same result)
-    if (!ext) total = 1.0;
-    query<false>(S, cptr(S.sph32), ext, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
-    return true;
-  }
-  const float rf = (float)r;
-  // far bound on the ray parameter: EXTEND the current best hit, SHADOW the light
-  float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + mS / rf;
-  if (!resume) {
-    ncov = 0;
-    ovf = false;
-    ref = S.bvh_root;
-    sp = 0;
-  }
+// The float32 set-up of a walk's culls (§2.1 pre-test, §2.2 slab test), shared
+// by the hierarchy walk and the flat leaf scan.
+struct SlabRay {
+  float ox, oy, oz, dx, dy, dz, dd, Sx, ms2, mS, kline, qneg;
+  F2 pix, piy, piz, pax, pay, paz;   // packed operands of the slab test: {lo, hi} * {i, i} + {-a, -b} per axis
+  bool fin;                          // false: a non-finite or zero ray, no float32 cull is valid
+};
 
-  // planes and boxes first, in run order (their order does not matter either)
+__device__ __forceinline__ SlabRay slab_setup(const SceneDev& S, V3 o, V3 d) {
+  SlabRay s;
+  s.ox = (float)o.x, s.oy = (float)o.y, s.oz = (float)o.z;
+  s.dx = (float)d.x, s.dy = (float)d.y, s.dz = (float)d.z;
+  s.dd = __builtin_fmaf(s.dx, s.dx, __builtin_fmaf(s.dy, s.dy, s.dz * s.dz));
+  s.Sx = fabsf(s.ox) + fabsf(s.oy) + fabsf(s.oz) + S.sph_scale;
+  s.ms2 = CULL_M * s.Sx * s.Sx;
+  s.mS = CULL_M * s.Sx;
+  s.kline = s.dd * s.ms2;
+  s.qneg = -CULL_M * s.Sx * sqrtf(s.dd);
+  // slab set-up: reciprocal direction and the dilated origin terms
+  const float l1 = fabsf(s.dx) + fabsf(s.dy) + fabsf(s.dz);
+  const float tiny = 1e-20f * l1;
+  const float ex = fabsf(s.dx) < tiny ? copysignf(tiny, s.dx) : s.dx;
+  const float ey = fabsf(s.dy) < tiny ? copysignf(tiny, s.dy) : s.dy;
+  const float ez = fabsf(s.dz) < tiny ? copysignf(tiny, s.dz) : s.dz;
+  const float ix = 1.0f / ex, iy = 1.0f / ey, iz = 1.0f / ez;
+  const float ax = (s.ox + s.mS) * ix, ay = (s.oy + s.mS) * iy, az = (s.oz + s.mS) * iz;   // lo - mS side
+  const float bx = (s.ox - s.mS) * ix, by = (s.oy - s.mS) * iy, bz = (s.oz - s.mS) * iz;   // hi + mS side
+  s.pix = F2{ix, ix}, s.piy = F2{iy, iy}, s.piz = F2{iz, iz};
+  s.pax = F2{-ax, -bx}, s.pay = F2{-ay, -by}, s.paz = F2{-az, -bz};
+  s.fin = __builtin_isfinite(s.dd) && __builtin_isfinite(s.Sx) && l1 > 0.0f && __builtin_isfinite(ix) &&
+          __builtin_isfinite(iy) && __builtin_isfinite(iz);
+  return s;
+}
+
+// Entry distance of child box k of `node` if the ray may want it (the slab test
+// of the box dilated by m*S, §2.2, against the far bound thi), else +inf.
+template <typename NR>
+__device__ __forceinline__ float slab_key(const NR& node, int k, const SlabRay& s, float thi) {
+  // {t0, t1} per axis in one v_pk_fma_f32 each: the same fused FP32 operations as
+  // fmaf(lo, i, -a), fmaf(hi, i, -b)
+  const F2 tx = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&node.lh[0][k][0]), s.pix, s.pax);
+  const F2 ty = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&node.lh[1][k][0]), s.piy, s.pay);
+  const F2 tz = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&node.lh[2][k][0]), s.piz, s.paz);
+  const float t0x = tx.x, t1x = tx.y, t0y = ty.x, t1y = ty.y, t0z = tz.x, t1z = tz.y;
+  const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+  const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+  // empty slots hold a box at (3e38, 3e38, 3e38): never wanted by a finite ray
+  return (tn <= tf && tf >= 0.0f && tn <= thi) ? tn : __builtin_inff();
+}
+
+// Planes and boxes first, in run order (their order does not matter either).
+template <int BS>
+__device__ __forceinline__ void walk_planes_boxes(const SceneDev& S, bool ext, V3 o, V3 d, V3 L, double r,
+                                                  double& best, int& besti, V3& bhit, bool& bin, float& thi, int* ci,
+                                                  double* cv, int& ncov, bool& ovf) {
   const RTX_CONST Run* runs = cptr(S.runs);
-  const int n_runs = resume ? 0 : uni(S.n_runs);
+  const int n_runs = uni(S.n_runs);
   for (int ri = 0; ri < n_runs; ri++) {
     const int type = uni(runs[ri].type);
     if (type == OBJ_SPHERE) continue;
@@ -524,6 +522,115 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
         push_cover<BS>(ci, cv, ncov, ovf, obj0 + k, 1.0);
       }
     }
+  }
+}
+
+// One leaf (reference lf < 0): the §2.1 pre-test of its spheres, the exact
+// test for those not ruled out, then the nearest-hit update or the cover list.
+template <int BS, typename LP, typename XP, typename OP>
+__device__ __forceinline__ void walk_leaf(int lf, LP leaf4, XP x64, OP xobj, const SlabRay& s, bool ext, V3 o, V3 d,
+                                          V3 dn, double r, double r2, V3 L, double radius, double& best, int& besti,
+                                          V3& bhit, bool& bin, float& thi, uint32_t& err, int* ci, double* cv,
+                                          int& ncov, bool& ovf) {
+  const int v = ~lf;
+  const int slot0 = (v >> 2) * BVH_LEAF;
+  const int cnt = (v & 3) + 1;
+  // the leaf's 4 records as {x0..x3}, {y0..y3}, {z0..z3}, {R^2 0..3}: the
+  // pre-test of §2.1 on two spheres per packed FP32 instruction (the same
+  // operations as the per-sphere form in query())
+  const float4 cx = leaf4[slot0], cy = leaf4[slot0 + 1], cz = leaf4[slot0 + 2], cw = leaf4[slot0 + 3];
+  uint32_t keep = 0;
+  const F2 po = {s.ox, s.ox}, poy = {s.oy, s.oy}, poz = {s.oz, s.oz};
+  const F2 pdx = {s.dx, s.dx}, pdy = {s.dy, s.dy}, pdz = {s.dz, s.dz}, pdd = {s.dd, s.dd};
+  const F2 pkl = {s.kline, s.kline}, pms = {s.ms2, s.ms2};
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const F2 X = h ? F2{cx.z, cx.w} : F2{cx.x, cx.y}, Y = h ? F2{cy.z, cy.w} : F2{cy.x, cy.y};
+    const F2 Z = h ? F2{cz.z, cz.w} : F2{cz.x, cz.y}, Wr = h ? F2{cw.z, cw.w} : F2{cw.x, cw.y};
+    const F2 ocx = X - po, ocy = Y - poy, ocz = Z - poz;
+    const F2 sq = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
+    const F2 q = __builtin_elementwise_fma(ocx, pdx, __builtin_elementwise_fma(ocy, pdy, ocz * pdz));
+    const F2 l = __builtin_elementwise_fma(sq, pdd, -(q * q));
+    const F2 rr = __builtin_elementwise_fma(pdd, Wr, pkl);
+    const F2 wm = Wr + pms;
+    const bool m0 = l.x > rr.x || (q.x < s.qneg && sq.x > wm.x);   // misses the line, or wholly behind
+    const bool m1 = l.y > rr.y || (q.y < s.qneg && sq.y > wm.y);
+    keep |= (m0 ? 0u : 1u << (2 * h)) | (m1 ? 0u : 2u << (2 * h));
+  }
+  keep &= (1u << cnt) - 1u;
+  while (keep) {
+    const int u = __builtin_ctz(keep);
+    keep &= keep - 1;
+    const Sphere64 sp64 = x64[slot0 + u];
+    const V3 C = v3(sp64.c[0], sp64.c[1], sp64.c[2]);
+    V3 hit;
+    bool in;
+    if (!sphere_exact(C, sp64.r, o, d, dn, r2, hit, in)) continue;
+    const int obj = xobj[slot0 + u];
+    if (ext) {
+      const double dist = vr(vsub(o, hit));      // Ray#distance
+      if (lex_better(dist, obj, best, besti)) {
+        best = dist;
+        besti = obj;
+        bhit = hit;
+        bin = in;
+        thi = (float)(best / r * (1.0 + 1e-6));
+      }
+    } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
+      const double cov = penumbra(C, sp64.r, o, d, radius, err);
+      if (cov != 0.0) push_cover<BS>(ci, cv, ncov, ovf, obj, cov);
+    }
+  }
+}
+
+// World#lit_area's result from a shadow walk's ordered cover list.
+template <int BS>
+__device__ __forceinline__ void walk_covers(const SceneDev& S, V3 o, V3 d, V3 L, double radius, double& best,
+                                            int& besti, V3& bhit, bool& bin, double& total, uint32_t& err,
+                                            const double* cv, int ncov, bool ovf) {
+  total = 1.0;
+  if (ovf) {
+    // more than COVER_K non-zero covers: the ordered linear walk (rare)
+    query<false>(S, cptr(S.sph32), false, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
+  } else {
+    for (int k = 0; k < ncov; k++) total -= cv[k * BS];
+  }
+}
+
+// Resumable: a lane whose walk is still running when fewer than `postpone`
+// lanes of its wave are is postponed (returns false) with its walk in
+// ref / sp (+ the LDS stack) / ncov / ovf (+ the LDS cover list) and best /
+// besti / bhit / bin, and continues where it stopped at the next call with
+// resume = true; meanwhile the wave's other lanes shade and start new
+// queries instead of idling.  Every lane visits the same nodes and leaves in
+// the same order either way, so the result is unchanged.
+template <int BS, bool PP, typename NP, typename LP, typename XP, typename OP>
+__device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4, XP x64, OP xobj, int* stk, int* ci,
+                                          double* cv,
+                                          bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
+                                          V3& bhit, bool& bin, double& total, uint32_t& err, int& ref, int& sp,
+                                          int& ncov, bool& ovf, bool resume, int postpone) {
+  const double r = vr(d);
+  const double r2 = r * r;                        // front.r2
+  V3 dn = d;
+  if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r); // front.normalize (same bits as the walk)
+  const SlabRay s = slab_setup(S, o, d);
+  // A non-finite or zero ray makes no cull (comparisons would be unordered).
+  if (!s.fin) {
+    // no float32 cull is valid for this ray: the ordered linear walk (same result)
+    if (!ext) total = 1.0;
+    query<false>(S, cptr(S.sph32), ext, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
+    return true;
+  }
+  const float rf = (float)r;
+  // far bound on the ray parameter: EXTEND the current best hit, SHADOW the light
+  float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + s.mS / rf;
+  if (!resume) {
+    ncov = 0;
+    ovf = false;
+    ref = S.bvh_root;
+    sp = 0;
+    walk_planes_boxes<BS>(S, ext, o, d, L, r, best, besti, bhit, bin, thi, ci, cv, ncov, ovf);
   }
 
   unsigned long long ws_ni = 0, ws_nl = 0, ws_li = 0, ws_ll = 0;   // RTX_WALKSTATS only
@@ -554,16 +661,7 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         ch[k] = nodes[ref].child[k];
-        // {t0, t1} per axis in one v_pk_fma_f32 each: the same fused FP32 operations as
-        // fmaf(lo, i, -a), fmaf(hi, i, -b)
-        const F2 tx = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&nodes[ref].lh[0][k][0]), pix, pax);
-        const F2 ty = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&nodes[ref].lh[1][k][0]), piy, pay);
-        const F2 tz = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&nodes[ref].lh[2][k][0]), piz, paz);
-        const float t0x = tx.x, t1x = tx.y, t0y = ty.x, t1y = ty.y, t0z = tz.x, t1z = tz.y;
-        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
-        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-        // empty slots hold a box at (3e38, 3e38, 3e38): never wanted by a finite ray
-        key[k] = (tn <= tf && tf >= 0.0f && tn <= thi) ? tn : __builtin_inff();
+        key[k] = slab_key(nodes[ref], k, s, thi);
       }
 #define RTX_CS(a, b)         \
   if (key[b] < key[a]) {     \
@@ -600,57 +698,9 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
       ws_ll++;
       if ((int)__lane_id() == __builtin_ctzll(am)) ws_li++;
     }
-    if (lf != BVH_NONE) {
-      const int v = ~lf;
-      const int slot0 = (v >> 2) * BVH_LEAF;
-      const int cnt = (v & 3) + 1;
-      // the leaf's 4 records as {x0..x3}, {y0..y3}, {z0..z3}, {R^2 0..3}: the
-      // pre-test of §2.1 on two spheres per packed FP32 instruction (the same
-      // operations as the per-sphere form in query())
-      const float4 cx = leaf4[slot0], cy = leaf4[slot0 + 1], cz = leaf4[slot0 + 2], cw = leaf4[slot0 + 3];
-      uint32_t keep = 0;
-      const F2 po = {ox, ox}, poy = {oy, oy}, poz = {oz, oz};
-      const F2 pdx = {dx, dx}, pdy = {dy, dy}, pdz = {dz, dz}, pdd = {dd, dd}, pkl = {kline, kline};
-      const F2 pms = {ms2, ms2};
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const F2 X = h ? F2{cx.z, cx.w} : F2{cx.x, cx.y}, Y = h ? F2{cy.z, cy.w} : F2{cy.x, cy.y};
-        const F2 Z = h ? F2{cz.z, cz.w} : F2{cz.x, cz.y}, Wr = h ? F2{cw.z, cw.w} : F2{cw.x, cw.y};
-        const F2 ocx = X - po, ocy = Y - poy, ocz = Z - poz;
-        const F2 s = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
-        const F2 q = __builtin_elementwise_fma(ocx, pdx, __builtin_elementwise_fma(ocy, pdy, ocz * pdz));
-        const F2 l = __builtin_elementwise_fma(s, pdd, -(q * q));
-        const F2 r = __builtin_elementwise_fma(pdd, Wr, pkl);
-        const F2 wm = Wr + pms;
-        const bool m0 = l.x > r.x || (q.x < qneg && s.x > wm.x);   // misses the line, or wholly behind
-        const bool m1 = l.y > r.y || (q.y < qneg && s.y > wm.y);
-        keep |= (m0 ? 0u : 1u << (2 * h)) | (m1 ? 0u : 2u << (2 * h));
-      }
-      keep &= (1u << cnt) - 1u;
-      while (keep) {
-        const int u = __builtin_ctz(keep);
-        keep &= keep - 1;
-        const Sphere64 sp64 = x64[slot0 + u];
-        const V3 C = v3(sp64.c[0], sp64.c[1], sp64.c[2]);
-        V3 hit;
-        bool in;
-        if (!sphere_exact(C, sp64.r, o, d, dn, r2, hit, in)) continue;
-        const int obj = xobj[slot0 + u];
-        if (ext) {
-          const double dist = vr(vsub(o, hit));      // Ray#distance
-          if (lex_better(dist, obj, best, besti)) {
-            best = dist;
-            besti = obj;
-            bhit = hit;
-            bin = in;
-            thi = (float)(best / r * (1.0 + 1e-6));
-          }
-        } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {   // cover factor 1
-          const double cov = penumbra(C, sp64.r, o, d, radius, err);
-          if (cov != 0.0) push_cover<BS>(ci, cv, ncov, ovf, obj, cov);
-        }
-      }
-    }
+    if (lf != BVH_NONE)
+      walk_leaf<BS>(lf, leaf4, x64, xobj, s, ext, o, d, dn, r, r2, L, radius, best, besti, bhit, bin, thi, err, ci, cv,
+                    ncov, ovf);
     if (!SPEC) {
       ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
       if (PP && __popcll(__ballot(ref != BVH_NONE)) < postpone && ref != BVH_NONE) return false;
@@ -663,15 +713,7 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
     atomicAdd(&w[2], ws_li);
     atomicAdd(&w[3], ws_ll);
   }
-  if (!ext) {
-    total = 1.0;
-    if (ovf) {
-      // more than COVER_K non-zero covers: the ordered linear walk (rare)
-      query<false>(S, cptr(S.sph32), false, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
-    } else {
-      for (int k = 0; k < ncov; k++) total -= cv[k * BS];
-    }
-  }
+  if (!ext) walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf);
   return true;
 }
 
