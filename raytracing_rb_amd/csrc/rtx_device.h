@@ -777,10 +777,13 @@ __device__ __forceinline__ V3 vertical_vector(V3 n, uint32_t& err) {   // world_
 // Spheres and planes: `hit` and `in` are the walk's own evaluation of the
 // winner (kept when it became the nearest; same bits a re-evaluation gives).
 // Boxes re-evaluate to find the face.
-RTX_SHADE_FN void hit_info(const SceneDev& S, int obj, const Ray& ray, V3& hit, V3& delta, V3& n, bool& in) {
-  const Material& m = S.mat[obj];
+// `m` is the object's material and `sph64` the sphere records (global memory,
+// or the copies a bounce-level workgroup staged in LDS).
+template <typename SP>
+RTX_SHADE_FN void hit_info_m(const SceneDev& S, const Material& m, SP sph64, const Ray& ray, V3& hit, V3& delta,
+                             V3& n, bool& in) {
   if (m.type == OBJ_SPHERE) {
-    const Sphere64 sp = S.sph64[m.rec];
+    const Sphere64 sp = sph64[m.rec];
     const V3 C = v3p(sp.c);
     delta = vsc(vsc(vsub(hit, C), EPS), in ? 1.0 : -1.0);
     n = in ? vsub(hit, C) : vsub(C, hit);
@@ -800,6 +803,9 @@ RTX_SHADE_FN void hit_info(const SceneDev& S, int obj, const Ray& ray, V3& hit, 
   const double nfd = -fd;
   delta = vsc(vsc(F, EPS), nfd > 0 ? 1.0 : (nfd < 0 ? -1.0 : 0.0));   // (-f.d <=> 0).to_f
   n = fd > 0 ? vneg(F) : F;
+}
+RTX_SHADE_FN void hit_info(const SceneDev& S, int obj, const Ray& ray, V3& hit, V3& delta, V3& n, bool& in) {
+  hit_info_m(S, S.mat[obj], S.sph64, ray, hit, delta, n, in);
 }
 
 // Per-lane LIFO of pending rays (RayTracer#trace_sync's Array, ray_tracer.rb:21-30).
@@ -1121,7 +1127,7 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   const SceneDev& S = p.scene;
   size_t off = 0;
   if (mode == SPH_LIN_LDS) off = (size_t)(S.n_sphere + 4) * 16;
-  p.lds_x64 = p.lds_xobj = -1;
+  p.lds_x64 = p.lds_xobj = p.lds_mat = p.lds_sphr = -1;
   if (mode == SPH_BVH_LDS || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) {
     off = (size_t)S.n_nodes * sizeof(Bvh4Node);
     p.lds_leaf = (int32_t)off;
@@ -1131,6 +1137,11 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
       off += (size_t)S.n_slots * sizeof(Sphere64);
       p.lds_xobj = (int32_t)off;
       off += (size_t)S.n_slots * 4;
+      off = (off + 15) & ~(size_t)15;
+      p.lds_mat = (int32_t)off;                 // shading's material and sphere record of the hit object
+      off += (size_t)S.n_obj * sizeof(Material);
+      p.lds_sphr = (int32_t)off;
+      off += (size_t)S.n_sphere * sizeof(Sphere64);
     }
   }
   off = (off + 15) & ~(size_t)15;

@@ -671,7 +671,8 @@ size_t bvh_lds_budget() { return LDS_TOTAL_BYTES; }
 
 int resolve_mode(const SceneDev& S, int mode) {
   if (mode == SPH_BVH_LDSX) {                  // the staged hierarchy plus its exact records
-    const size_t need = bvh_lds_bytes(S.n_nodes, S.n_slots, S.bvh_stack) + (size_t)S.n_slots * (sizeof(Sphere64) + 4);
+    const size_t need = bvh_lds_bytes(S.n_nodes, S.n_slots, S.bvh_stack) + (size_t)S.n_slots * (sizeof(Sphere64) + 4) +
+                        16 + (size_t)S.n_obj * sizeof(Material) + (size_t)S.n_sphere * sizeof(Sphere64);
     if (need <= LDS_TOTAL_BYTES) return mode;
     mode = SPH_BVH_LDS;
   }

@@ -303,6 +303,11 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
       for (int i = threadIdx.x; i < 2 * S.n_slots; i += BS) x[i] = reinterpret_cast<const float4*>(S.bvh_sph64)[i];
       int32_t* o = reinterpret_cast<int32_t*>(lds + p.lds_xobj);
       for (int i = threadIdx.x; i < S.n_slots; i += BS) o[i] = S.bvh_obj[i];
+      float4* m = reinterpret_cast<float4*>(lds + p.lds_mat);
+      const int nm = S.n_obj * (int)(sizeof(Material) / 16);
+      for (int i = threadIdx.x; i < nm; i += BS) m[i] = reinterpret_cast<const float4*>(S.mat)[i];
+      float4* sr = reinterpret_cast<float4*>(lds + p.lds_sphr);
+      for (int i = threadIdx.x; i < 2 * S.n_sphere; i += BS) sr[i] = reinterpret_cast<const float4*>(S.sph64)[i];
     }
     __syncthreads();
   }
@@ -392,7 +397,8 @@ __device__ __forceinline__ void lv_ray_key(const KParams& p, int root, int& x, i
 __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice, bool shade, bool active,
                                           const Item& cur, int root, int x, int y, int sample, int besti, bool hin,
                                           V3 hit, V3 delta, V3 nrm, V3 nn, double c, V3 lc, int nl, char* rec,
-                                          int nleaf, uint32_t errA, uint32_t errS, uint32_t errL, uint32_t errP) {
+                                          int nleaf, uint32_t errA, uint32_t errS, uint32_t errL, uint32_t errP,
+                                          const Material* m) {
   const SceneDev& S = p.scene;
   const CameraDev& cam = *p.cam;
   const int depth = cam.depth - level;
@@ -401,7 +407,6 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
   uint32_t mask = 0;
   double rate = 0.0;
   bool may_refract = false;
-  const Material* m = shade ? &S.mat[besti] : S.mat;
   if (shade) {
     const int cd = depth - 1;
     if (cd > 0 && !(vr(vmul(cur.att, v3p(m->refl_att))) < 0.0001)) mask |= 1u;
@@ -646,7 +651,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
     }
     RTX_LV_STAMP(3)
     lv_finish(p, level, slice, shade, active, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec,
-              nleaf, errA, errS, errL, errP);
+              nleaf, errA, errS, errL, errP, shade ? &S.mat[besti] : S.mat);
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
@@ -876,8 +881,16 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     RTX_LV_STAMP(4)
     V3 delta = hit, nrm = hit, nn = hit;
     double c = 0.0;
+    // the hit object's material (and sphere record): LDS copies when staged
+    // (SPH_BVH_LDSX), so shading's first loads do not queue behind the wave's
+    // record and ray stores (vmcnt counts loads and stores in issue order)
+    const Material* mats = SPH == SPH_BVH_LDSX ? reinterpret_cast<const Material*>(lds + p.lds_mat) : S.mat;
+    const Material* m = shade ? mats + besti : mats;
     if (shade) {
-      hit_info(S, besti, cur.ray, hit, delta, nrm, hin);
+      if (SPH == SPH_BVH_LDSX)
+        hit_info_m(S, *m, reinterpret_cast<const Sphere64*>(lds + p.lds_sphr), cur.ray, hit, delta, nrm, hin);
+      else
+        hit_info(S, besti, cur.ray, hit, delta, nrm, hin);
       nn = vnorm(nrm, errS);                  // n.normalize (world_object.rb:123)
       c = vcos(cur.ray.d, nrm, errS);         // ray.front.cos(-n): same bits as cos(n)
     }
@@ -909,7 +922,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     }
     RTX_LV_STAMP(3)
     lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec, 0,
-              errA, errS, errL, errP);
+              errA, errS, errL, errP, m);
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
@@ -1131,7 +1144,7 @@ __device__ __forceinline__ void k_lv_shade_body(const KParams& p, int level) {
       }
     }
     lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec,
-              0, errA, errS, errL, errP);
+              0, errA, errS, errL, errP, shade ? &S.mat[besti] : S.mat);
   }
 }
 
@@ -1612,7 +1625,8 @@ int levels_auto_mode(const SceneDev& S, int mode, int compact, int split) {
   const size_t waves = BS_BVH / 64;
   const size_t walk = (size_t)S.bvh_stack * BS_BVH * 4 + (size_t)COVER_K * BS_BVH * 12 + 64;
   const size_t nodes = (size_t)S.n_nodes * sizeof(Bvh4Node), leaves = (size_t)S.n_slots * 16;
-  const size_t exact = (size_t)S.n_slots * (sizeof(Sphere64) + 4);
+  const size_t exact = (size_t)S.n_slots * (sizeof(Sphere64) + 4) + 16 + (size_t)S.n_obj * sizeof(Material) +
+                       (size_t)S.n_sphere * sizeof(Sphere64);   // + shading's materials and sphere records
   // C2: the exact test's records staged too (r05d: 4.91-4.94 -> 4.85 ms, same bits)
   if (nodes + leaves + exact + walk + waves * LV_RING_WAVE_BYTES <= LDS_TOTAL_BYTES) return SPH_BVH_LDSX;
   if (nodes + leaves + walk + waves * LV_RING_WAVE_BYTES <= LDS_TOTAL_BYTES) return mode;   // LDS + full ring

@@ -79,6 +79,8 @@ struct Material {
   int32_t rec;            // index into the type's record array
 };
 
+static_assert(sizeof(Material) % 16 == 0, "Material staged in LDS as float4");
+
 struct LightDev {
   double pos[3];
   double color[3];
