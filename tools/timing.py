@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--size", default="")
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--share", default="", help="k/N: time rank k's share of N ranks (8-row tiles)")
+    ap.add_argument("--share", default="", help="k/N: time rank k's share of N ranks (--tile-rows-row tiles)")
+    ap.add_argument("--tile-rows", type=int, default=8, help="rows per round-robin tile of --share")
     ap.add_argument("--dummy-streams", type=int, default=0,
                     help="with --inflight: create this many unused streams before each option set's streams")
     ap.add_argument("--keep", action="store_true", help="with --inflight: keep every option set's contexts open")
@@ -52,7 +53,7 @@ def main():
 
     def render(r):
         if share:
-            r.render_tiles_device(out.data_ptr(), 8, share[0], share[1], stream=s.cuda_stream)
+            r.render_tiles_device(out.data_ptr(), a.tile_rows, share[0], share[1], stream=s.cuda_stream)
         else:
             r.render_device(out.data_ptr(), stream=s.cuda_stream)
     kept = []
@@ -72,7 +73,7 @@ def main():
             def frame(i):
                 k = i % a.inflight
                 if share:
-                    rs[k].render_tiles_device(outs[k].data_ptr(), 8, share[0], share[1], stream=ss[k].cuda_stream)
+                    rs[k].render_tiles_device(outs[k].data_ptr(), a.tile_rows, share[0], share[1], stream=ss[k].cuda_stream)
                 else:
                     rs[k].render_device(outs[k].data_ptr(), stream=ss[k].cuda_stream)
             for i in range(2 * a.inflight):
