@@ -195,8 +195,11 @@ def main():
     ap.add_argument("--force-collective", action="store_true",
                     help="run the multi-GPU step (tile shares, RCCL gather to rank 0, pipelined) even with one "
                          "rank: a 1-rank RCCL group (evidence that the C3 path runs on ROCm)")
+    ap.add_argument("--tile-rows", type=int, default=TILE_ROWS,
+                    help="rows per round-robin tile of a rank's share (default %d)" % TILE_ROWS)
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # CPU test of the rank plumbing
     args = ap.parse_args()
+    globals()["TILE_ROWS"] = args.tile_rows      # every share / gather of this run
 
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
