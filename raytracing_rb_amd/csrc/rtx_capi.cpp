@@ -974,6 +974,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_lcap = (uint32_t)lcap;
   p.lv_rec_bytes = rec_bytes;
   p.lv_ray_dbl = (c->opt_lv_ray_bytes == 96 || !path32) ? 12 : 10;
+  p.lv_last_level = c->cam.depth >= 1 ? c->cam.depth - 1 : -1;
   p.lv_acc = c->d_lvstats;
   p.samples = nullptr;
   LvAux aux{};

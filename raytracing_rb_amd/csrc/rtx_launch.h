@@ -99,6 +99,8 @@ struct KParams {
   double* lv_area;                 // split: {1 - covers, raise} per (hit, light)
   int32_t lv_compact;              // k_level: park hits in an LDS ring, shade full waves (-1 auto, 0 off, 1 on, 2 compact ring)
   int32_t lds_ring;                // k_level (compacting): LDS byte offset of the per-wave hit rings
+  int32_t lv_last_level;           // trace_depth - 1 (-1 if trace_depth < 1): the level whose children are all
+                                   // cut off, run by a k_level_c compiled for it
   int32_t lv_grid_div;             // level launches: persistent grid = resident workgroups / this (option lv_grid_div)
   int32_t lv_fin_cap;              // tree reduction: records of a tile gathered into LDS (0: walk from global memory)
   int32_t lv_fin_tiles;            // tree reduction pass 0: tiles of the batch (grid-stride loop when the grid is smaller)

@@ -398,10 +398,10 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
                                           const Item& cur, int root, int x, int y, int sample, int besti, bool hin,
                                           V3 hit, V3 delta, V3 nrm, V3 nn, double c, V3 lc, int nl, char* rec,
                                           int nleaf, uint32_t errA, uint32_t errS, uint32_t errL, uint32_t errP,
-                                          const Material* m) {
+                                          const Material* m, bool last = false) {
   const SceneDev& S = p.scene;
   const CameraDev& cam = *p.cam;
-  const int depth = cam.depth - level;
+  const int depth = last ? 1 : cam.depth - level;   // last: the batch's last level (every child is cut off)
   const int pt = cam.pt;
   const uint64_t R = (uint64_t)pt + 3;
   uint32_t mask = 0;
@@ -705,7 +705,7 @@ constexpr int LV_RING_FIELDS_SMALL = 5;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
 constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMALL * 8;
 
-template <int SPH, int BS, int RF>
+template <int SPH, int BS, int RF, bool LAST>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
   constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
@@ -717,7 +717,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   if (in.chunks == 0) return;                 // uniform: before any barrier
   lv_stage_scene<SPH, BS>(p, lds_sph);
   const uint32_t base = lv_base(p, level);
-  const int depth = p.cam->depth - level;
+  const int depth = LAST ? 1 : p.cam->depth - level;   // LAST: the batch's last level, compiled apart
   LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
   const int slice = sched.wave_id() & (LV_SLICES - 1);
   const int lane = (int)__lane_id();
@@ -922,7 +922,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     }
     RTX_LV_STAMP(3)
     lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec, 0,
-              errA, errS, errL, errP, m);
+              errA, errS, errL, errP, m, LAST);
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
@@ -940,9 +940,9 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS, int RF>
+template <int SPH, int BS, int RF, bool LAST>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
-  k_level_c_body<SPH, BS, RF>(p, level);
+  k_level_c_body<SPH, BS, RF, LAST>(p, level);
   lv_level_done(p, level + 1);
 }
 
@@ -1690,11 +1690,12 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
     if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
-      kern = k_level_c<SPH, BS, LV_RING_FIELDS>;
+      kern = level == q.lv_last_level ? k_level_c<SPH, BS, LV_RING_FIELDS, true> : k_level_c<SPH, BS, LV_RING_FIELDS, false>;
     } else if (BVH && need_small <= budget) {  // the compact ring (C4-sized hierarchies)
       q.lds_ring = (int32_t)ring;
       lds = need_small;
-      kern = k_level_c<SPH, BS, LV_RING_FIELDS_SMALL>;
+      kern = level == q.lv_last_level ? k_level_c<SPH, BS, LV_RING_FIELDS_SMALL, true>
+                                      : k_level_c<SPH, BS, LV_RING_FIELDS_SMALL, false>;
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)
