@@ -408,37 +408,86 @@ def main():
     r.set_option("kernel_events", 0)
     kern_frame_ms = float(np.median(kern_ms))
 
+    # ---- multi-rank step (C3): what each rank's share and the gather cost, so
+    # the driver's N-GPU line explains itself: every rank renders its share
+    # alone (one frame, context 0, HIP events on its stream), then the
+    # ranks time the gather itself (events around a blocking dist.gather on the
+    # current stream, after a barrier); rank 0 collects them.
+    rank_breakdown = None
+    if dist_step:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        rms_ = []
+        for _ in range(3):
+            ev[0].record(streams[0])
+            r.render_tiles_device(df.bufs[0].data_ptr(), TILE_ROWS, rank, world, seed=1,
+                                  stream=streams[0].cuda_stream)
+            ev[1].record(streams[0])
+            ev[1].synchronize()
+            rms_.append(ev[0].elapsed_time(ev[1]))
+        r.sync(streams[0].cuda_stream)
+        gms = []
+        for _ in range(3):
+            barrier()
+            ev[0].record(stream)
+            df.gather_finish(df.gather_start(df.bufs[0]))
+            ev[1].record(stream)
+            ev[1].synchronize()
+            gms.append(ev[0].elapsed_time(ev[1]))
+        mine = torch.tensor([float(np.median(rms_)), float(np.median(gms))], dtype=torch.float64, device=dev)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        rank_breakdown = {"render_ms": [round(float(v[0]), 4) for v in allv],
+                          "gather_ms": [round(float(v[1]), 4) for v in allv],
+                          "packed_bytes_per_rank": int(rows_per_rank(H, TILE_ROWS, world) * W * 3 * 8),
+                          "method": "one frame's share rendered alone on context 0 of each rank (HIP events on its "
+                                    "stream, median of 3); the gather of one packed frame to rank 0 after a "
+                                    "barrier (events around a blocking dist.gather on the current stream, median "
+                                    "of 3; it includes waiting for the slowest rank's enqueue)"}
+
     # ---- 1-GPU projection of the tile-sharded frame (C3) for N = 2, 4, 8
     projection = None
     if world == 1 and emulate is None and not args.no_projection:
-        def timed(fn, reps=3):
-            """Per-frame ms of fn(j) over F frames in flight (frame i on context i mod F), median of reps."""
+        def timed(fn, nf):
+            """Per-frame ms of nf frames of fn(j) in flight (frame i on context i mod F)."""
+            a = time.perf_counter()
+            for i in range(nf):
+                fn(i % F)
+            torch.cuda.synchronize(dev)
+            return (time.perf_counter() - a) / nf * 1e3
+
+        def warm(fn):
             for j in range(F):
                 fn(j)
             torch.cuda.synchronize(dev)
-            ts = []
-            nf = 4 * F
-            for _ in range(reps):
-                a = time.perf_counter()
-                for i in range(nf):
-                    fn(i % F)
-                torch.cuda.synchronize(dev)
-                ts.append((time.perf_counter() - a) / nf)
-            return float(np.median(ts)) * 1e3
-        full_ms = timed(render_full)
+        REPS = 5
+        warm(render_full)
+        full_ms = float(np.median([timed(render_full, 4 * F) for _ in range(REPS)]))
         projection = {"method": "each rank's share rendered alone on this GPU (rtx_render_tiles_device) with the "
-                                "bench's %d frame(s) in flight, per-frame median of 3 x %d frames after a warm-up; "
-                                "projected frame = max over ranks; the RCCL gather is estimated separately at %.0f "
-                                "GB/s per xGMI link (the multi-GPU step overlaps it with the next frame's render)"
-                                % (F, 4 * F, XGMI_LINK_GBS),
+                                "bench's %d frame(s) in flight: every share warmed up once, then %d rounds that "
+                                "time every rank's share (%d frames each) in an order rotated by one rank per "
+                                "round, so clock or warm-up drift spreads over all ranks; rank_ms = per-rank "
+                                "median; projected frame = max over ranks; the RCCL gather is estimated "
+                                "separately at %.0f GB/s per xGMI link (the multi-GPU step overlaps it with the "
+                                "next frame's render)" % (F, REPS, 4 * F, XGMI_LINK_GBS),
                       "full_frame_ms": round(full_ms, 4), "per_n": {}}
         for n in PROJECT_N:
-            shares = [timed(lambda j, k=k: share_render(k, n, j)) for k in range(n)]
+            fns = [lambda j, k=k: share_render(k, n, j) for k in range(n)]
+            for fn in fns:
+                warm(fn)
+            per = [[] for _ in range(n)]
+            for rep in range(REPS):
+                for q in range(n):
+                    k = (q + rep) % n
+                    per[k].append(timed(fns[k], 4 * F))
+            shares = [float(np.median(v)) for v in per]
             packed_bytes = rows_per_rank(H, TILE_ROWS, n) * W * 3 * 8
             gather_ms = packed_bytes / (XGMI_LINK_GBS * 1e9) * 1e3
             mx = max(shares)
+            med = float(np.median(shares))
             projection["per_n"][str(n)] = {
                 "rank_ms": [round(v, 4) for v in shares], "max_rank_ms": round(mx, 4),
+                "rank_spread": round((mx - min(shares)) / med, 4),
+                "rank_ms_rounds": [[round(x, 4) for x in v] for v in per],
                 "gather_est_ms": round(gather_ms, 4),
                 "projected_speedup": round(full_ms / (mx + gather_ms), 3),
                 "projected_speedup_no_gather": round(full_ms / mx, 3)}
@@ -519,6 +568,8 @@ def main():
         }
         if gather_check is not None:
             line["gather_check"] = gather_check
+        if rank_breakdown is not None:
+            line["ranks"] = rank_breakdown
         if emulate:
             line["emulate_rank"] = {"rank": emulate[0], "nranks": emulate[1],
                                     "rank_ms_per_frame": round(elapsed / args.steps * 1e3, 4)}

@@ -312,7 +312,10 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          neutral on C2), "lv_ray_bytes" (bounce levels: staged ray record, 80 = origin, direction, attenuation,
          {path, root} with the RNG key decoded from the root, 96 = with a 64-bit path and the key stored; 0 [default]
          = 80 whenever (monte_carlo_diffusion_times + 3)^trace_depth <= 2^32, else 96; 80 for a camera whose paths
-         do not fit fails the render with RTX_EINVAL; same bits). */
+         do not fit fails the render with RTX_EINVAL; same bits), "exact_raises" (1: every shadow walk of
+         local_lights also checks the Math.acos raise of the covers it skips, spheres whose binary cover factor is 0
+         (sphere.rb:45-46), so the reference's raise is reported wherever it happens; 0 [default]:
+         only the covers the walk evaluates; World#high_lights' lit_area is checked either way; same colours). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

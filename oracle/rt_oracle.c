@@ -17,8 +17,9 @@
  * this image) and pinned by the two restatements + goldens.
  *
  * Departures (documented in DESIGN.md): counter RNG instead of Random.rand;
- * World#high_lights' truthiness-only lit_area call (world.rb:91-92) is not
- * evaluated; no LOG tracing.
+ * no LOG tracing.  World#high_lights' lit_area (world.rb:92-93) is evaluated
+ * for its raises (its value is always truthy) but not counted in the work
+ * counters, which count the brute-force events of local_lights' walks.
  */
 #define _GNU_SOURCE
 #include "../include/rtx.h"
@@ -495,7 +496,16 @@ static void rt_map(Tr* tr, Item it, V* sum, T* t) {                /* ray_tracer
     double c = vcos(it.ray.d, vsub(s->light[l].pos, it.ray.o), t);
     if (c < -1) c = -1;
     if (c > 1) c = 1;
-    if (dacos(c, t) < (s->light[l].hl_angle / 180.0 * M_PI)) tr->lit[nfired++].light = l;
+    if (dacos(c, t) < (s->light[l].hl_angle / 180.0 * M_PI)) {
+      /* `&& lit_area(ray.position, light.position, light.radius, object)`
+       * (world.rb:92-93): a number, always truthy, but its Sphere#cover_area
+       * can raise (Math.acos, sphere.rb:45-46) */
+      uint64_t keep[RTX_NCOUNT];
+      memcpy(keep, t->cnt, sizeof keep);
+      (void)lit_area(s, it.ray.o, s->light[l].pos, s->light[l].radius, t);
+      memcpy(t->cnt, keep, sizeof keep);
+      tr->lit[nfired++].light = l;
+    }
   }
   if (nfired) {
     for (int k = 0; k < nfired; k++) {

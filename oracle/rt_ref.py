@@ -8,8 +8,8 @@ bit-exact cross-check of the C oracle (``rt_oracle.c``).
 Deliberate, documented departures from the Ruby program:
 * ``Random.rand`` is replaced by the counter RNG of ``oracle/rng.py``.
 * ``World#high_lights`` evaluates ``lit_area`` only for its truthiness, which is
-  always true in Ruby (``world.rb:91-92``); the call cannot change a pixel, so it
-  is not evaluated here (nor in the C oracle, nor on the GPU).
+  always true in Ruby (``world.rb:92-93``); it is evaluated here (and in the C
+  oracle, and on the GPU) because its ``Sphere#cover_area`` can raise.
 * The ``LOG.logt`` trace (``logger.rb``) is not emitted (no effect on pixels).
 * Texture files are decoded by Pillow (``>>8`` on 16-bit samples, matching
   RMagick's ``(pixel.red >> 8)`` at ``texture.rb:19``).
@@ -427,7 +427,10 @@ class World:                       # src/world.rb
             if cos_theta > 1:
                 cos_theta = 1
             ang = _acos(cos_theta)
-            if ang < (light.high_light_angle / 180.0 * math.pi):
+            # `&& lit_area(ray.position, light.position, light.radius, object)`
+            # (:92-93): always truthy (a number), but it runs and can raise
+            if ang < (light.high_light_angle / 180.0 * math.pi) and \
+                    self.lit_area(ray.position, light.position, light.radius) is not None:
                 ret.append((light, light.color * float(light.high_light_rate)))
         return ret
 

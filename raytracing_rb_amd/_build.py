@@ -46,20 +46,28 @@ def build_cli(force=False, verbose=False):
     return CLI_OUT
 
 
-def source_sha():
+def source_sha(extra=()):
     """Identity of the kernel build: sha256 over the device sources, headers and
-    build flags (embedded in librtx.so as rtx_build_id, checked at load)."""
+    build flags, plus any extra defines (embedded in librtx.so as rtx_build_id,
+    checked at load against the no-defines identity: a diagnostic build written
+    in place of the production library is refused)."""
     import hashlib
     h = hashlib.sha256()
     for f in SOURCES + HEADERS:
         with open(f, "rb") as fh:
             h.update(fh.read())
     h.update(" ".join(FLAGS).encode())
+    if extra:
+        h.update(("\0" + " ".join(extra)).encode())
     return h.hexdigest()[:16]
 
 
 def stale():
     if not os.path.exists(OUT):
+        return True
+    # a diagnostic build (defines) written over the production library is stale
+    tag = os.path.join(ROOT, "build", "obj", os.path.basename(OUT), "flags")
+    if not os.path.exists(tag) or open(tag).read() != " ".join(FLAGS):
         return True
     t = os.path.getmtime(OUT)
     return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS + [__file__])
@@ -80,7 +88,7 @@ def build(force=False, verbose=False, out=None, defines=()):
     with open(tag, "w") as f:
         f.write(" ".join(FLAGS + dflags))
     newest_dep = max(os.path.getmtime(p) for p in HEADERS + [__file__])
-    sha = source_sha()
+    sha = source_sha(dflags)
     for src in SOURCES:
         obj = os.path.join(odir, os.path.basename(src) + ".o")
         objs.append(obj)

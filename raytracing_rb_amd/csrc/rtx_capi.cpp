@@ -88,6 +88,7 @@ struct rtx_context {
   int64_t opt_lv_redo_blocks = 8;    // bounce levels: workgroups of the overflow re-render launch (0: all resident)
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   int64_t opt_lv_ray_bytes = 0;      // bounce levels: staged ray record, 0 auto (80 B when every path fits 32 bits), 80, 96
+  int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also run the raise walk of the covers they skip
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
@@ -429,7 +430,8 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact},
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
       {"lv_redo_blocks", c->opt_lv_redo_blocks}, {"lv_fin_cap", c->opt_lv_fin_cap},
-      {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes}};
+      {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
+      {"exact_raises", c->opt_exact_raises}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -516,6 +518,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_fin_cap")) {        // bounce levels: LDS tree records per tile in the reduction, 0 = off
     if (value < 0 || value > 4096) return fail(c, RTX_EINVAL, "lv_fin_cap must be in [0, 4096]");
     c->opt_lv_fin_cap = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "exact_raises")) {      // every shadow walk also checks the skipped covers' acos raises
+    if (value != 0 && value != 1) return fail(c, RTX_EINVAL, "exact_raises must be 0 or 1");
+    c->opt_exact_raises = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_ray_bytes")) {      // bounce levels: staged ray record size (0 auto)
@@ -867,6 +874,7 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
   p.max_samples = c->cam.max_samples;
   // Postponing long walks pays when walks are long (C4, 341 nodes: 550 -> 507 ms)
   // and costs when they are short (C2, a few nodes: 9.0 -> 9.3 ms).
+  p.exact_raises = (int32_t)c->opt_exact_raises;
   p.postpone = c->opt_postpone >= 0 ? (int32_t)c->opt_postpone : (c->scene.n_nodes >= RTX_POSTPONE_NODES ? 16 : 0);
   return RTX_OK;
 }
@@ -1322,9 +1330,11 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
       if (re != ncclSuccess && !what) r = re, what = "ncclGroupEnd";
     }
     if (what) {
+      // sends / receives may already be enqueued: abort (ncclCommDestroy would
+      // wait for them and can hang where abort does not)
       for (size_t k = 0; k < c0->comms.size(); k++) {
         hipSetDevice(c0->comm_devs[k]);
-        ncclCommDestroy(c0->comms[k]);
+        ncclCommAbort(c0->comms[k]);
       }
       c0->comms.clear();
       c0->comm_devs.clear();
@@ -1349,15 +1359,23 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
   ErrState all;
   all.flags = 0;
   for (int code = 0; code < 5; code++) all.first[code] = ~0ull;
+  // Every rank's record is taken (and reset) even after one fails, so no
+  // rank is left holding raises for a later call; the first failure wins.
+  rtx_status take_fail = RTX_OK;
+  int fail_rank = -1;
   for (int k = 0; k < n; k++) {
     ErrState e;
     const rtx_status st = take_errors(ctxs[k], nullptr, &e);
-    if (st) return fail(c0, st, "rank %d: %s", k, rtx_last_error(ctxs[k]));
+    if (st) {
+      if (!take_fail) take_fail = st, fail_rank = k;
+      continue;
+    }
     all.flags |= e.flags;
     for (int code = 0; code < 5; code++)
       if (e.first[code] < all.first[code]) all.first[code] = e.first[code];
   }
   hipSetDevice(devs[0]);
+  if (take_fail) return fail(c0, take_fail, "rank %d: %s", fail_rank, rtx_last_error(ctxs[fail_rank]));
   return report_errors(c0, all);
 }
 

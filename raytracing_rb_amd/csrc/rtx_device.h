@@ -717,6 +717,155 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
   return true;
 }
 
+// ----------------------------------------------------------------- World#lit_area's raises
+// Sphere#cover_area (sphere.rb:28-57) runs its penumbra arithmetic for every
+// sphere, whatever its binary factor, and Math.acos raises Math::DomainError
+// for a cos_theta below -1 (only the upper clamp exists, :43-44).  Inside the
+// branch d > |R - r1| neither can be below -1 in exact arithmetic:
+//   cos_theta1 + 1 = (r1 + d - R)(r1 + d + R) / (2 r1 d),
+//   cos_theta2 + 1 = (R + d - r1)(R + d + r1) / (2 R d);
+// rounded, either can when d is within a few ulps of |R - r1| (DESIGN.md §2.4;
+// tools/raise_search.py finds such configurations).  The shading walks skip
+// the penumbra of spheres whose factor is 0, so these raises need their own
+// walk: World#high_lights' lit_area (world.rb:92-93) always, World#local_lights'
+// (world.rb:76) with option exact_raises.
+//
+// penumbra_raises: the reference's own operations up to the two acos
+// arguments (the bits of penumbra() and of rt_oracle.c's cover_area).
+__device__ __forceinline__ bool penumbra_raises(V3 C, double R, V3 T, V3 lt, double radius) {
+  const double t = vdot(vsub(C, T), lt) / vr2(lt);
+  const V3 x1 = vadd(T, vsc(lt, t));
+  const double r1 = radius * (vr(vsub(x1, T)) / vr(lt));
+  const double d = vr(vsub(x1, C));
+  if (d >= r1 + R) return false;                 // :38-39 (a NaN goes on, as in Ruby, and never raises)
+  if (!(d > fabs(R - r1))) return false;         // :42
+  const double c1 = (r1 * r1 + d * d - R * R) / (2.0 * r1 * d);
+  const double c2 = (R * R + d * d - r1 * r1) / (2.0 * R * d);
+  return c1 < -1.0 || c2 < -1.0;                 // ([x, 1.0].min < -1 iff x < -1)
+}
+
+// Which spheres can raise, in float32 (s: signed distance of the center along
+// the unit axis u from T, rho: its distance from the axis line, k = radius /
+// |L - T|, so r1 = k |s|).  A raise needs d = |R - r1| up to rounding:
+//   (A) R > r1: rho ~ R - r1 <= R, the axis line meets the ball;
+//   (B) r1 > R: rho + R ~ k |s|, the ball touches the cone rho = k |s| from
+//       inside (its point farthest from the axis lies on the cone).
+// A child box is searched when its bounding ball (center c, radius h) could
+// hold such a sphere: the line meets the ball, or f = rho - k |s| takes values
+// of both signs on it.  mg covers the float32 rounding of T, u, k, the centers
+// and the box bounds (each a few ulps of the scene scale Sx, times 1 + k for
+// the cone): 2e-5 Sx (1 + k) is more than ten times that.
+struct RaiseAxis {
+  float tx, ty, tz, ux, uy, uz, k, mg;
+};
+
+__device__ __forceinline__ void raise_sr(const RaiseAxis& a, float cx, float cy, float cz, float& s, float& rho) {
+  const float wx = cx - a.tx, wy = cy - a.ty, wz = cz - a.tz;
+  s = __builtin_fmaf(wx, a.ux, __builtin_fmaf(wy, a.uy, wz * a.uz));
+  const float px = __builtin_fmaf(wy, a.uz, -wz * a.uy), py = __builtin_fmaf(wz, a.ux, -wx * a.uz),
+              pz = __builtin_fmaf(wx, a.uy, -wy * a.ux);
+  rho = sqrtf(__builtin_fmaf(px, px, __builtin_fmaf(py, py, pz * pz)));
+}
+
+__device__ __forceinline__ bool raise_box(const RaiseAxis& a, float lx, float hx, float ly, float hy, float lz, float hz) {
+  float s, rho;
+  raise_sr(a, 0.5f * (lx + hx), 0.5f * (ly + hy), 0.5f * (lz + hz), s, rho);
+  const float h = 0.5f * ((hx - lx) + (hy - ly) + (hz - lz));   // >= the half diagonal
+  const float as = fabsf(s);
+  if (rho - h <= a.mg) return true;                                        // (A)
+  const float fmin = fmaxf(rho - h, 0.0f) - a.k * (as + h);
+  const float fmax = rho + h - a.k * fmaxf(as - h, 0.0f);
+  return fmin <= a.mg && fmax >= -a.mg;                                    // (B); NaN: false
+}
+
+__device__ __forceinline__ bool raise_sphere(const RaiseAxis& a, float cx, float cy, float cz, float R2) {
+  float s, rho;
+  raise_sr(a, cx, cy, cz, s, rho);
+  const float R = sqrtf(R2);
+  return rho <= R + a.mg || fabsf(rho + R - a.k * fabsf(s)) <= a.mg;
+}
+
+// Does World#lit_area(T, L, radius) raise?  `nodes`/`leaf4`/`x64` are the
+// hierarchy (LDS or global; nullptr: every sphere in record order), `stk`
+// this lane's traversal stack (stride BS entries, free while this runs).
+// Rare (highlight rays) or optional (exact_raises), so out of line: its
+// registers stay out of the level kernels' allocation.
+__device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Node* nodes, const float4* leaf4,
+                                             const Sphere64* x64, int* stk, int bs, V3 T, V3 L, double radius) {
+  if (!(radius > 0.0) || S.n_sphere == 0) return false;   // r1 <= 0: no d with |R - r1| < d < r1 + R
+  const V3 lt = vsub(L, T);
+  RaiseAxis a;
+  a.tx = (float)T.x, a.ty = (float)T.y, a.tz = (float)T.z;
+  const float lx = (float)lt.x, ly = (float)lt.y, lz = (float)lt.z;
+  const float ln = sqrtf(__builtin_fmaf(lx, lx, __builtin_fmaf(ly, ly, lz * lz)));
+  a.ux = lx / ln, a.uy = ly / ln, a.uz = lz / ln;
+  a.k = (float)radius / ln;
+  const float Sx = fabsf(a.tx) + fabsf(a.ty) + fabsf(a.tz) + S.sph_scale;
+  a.mg = CULL_M * Sx * (1.0f + a.k);
+  const bool fin = __builtin_isfinite(a.ux) && __builtin_isfinite(a.uy) && __builtin_isfinite(a.uz) &&
+                   __builtin_isfinite(a.k) && __builtin_isfinite(a.mg) && ln > 0.0f;
+  if (nodes == nullptr || S.bvh_root == BVH_NONE || !fin) {
+    // every sphere in record order (the float32 filter only where it is valid)
+    for (int i = 0; i < S.n_sphere; i++) {
+      if (fin && !raise_sphere(a, S.sph32[4 * i], S.sph32[4 * i + 1], S.sph32[4 * i + 2], S.sph32[4 * i + 3]))
+        continue;
+      const Sphere64 sp = S.sph64[i];
+      if (penumbra_raises(v3p(sp.c), sp.r, T, lt, radius)) return true;
+    }
+    return false;
+  }
+  int sp = 0;
+  int ref = S.bvh_root;
+  while (true) {
+    if (ref >= 0 && ref != BVH_NONE) {           // inner node: every child that may hold a raising sphere
+      const Bvh4Node& nd = nodes[ref];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int ch = nd.child[k];
+        if (ch == BVH_NONE) continue;
+        if (raise_box(a, nd.lh[0][k][0], nd.lh[0][k][1], nd.lh[1][k][0], nd.lh[1][k][1], nd.lh[2][k][0],
+                      nd.lh[2][k][1]))
+          stk[(sp++) * bs] = ch;
+      }
+    } else if (ref != BVH_NONE) {                // leaf
+      const int v = ~ref;
+      const int slot0 = (v >> 2) * BVH_LEAF;
+      const int cnt = (v & 3) + 1;
+      const float4 cx = leaf4[slot0], cy = leaf4[slot0 + 1], cz = leaf4[slot0 + 2], cw = leaf4[slot0 + 3];
+      const float X[4] = {cx.x, cx.y, cx.z, cx.w}, Y[4] = {cy.x, cy.y, cy.z, cy.w}, Z[4] = {cz.x, cz.y, cz.z, cz.w},
+                  W[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (u >= cnt || !raise_sphere(a, X[u], Y[u], Z[u], W[u])) continue;
+        const Sphere64 s64 = x64[slot0 + u];
+        if (penumbra_raises(v3p(s64.c), s64.r, T, lt, radius)) return true;
+      }
+    }
+    if (sp == 0) break;
+    ref = stk[(--sp) * bs];
+  }
+  return false;
+}
+
+// lit_area_raises over a launch's sphere mode: the hierarchy from where the
+// workgroup staged it (SphMode), the lane's LDS traversal stack.
+template <int SPH, int BS>
+__device__ __forceinline__ bool raises_walk(const KParams& p, char* lds, V3 T, V3 L, double radius) {
+  const SceneDev& S = p.scene;
+  int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
+  if (SPH == SPH_BVH_LDS || SPH == SPH_BVH_LDSX)
+    return lit_area_raises(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
+                           SPH == SPH_BVH_LDSX ? reinterpret_cast<const Sphere64*>(lds + p.lds_x64) : S.bvh_sph64, stk,
+                           BS, T, L, radius);
+  if (SPH == SPH_BVH_MIX)
+    return lit_area_raises(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(S.bvh_sph32),
+                           S.bvh_sph64, stk, BS, T, L, radius);
+  if (SPH == SPH_BVH_GLOBAL)
+    return lit_area_raises(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, stk, BS, T, L,
+                           radius);
+  return lit_area_raises(S, nullptr, nullptr, nullptr, nullptr, 0, T, L, radius);
+}
+
 // ----------------------------------------------------------------- shading
 // WorldObject#get_reflection_by_ray_and_n (world_object.rb:121-125).
 // nn = n.normalize, c = ray.front.cos(-n) (== ray.front.cos(n): |cos| of a
@@ -992,12 +1141,18 @@ __device__ __forceinline__ Ray lens_ray(const CameraDev& c, V3 target, int x, in
 
 // World#high_lights (world.rb:83-98) for `ray`: every fired light's leaf goes
 // to `leaf(V3)` in light order.  Returns true if any light fired (the ray then
-// stops, ray_tracer.rb:77).  The `&& lit_area(...)` is always truthy in Ruby and
-// is not evaluated.
+// stops, ray_tracer.rb:77).  The `&& lit_area(ray.position, light.position,
+// light.radius, object)` of a light whose cone the ray is in is always truthy
+// in Ruby (a number), but it runs, and its Sphere#cover_area can raise
+// (Math.acos, sphere.rb:45-46): `raises(T, L, radius)` answers whether it does
+// (lit_area_raises), asked only while the ray has no raise yet.
 // att_fn() gives the ray's attenuation, asked for only when a light fires.
-template <typename Att, typename Leaf>
+#ifndef RTX_HL_RAISES
+#define RTX_HL_RAISES 1      // 0: diagnostic builds only (timing without the highlight's lit_area raise walk)
+#endif
+template <typename Att, typename Leaf, typename Rz>
 __device__ __forceinline__ bool highlight_leaves_att(const SceneDev& S, const Ray& ray, Att&& att_fn, Leaf&& leaf,
-                                                     uint32_t& err) {
+                                                     uint32_t& err, Rz&& raises) {
   Item it;
   it.ray = ray;
   uint32_t fired = 0;
@@ -1029,6 +1184,8 @@ __device__ __forceinline__ bool highlight_leaves_att(const SceneDev& S, const Ra
     if (fire) {
       fired |= 1u << l;
       nfired++;
+      if (RTX_HL_RAISES && !(err & 0xffu) && raises(it.ray.o, v3(L.pos[0], L.pos[1], L.pos[2]), L.radius))
+        seterr(err, ERR_DOMAIN);
     }
   }
   if (!nfired) return false;
@@ -1041,20 +1198,21 @@ __device__ __forceinline__ bool highlight_leaves_att(const SceneDev& S, const Ra
   return true;
 }
 
-template <typename Leaf>
-__device__ __forceinline__ bool highlight_leaves(const SceneDev& S, const Item& it, Leaf&& leaf, uint32_t& err) {
-  return highlight_leaves_att(S, it.ray, [&] { return it.att; }, leaf, err);
+template <typename Leaf, typename Rz>
+__device__ __forceinline__ bool highlight_leaves(const SceneDev& S, const Item& it, Leaf&& leaf, uint32_t& err,
+                                                 Rz&& raises) {
+  return highlight_leaves_att(S, it.ray, [&] { return it.att; }, leaf, err, raises);
 }
 
 // The same into a running sum.  REDUCE: leaves go through rt_reduce
 // (trace_sync); path_trace adds them with a plain `ret +=` (ray_tracer.rb:210),
 // no "color greater than 1" check.
-template <bool REDUCE = true>
-__device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3& sum, uint32_t& err) {
+template <bool REDUCE = true, typename Rz>
+__device__ __forceinline__ bool highlights(const SceneDev& S, const Item& it, V3& sum, uint32_t& err, Rz&& raises) {
   return highlight_leaves(S, it, [&](V3 c) {
     if (REDUCE) add_leaf(sum, c, err);
     else sum = vadd(sum, c);
-  }, err);
+  }, err, raises);
 }
 
 // `key` orders the raise sites as the reference meets them: (x * height + y) * 2

@@ -30,6 +30,8 @@
 // so it changes no bit of any result.
 #include "rtx_device.h"
 
+#include <unordered_map>
+
 #include <mutex>
 #include <vector>
 
@@ -172,7 +174,9 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
           cnt[C_RAYS]++;
           cnt[C_HIGHLIGHT_TESTS] += S.n_light;
         }
-        if (highlights(S, cur, sum, err)) continue;
+        if (highlights(S, cur, sum, err,
+                       [&](V3 T, V3 L, double rad) { return raises_walk<SPH, BS>(p, lds, T, L, rad); }))
+          continue;
         mode = M_EXTEND;
         qo = cur.ray.o;
         qd = cur.ray.d;
@@ -313,6 +317,9 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
     } else {
       // World#local_lights (world.rb:72-80) fused with the light loop of
       // WorldObject#local_lighting (world_object.rb:51-74): same order, same sums.
+      // option exact_raises: the raises of the covers the walk skipped (factor 0)
+      if (p.exact_raises && !(err & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, qrad))
+        seterr(err, ERR_DOMAIN);
       const double area = total > 0 ? total : 0.0;
       if (area > 0) {
         const LightDev& L = S.light[li];
@@ -400,7 +407,10 @@ __global__ __launch_bounds__(256) void k_path_trace(KParams p) {
   it.depth = p.cam->depth;
   uint32_t err = 0;
   V3 sum = v3(0.0, 0.0, 0.0);
-  if (it.depth > 0 && !(vr(it.att) < 0.0001) && !highlights<false>(S, it, sum, err)) {
+  if (it.depth > 0 && !(vr(it.att) < 0.0001) &&
+      !highlights<false>(S, it, sum, err, [&](V3 T, V3 L, double rad) {
+        return lit_area_raises(S, nullptr, nullptr, nullptr, nullptr, 0, T, L, rad);   // (ordered linear walk)
+      })) {
     double best = S.max_distance, total = 0.0;
     int besti = -1;
     V3 hit = sum;
@@ -699,22 +709,30 @@ hipError_t launch_fit(const void* kern, int bs, size_t lds, int& cus, int& per_c
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  struct Ent {
+  struct Key {
     const void* k;
-    int bs;
+    int bs, dev;
     size_t lds;
-    int dev, cus, per_cu;
+    bool operator==(const Key& o) const { return k == o.k && bs == o.bs && dev == o.dev && lds == o.lds; }
+  };
+  struct KeyHash {
+    size_t operator()(const Key& x) const {
+      size_t h = std::hash<const void*>()(x.k);
+      h = h * 1000003u ^ std::hash<size_t>()(x.lds);
+      return h * 1000003u ^ (size_t)(x.bs * 64 + x.dev);
+    }
   };
   static std::mutex mu;
-  static std::vector<Ent> cache;
+  static std::unordered_map<Key, std::pair<int, int>, KeyHash> cache;   // -> (cus, per_cu)
+  const Key key{kern, bs, dev, lds};
   {
     std::lock_guard<std::mutex> g(mu);
-    for (const Ent& c : cache)
-      if (c.k == kern && c.bs == bs && c.lds == lds && c.dev == dev) {
-        cus = c.cus;
-        per_cu = c.per_cu;
-        return hipSuccess;
-      }
+    const auto it = cache.find(key);
+    if (it != cache.end()) {
+      cus = it->second.first;
+      per_cu = it->second.second;
+      return hipSuccess;
+    }
   }
   if (lds > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -722,7 +740,10 @@ hipError_t launch_fit(const void* kern, int bs, size_t lds, int& cus, int& per_c
   if (e != hipSuccess) return e;
   if (per_cu < 1) per_cu = 1;
   std::lock_guard<std::mutex> g(mu);
-  cache.push_back({kern, bs, lds, dev, cus, per_cu});
+  // the LDS size depends on the scene: a process that uploads very many scene
+  // sizes starts over rather than growing without bound
+  if (cache.size() >= 4096) cache.clear();
+  cache[key] = {cus, per_cu};
   return hipSuccess;
 }
 

@@ -106,6 +106,7 @@ struct KParams {
   int32_t lv_fin_tiles;            // tree reduction pass 0: tiles of the batch (grid-stride loop when the grid is smaller)
   int32_t lv_redo_blocks;          // the lanes-engine re-render of overflowed samples: at most this many workgroups (0: all resident)
   int32_t lv_ray_dbl;              // staged ray record, doubles: 10 (80 B: path < 2^32, RNG key decoded from the root) or 12
+  int32_t exact_raises;            // 1: every shadow walk (local_lights) also runs lit_area_raises (option exact_raises)
 };
 
 // Where the sphere walk reads its records:

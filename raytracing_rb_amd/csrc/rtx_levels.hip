@@ -598,7 +598,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
         leafp[3 * nleaf + 1] = c.y;
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
-      }, errA);
+      }, errA, [&](V3 T, V3 L, double rad) { return raises_walk<SPH, BS>(p, lds, T, L, rad); });
     RTX_LV_STAMP(0)
     // ---- World#intersect (world.rb:37-59)
     const bool ext = alive && !fired;
@@ -637,6 +637,8 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
       V3 h2 = qo;
       bool in2 = true;
       lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL);
+      if (p.exact_raises && !(errL & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, L.radius))
+        seterr(errL, ERR_DOMAIN);             // option exact_raises: covers the walk skipped (factor 0)
       const double area = tot > 0 ? tot : 0.0;
       if (area > 0) {
         nl++;
@@ -783,7 +785,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
           leafp[3 * nleaf + 1] = c.y;
           leafp[3 * nleaf + 2] = c.z;
           nleaf++;
-        }, errA);
+        }, errA, [&](V3 T, V3 L, double rad) { return raises_walk<SPH, BS>(p, lds, T, L, rad); });
       RTX_LV_STAMP(0)
       const bool ext = alive && !fired;
       double best = S.max_distance, total = 0.0;
@@ -908,6 +910,8 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       V3 h2 = qo;
       bool in2 = true;
       lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL);
+      if (p.exact_raises && !(errL & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, L.radius))
+        seterr(errL, ERR_DOMAIN);             // option exact_raises: covers the walk skipped (factor 0)
       const double area = tot > 0 ? tot : 0.0;
       if (area > 0) {
         nl++;
@@ -1014,7 +1018,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
         leafp[3 * nleaf + 1] = c.y;
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
-      }, errA);
+      }, errA, [&](V3 T, V3 L, double rad) { return raises_walk<SPH, BS>(p, lds, T, L, rad); });
     const bool ext = alive && !fired;
     double best = S.max_distance, total = 0.0;
     int besti = -1;
@@ -1074,6 +1078,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_shadow(KParams p, in
       bool in2 = true;
       uint32_t err = 0;
       lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, err);
+      if (p.exact_raises && !(err & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, L.radius)) seterr(err, ERR_DOMAIN);
       reinterpret_cast<double2*>(p.lv_area)[(size_t)hs * nL + li] =
           make_double2(tot, __builtin_bit_cast(double, (uint64_t)err));
     }

@@ -172,6 +172,11 @@ class PipelinedTiles:
         import torch
         j = self.i % self.F
         self.i += 1
+        # Buffer j may still be read by a started gather (always so with F = 1):
+        # finish gathers until none reads it, so its free event exists and the
+        # render below is ordered after the gather.
+        while any(jj == j for _, jj in self.pending):
+            self._finish_one()
         if self.free_ev[j] is not None:
             self.streams[j].wait_event(self.free_ev[j])
         self.rs[j].render_tiles_device(self.df.bufs[j].data_ptr(), self.tile_rows, self.rank, self.nranks,

@@ -673,3 +673,23 @@ def test_pre_sample_raise_before_extra_sample_raise(gpu, tmp_path):
             _renderer(sd, cd, engine, **opts).render(seed=chosen)
         assert e.value.kind == "domain", (engine, opts, str(e.value))
         assert "pixel (0,0)" in str(e.value)
+
+
+# ---- tree reduction as a grid-stride loop over the batch's tiles (option lv_fin_grid)
+@pytest.mark.parametrize("world,camera,ov", [
+    ("c2_world.yml", "c2_camera.yml", dict(width=320, height=181)),       # 920 tiles
+    ("mix_world.yml", "mix_camera.yml", dict(width=272, height=153, pre_sample_times=2, max_sample_times=5,
+                                             variant_threshold=0.0)),     # 680 tiles; extra samples: pass 1
+])
+def test_grid_stride_reduction_changes_no_bit(gpu, world, camera, ov):
+    """lv_fin_grid = k: k reduction blocks per CU loop over the tiles, reusing
+    their LDS column and raise slots between tiles.  With one
+    part (lv_streams 1) and k = 1 the grid (one block per CU) is smaller than
+    the tile count, so blocks take several tiles each."""
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=4)
+    for k in (1, 4):
+        for opts in (dict(), dict(lv_fin_cap=0), dict(lv_stage_pct=5, lv_floor=0)):
+            r = _renderer(sd, cd, 1, lv_fin_grid=k, lv_streams=1, **opts)
+            assert _same(r.render(seed=4), lanes), (k, opts)
+            r.close()
