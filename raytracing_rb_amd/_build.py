@@ -65,9 +65,13 @@ def source_sha(extra=()):
 def stale():
     if not os.path.exists(OUT):
         return True
-    # a diagnostic build (defines) written over the production library is stale
-    tag = os.path.join(ROOT, "build", "obj", os.path.basename(OUT), "flags")
+    # a diagnostic build (defines) written over the production library is stale,
+    # and so is one whose sources changed while it compiled (the identity it embeds)
+    odir = os.path.join(ROOT, "build", "obj", os.path.basename(OUT))
+    tag, ident = os.path.join(odir, "flags"), os.path.join(odir, "built_sha")
     if not os.path.exists(tag) or open(tag).read() != " ".join(FLAGS):
+        return True
+    if not os.path.exists(ident) or open(ident).read() != source_sha():
         return True
     t = os.path.getmtime(OUT)
     return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS + [__file__])
@@ -109,6 +113,8 @@ def build(force=False, verbose=False, out=None, defines=()):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    with open(os.path.join(odir, "built_sha"), "w") as f:
+        f.write(sha)
     return out
 
 

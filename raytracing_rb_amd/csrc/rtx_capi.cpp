@@ -88,6 +88,7 @@ struct rtx_context {
   int64_t opt_lv_redo_blocks = 8;    // bounce levels: workgroups of the overflow re-render launch (0: all resident)
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   int64_t opt_lv_ray_bytes = 0;      // bounce levels: staged ray record, 0 auto (80 B when every path fits 32 bits), 80, 96
+  int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
   int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also run the raise walk of the covers they skip
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
@@ -431,7 +432,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
       {"lv_redo_blocks", c->opt_lv_redo_blocks}, {"lv_fin_cap", c->opt_lv_fin_cap},
       {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
-      {"exact_raises", c->opt_exact_raises}};
+      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -518,6 +519,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_fin_cap")) {        // bounce levels: LDS tree records per tile in the reduction, 0 = off
     if (value < 0 || value > 4096) return fail(c, RTX_EINVAL, "lv_fin_cap must be in [0, 4096]");
     c->opt_lv_fin_cap = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_hl_cap")) {         // bounce levels: deferred highlight-check list entries, 0 auto
+    if (value < 0 || value > (1 << 26)) return fail(c, RTX_EINVAL, "lv_hl_cap must be in [0, 2^26]");
+    c->opt_lv_hl_cap = value;
     return RTX_OK;
   }
   if (!strcmp(key, "exact_raises")) {      // every shadow walk also checks the skipped covers' acos raises
@@ -930,6 +936,11 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   if (c->opt_lv_ray_bytes == 80 && !path32)
     return fail(c, RTX_EINVAL, "lv_ray_bytes 80: this camera's ray paths need 64 bits ((pt + 3)^trace_depth > 2^32)");
   const int rec_bytes = levels_rec_bytes(c->scene.n_light);
+  // deferred highlight checks (k_hl_raise): room for 1/256 of the batch's tree
+  // records (rays; C2 fires on ~0.1 % of them); a ray that finds the list full
+  // has its sample re-rendered by the lanes engine (option lv_hl_cap: the size)
+  const size_t hlcap = c->opt_lv_hl_cap > 0 ? (size_t)c->opt_lv_hl_cap : std::max<size_t>(4096, lcap / 256);
+  const size_t sz_hlq = al256(hlcap * 64);
   const size_t sz_ctl = al256(sizeof(LevelCtl)), sz_redo = al256(n0 * 4), sz_smp = al256(n0 * 32),
                sz_stage = al256(scap * RAY_BYTES), sz_rec = al256(lcap * (size_t)rec_bytes),
                sz_extra = al256((npx + 64) * 4);
@@ -946,7 +957,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // others' levels).  The extra-sample list and the statistics are shared
   // (appended / added atomically); each part has its own level buffers, its
   // own lanes-engine work counter and ray stacks for its overflow re-render.
-  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area;
+  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq;
   const size_t total = parts * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
@@ -960,7 +971,9 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_stage[1] = (double*)q;               q += sz_stage;
     k.lv_rec = q;                             q += sz_rec;
     k.lv_hit = split ? (double*)q : nullptr;  q += sz_hit;
-    k.lv_area = split ? (double*)q : nullptr;
+    k.lv_area = split ? (double*)q : nullptr; q += sz_area;
+    k.lv_hlq = (double*)q;
+    k.lv_hlq_cap = (uint32_t)hlcap;
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;

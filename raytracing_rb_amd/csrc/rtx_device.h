@@ -767,12 +767,25 @@ __device__ __forceinline__ void raise_sr(const RaiseAxis& a, float cx, float cy,
   rho = sqrtf(__builtin_fmaf(px, px, __builtin_fmaf(py, py, pz * pz)));
 }
 
+// (A) for child k of a node: the slab test of the box dilated by m S (§2.2)
+// along the whole line (both directions: no t >= 0, no far bound).
+template <typename NR>
+__device__ __forceinline__ bool slab_line(const NR& node, int k, const SlabRay& s) {
+  const F2 tx = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&node.lh[0][k][0]), s.pix, s.pax);
+  const F2 ty = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&node.lh[1][k][0]), s.piy, s.pay);
+  const F2 tz = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&node.lh[2][k][0]), s.piz, s.paz);
+  const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+  const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+  return tn <= tf;
+}
+
+// (B) for a box: its bounding ball (center, h >= the half diagonal) meets the
+// cone surface rho = k |s| (f = rho - k |s| takes both signs on the ball).
 __device__ __forceinline__ bool raise_box(const RaiseAxis& a, float lx, float hx, float ly, float hy, float lz, float hz) {
   float s, rho;
   raise_sr(a, 0.5f * (lx + hx), 0.5f * (ly + hy), 0.5f * (lz + hz), s, rho);
   const float h = 0.5f * ((hx - lx) + (hy - ly) + (hz - lz));   // >= the half diagonal
   const float as = fabsf(s);
-  if (rho - h <= a.mg) return true;                                        // (A)
   const float fmin = fmaxf(rho - h, 0.0f) - a.k * (as + h);
   const float fmax = rho + h - a.k * fmaxf(as - h, 0.0f);
   return fmin <= a.mg && fmax >= -a.mg;                                    // (B); NaN: false
@@ -802,8 +815,9 @@ __device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Nod
   a.k = (float)radius / ln;
   const float Sx = fabsf(a.tx) + fabsf(a.ty) + fabsf(a.tz) + S.sph_scale;
   a.mg = CULL_M * Sx * (1.0f + a.k);
+  const SlabRay sl = slab_setup(S, T, lt);
   const bool fin = __builtin_isfinite(a.ux) && __builtin_isfinite(a.uy) && __builtin_isfinite(a.uz) &&
-                   __builtin_isfinite(a.k) && __builtin_isfinite(a.mg) && ln > 0.0f;
+                   __builtin_isfinite(a.k) && __builtin_isfinite(a.mg) && ln > 0.0f && sl.fin;
   if (nodes == nullptr || S.bvh_root == BVH_NONE || !fin) {
     // every sphere in record order (the float32 filter only where it is valid)
     for (int i = 0; i < S.n_sphere; i++) {
@@ -823,8 +837,8 @@ __device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Nod
       for (int k = 0; k < 4; k++) {
         const int ch = nd.child[k];
         if (ch == BVH_NONE) continue;
-        if (raise_box(a, nd.lh[0][k][0], nd.lh[0][k][1], nd.lh[1][k][0], nd.lh[1][k][1], nd.lh[2][k][0],
-                      nd.lh[2][k][1]))
+        if (slab_line(nd, k, sl) || raise_box(a, nd.lh[0][k][0], nd.lh[0][k][1], nd.lh[1][k][0], nd.lh[1][k][1],
+                                              nd.lh[2][k][0], nd.lh[2][k][1]))
           stk[(sp++) * bs] = ch;
       }
     } else if (ref != BVH_NONE) {                // leaf

@@ -77,6 +77,38 @@ __device__ __forceinline__ void lv_redo(const KParams& p, int root) {
   }
 }
 
+// World#high_lights' lit_area (world.rb:92-93), deferred.  Its only effect is
+// a raise (Math.acos in Sphere#cover_area, lit_area_raises), and its walk,
+// run in the level kernel by the one lane whose ray fired while the wave's
+// other lanes wait, cost C2 2.8 % and C4 11 % (r07a).  So a level kernel only
+// appends a fired ray {o, d, record, root} to the batch's list (wave-
+// aggregated: one atomic per wave) and k_hl_raise re-runs the highlight loop
+// of every listed ray with the walk, full waves of them, after the batch's
+// levels, rewriting the raise byte of the ray's record.  A ray that finds the
+// list full sends its sample to the lanes engine (lv_redo), exact either way.
+// All lanes of the wave call it.
+constexpr int HLQ_DOUBLES = 8;
+template <typename RootFn>
+__device__ __forceinline__ void lv_hl_defer(const KParams& p, bool want, const Ray& r, uint32_t rec, RootFn&& root_fn) {
+  const uint64_t m = __ballot(want);
+  if (!m) return;
+  const int lane = (int)__lane_id(), first = __builtin_ctzll(m);
+  uint32_t b = 0;
+  if (lane == first) b = atomicAdd(&p.lv_ctl->hl_n, (uint32_t)__popcll(m));
+  b = (uint32_t)__builtin_amdgcn_readlane((int)b, first);
+  if (!want) return;
+  const uint32_t e = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  if (e >= p.lv_hlq_cap) {
+    lv_redo(p, root_fn());
+    return;
+  }
+  double2* q = reinterpret_cast<double2*>(p.lv_hlq + (size_t)e * HLQ_DOUBLES);
+  q[0] = make_double2(r.o.x, r.o.y);
+  q[1] = make_double2(r.o.z, r.d.x);
+  q[2] = make_double2(r.d.y, r.d.z);
+  q[3] = make_double2(__builtin_bit_cast(double, (uint64_t)rec), 0.0);
+}
+
 // root: the level-0 item of the ray's tree; (x, y, sample): its RNG key.
 __device__ __forceinline__ void lv_store_ray(const KParams& p, double* dst, const Ray& r, V3 att, uint64_t path,
                                              int root, int x, int y, int sample) {
@@ -591,14 +623,15 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
     // ---- rt_map: highlights (ray_tracer.rb:60-75)
     uint32_t errA = 0, errS = 0, errL = 0, errP = 0;
     int nleaf = 0;
-    bool fired = false;
+    bool fired = false, hl_defer = false;
     if (alive)
       fired = highlight_leaves(S, cur, [&](V3 c) {
         leafp[3 * nleaf] = c.x;
         leafp[3 * nleaf + 1] = c.y;
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
-      }, errA, [&](V3 T, V3 L, double rad) { return raises_walk<SPH, BS>(p, lds, T, L, rad); });
+      }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
+    lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return root; });
     RTX_LV_STAMP(0)
     // ---- World#intersect (world.rb:37-59)
     const bool ext = alive && !fired;
@@ -774,7 +807,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       double* leafp = reinterpret_cast<double*>(rec + 8);
       uint32_t errA = 0, errL = 0;
       int nleaf = 0;
-      bool fired = false;
+      bool fired = false, hl_defer = false;
       if (alive)
         fired = highlight_leaves_att(S, cur.ray, [&] {
           if (level == 0) return cur.att;
@@ -785,7 +818,8 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
           leafp[3 * nleaf + 1] = c.y;
           leafp[3 * nleaf + 2] = c.z;
           nleaf++;
-        }, errA, [&](V3 T, V3 L, double rad) { return raises_walk<SPH, BS>(p, lds, T, L, rad); });
+        }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
+      lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return level == 0 ? root : lv_ray_root(p, qs); });
       RTX_LV_STAMP(0)
       const bool ext = alive && !fired;
       double best = S.max_distance, total = 0.0;
@@ -1011,14 +1045,15 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
     double* leafp = reinterpret_cast<double*>(rec + 8);
     uint32_t errA = 0, errL = 0;
     int nleaf = 0;
-    bool fired = false;
+    bool fired = false, hl_defer = false;
     if (alive)
       fired = highlight_leaves(S, cur, [&](V3 c) {
         leafp[3 * nleaf] = c.x;
         leafp[3 * nleaf + 1] = c.y;
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
-      }, errA, [&](V3 T, V3 L, double rad) { return raises_walk<SPH, BS>(p, lds, T, L, rad); });
+      }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
+    lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return root; });
     const bool ext = alive && !fired;
     double best = S.max_distance, total = 0.0;
     int besti = -1;
@@ -1574,6 +1609,45 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
   if (err) record_error(p.err, err, px_key(x, y, cam.height, 1));
 }
 
+// The batch's deferred highlight rays (lv_hl_defer): each thread re-runs
+// World#high_lights for one listed ray, now with lit_area_raises for every
+// light that fires (in light order, after that light's own cos raise, as
+// rt_map meets them), and rewrites the raise byte of the ray's record.  The
+// walk reads the hierarchy from global memory (L2-resident) with its stack in
+// LDS (bvh_stack words per thread).  Grid-stride over the device-side count.
+__global__ __launch_bounds__(256) void k_hl_raise(KParams p) {
+  extern __shared__ int lds_hl[];
+  const SceneDev& S = p.scene;
+  const uint32_t n = p.lv_ctl->hl_n < p.lv_hlq_cap ? p.lv_ctl->hl_n : p.lv_hlq_cap;
+  const Bvh4Node* nodes = S.bvh_root != BVH_NONE ? S.bvh : nullptr;
+  int* stk = lds_hl + threadIdx.x;
+  for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+    const double2* q = reinterpret_cast<const double2*>(p.lv_hlq + (size_t)e * HLQ_DOUBLES);
+    const double2 a = q[0], b = q[1], c = q[2], d = q[3];
+    Ray r;
+    r.o = v3(a.x, a.y, b.x);
+    r.d = v3(b.y, c.x, c.y);
+    const uint32_t rec = (uint32_t)__builtin_bit_cast(uint64_t, d.x);
+    uint32_t err = 0;
+    highlight_leaves_att(S, r, [] { return v3(0.0, 0.0, 0.0); }, [](V3) {}, err, [&](V3 T, V3 L, double rad) {
+      return lit_area_raises(S, nodes, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, stk, 256, T, L,
+                             rad);
+    });
+    uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)rec * p.lv_rec_bytes);
+    *h = (*h & ~0xffu) | (err & 0xffu);
+  }
+}
+
+static hipError_t launch_hl_raise(const KParams& q, hipStream_t s) {
+  if (q.scene.n_light == 0 || !q.lv_hlq) return hipSuccess;
+  const size_t lds = (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
+  int cus = 0, per_cu = 0;
+  hipError_t e = launch_fit(reinterpret_cast<const void*>(k_hl_raise), 256, lds, cus, per_cu);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_hl_raise, dim3((unsigned)std::max(1, cus * std::min(per_cu, 4))), dim3(256), lds, s, q);
+  return hipGetLastError();
+}
+
 // Per batch: the control block (count0 = the batch's level-0 items, pass 1:
 // from the device-side extra count; the slice counters of levels 1..nlev),
 // the lanes engine's work counter (the re-render launch); the call's first
@@ -1595,6 +1669,7 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
     p.lv_ctl->count0 = v;
     p.lv_ctl->redo_n = 0;
     p.lv_ctl->dropped = 0;
+    p.lv_ctl->hl_n = 0;
     p.lv_ctl->lay_base[0] = 0;
     p.lv_ctl->lay_base[1] = v;
   }
@@ -1833,6 +1908,7 @@ static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_ma
       e = launch_level_mode(q, mode, 2, d, hits * q.scene.n_light, s, kev);
     if (e == hipSuccess) e = launch_shade(q, d, hits, s, kev);
   }
+  if (e == hipSuccess) e = launch_hl_raise(q, s);
   if (e == hipSuccess) e = launch_redo(q, mode, maxs, n0_max, s);
   if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
   return e;
