@@ -1161,6 +1161,9 @@ __device__ __forceinline__ Ray lens_ray(const CameraDev& c, V3 target, int x, in
 // (Math.acos, sphere.rb:45-46): `raises(T, L, radius)` answers whether it does
 // (lit_area_raises), asked only while the ray has no raise yet.
 // att_fn() gives the ray's attenuation, asked for only when a light fires.
+#ifndef RTX_EXACT_RAISES
+#define RTX_EXACT_RAISES 1   // 0: diagnostic builds only (option exact_raises compiled out of the walk kernels)
+#endif
 #ifndef RTX_HL_RAISES
 #define RTX_HL_RAISES 1      // 0: diagnostic builds only (timing without the highlight's lit_area raise walk)
 #endif

@@ -318,7 +318,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
       // World#local_lights (world.rb:72-80) fused with the light loop of
       // WorldObject#local_lighting (world_object.rb:51-74): same order, same sums.
       // option exact_raises: the raises of the covers the walk skipped (factor 0)
-      if (p.exact_raises && !(err & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, qrad))
+      if (RTX_EXACT_RAISES && p.exact_raises && !(err & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, qrad))
         seterr(err, ERR_DOMAIN);
       const double area = total > 0 ? total : 0.0;
       if (area > 0) {
