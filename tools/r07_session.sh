@@ -1,6 +1,7 @@
 # Round-4 GPU session: tests, smoke, variant A/B (tools/variants.py: every
-# library under _variants/), C2 bench, the FETCH_SIZE probe, C4 variants.
-#   bash tools/r07_session.sh TAG [exact]    (exact: also time option exact_raises on C2 / C4)
+# library under _variants/), C2 bench, single-frame kernel-trace summary,
+# C4 variants.     bash tools/r07_session.sh TAG [exact]
+#   (exact: also time option exact_raises on C2 / C4)
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1
@@ -9,7 +10,9 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
 timeout -k 10 300 python tools/variants.py time --scene c2 --rounds 3 --reps 7 > $OUT/variants_c2.log 2>&1 && \
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err && \
-timeout -k 5 -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch_probe -o fp --output-format csv -- tools/fetch_probe > $OUT/fetch_probe.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_single -o kt --output-format csv -- \
+    python3 bench.py --inflight 1 --option lv_streams=1 --steps 5 --warmup 2 --no-cpu-baseline --no-projection \
+    > $OUT/prof_single.json 2> $OUT/prof_single.err && \
 timeout -k 10 300 python tools/variants.py time --scene c4 --rounds 2 --reps 2 > $OUT/variants_c4.log 2>&1 && \
 { if [ "$2" = exact ]; then
     timeout -k 10 300 python3 tools/timing.py --scene c2 --reps 7 '{}' '{"exact_raises": 1}' > $OUT/timing_c2.log 2>&1 && \
