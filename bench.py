@@ -197,6 +197,9 @@ def main():
                          "rank: a 1-rank RCCL group (evidence that the C3 path runs on ROCm)")
     ap.add_argument("--tile-rows", type=int, default=TILE_ROWS,
                     help="rows per round-robin tile of a rank's share (default %d)" % TILE_ROWS)
+    ap.add_argument("--balance", choices=("rr", "lpt"), default="rr",
+                    help="multi-GPU tile split: rr = round-robin tiles; lpt = tile lists balanced by the rays each "
+                         "tile traced in one whole-frame render (rtx_tile_rays, longest processing time first)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # CPU test of the rank plumbing
     args = ap.parse_args()
     globals()["TILE_ROWS"] = args.tile_rows      # every share / gather of this run
@@ -246,7 +249,7 @@ def main():
 
     from raytracing_rb_amd import config, roofline
     from raytracing_rb_amd.runtime import Renderer
-    from raytracing_rb_amd.tiles import PipelinedTiles, rows_per_rank
+    from raytracing_rb_amd.tiles import PipelinedTiles, lpt_plan, row_tile_costs, rows_per_rank
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -331,8 +334,17 @@ def main():
         # gather overlaps frame i + 1's render (tiles.PipelinedTiles); drain()
         # finishes the last one before the timed region closes: all K frames
         # are rendered AND gathered inside it.
+        plan = None
+        if args.balance == "lpt":
+            # every rank renders the whole frame once (outside the timed region)
+            # and derives the same plan from the same ray counts
+            full0 = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+            rs[0].render_device(full0.data_ptr(), seed=1, stream=streams[0].cuda_stream)
+            torch.cuda.synchronize(dev)
+            plan = lpt_plan(row_tile_costs(rs[0].tile_rays(), TILE_ROWS), world)
+            del full0
         pipe = PipelinedTiles(rs, streams, W, H, TILE_ROWS, rank, world, dev, seed=1,
-                              force_collective=args.force_collective)
+                              force_collective=args.force_collective, plan=plan)
         df = pipe.df
         step, drain = pipe.step, pipe.drain
 
@@ -402,7 +414,7 @@ def main():
         elif world == 1:
             share_render(emulate[0], emulate[1], 0)
         else:
-            r.render_tiles_device(df.bufs[0].data_ptr(), TILE_ROWS, rank, world, seed=1, stream=streams[0].cuda_stream)
+            pipe.render_share(0, df.bufs[0])
         ms, kern_launches = r.kernel_time()
         kern_ms.append(ms)
     r.set_option("kernel_events", 0)
@@ -419,8 +431,7 @@ def main():
         rms_ = []
         for _ in range(3):
             ev[0].record(streams[0])
-            r.render_tiles_device(df.bufs[0].data_ptr(), TILE_ROWS, rank, world, seed=1,
-                                  stream=streams[0].cuda_stream)
+            pipe.render_share(0, df.bufs[0])
             ev[1].record(streams[0])
             ev[1].synchronize()
             rms_.append(ev[0].elapsed_time(ev[1]))
@@ -438,7 +449,7 @@ def main():
         dist.all_gather(allv, mine)
         rank_breakdown = {"render_ms": [round(float(v[0]), 4) for v in allv],
                           "gather_ms": [round(float(v[1]), 4) for v in allv],
-                          "packed_bytes_per_rank": int(rows_per_rank(H, TILE_ROWS, world) * W * 3 * 8),
+                          "packed_bytes_per_rank": int(df.rows * W * 3 * 8), "balance": args.balance,
                           "method": "one frame's share rendered alone on context 0 of each rank (HIP events on its "
                                     "stream, median of 3); the gather of one packed frame to rank 0 after a "
                                     "barrier (events around a blocking dist.gather on the current stream, median "
@@ -462,6 +473,14 @@ def main():
         REPS = 5
         warm(render_full)
         full_ms = float(np.median([timed(render_full, 4 * F) for _ in range(REPS)]))
+        tile_rays = rs[0].tile_rays()           # rays per 8x8 tile of context 0's last whole frame
+
+        def plan_render(tiles_k, j):
+            key = ("plan", len(tiles_k), j)
+            if key not in packed_for:
+                packed_for[key] = torch.empty((len(tiles_k) * TILE_ROWS, W, 3), dtype=torch.float64, device=dev)
+            rs[j].render_tile_list_device(packed_for[key].data_ptr(), tiles_k, TILE_ROWS, seed=1,
+                                          stream=streams[j].cuda_stream)
         projection = {"method": "each rank's share rendered alone on this GPU (rtx_render_tiles_device) with the "
                                 "bench's %d frame(s) in flight: every share warmed up once, then %d rounds that "
                                 "time every rank's share (%d frames each) in an order rotated by one rank per "
@@ -491,6 +510,28 @@ def main():
                 "gather_est_ms": round(gather_ms, 4),
                 "projected_speedup": round(full_ms / (mx + gather_ms), 3),
                 "projected_speedup_no_gather": round(full_ms / mx, 3)}
+            # the same with cost-balanced tile lists (--balance lpt): the rays
+            # per tile of the whole frame, longest processing time first
+            plan = lpt_plan(row_tile_costs(tile_rays, TILE_ROWS), n)
+            cost = row_tile_costs(tile_rays, TILE_ROWS)
+            fns = [lambda j, k=k: plan_render(plan[k], j) for k in range(n)]
+            for fn in fns:
+                warm(fn)
+            per = [[] for _ in range(n)]
+            for rep in range(REPS):
+                for q in range(n):
+                    k = (q + rep) % n
+                    per[k].append(timed(fns[k], 4 * F))
+            ls = [float(np.median(v)) for v in per]
+            lmx, lmed = max(ls), float(np.median(ls))
+            lgather = len(plan[0]) * TILE_ROWS * W * 3 * 8 / (XGMI_LINK_GBS * 1e9) * 1e3
+            projection["per_n"][str(n)]["lpt"] = {
+                "rank_ms": [round(v, 4) for v in ls], "max_rank_ms": round(lmx, 4),
+                "rank_spread": round((lmx - min(ls)) / lmed, 4),
+                "rank_rays": [int(sum(int(cost[t]) for t in l if t < len(cost))) for l in plan],
+                "gather_est_ms": round(lgather, 4),
+                "projected_speedup": round(full_ms / (lmx + lgather), 3),
+                "projected_speedup_no_gather": round(full_ms / lmx, 3)}
 
     if rank == 0:
         counts = r.count_work(seed=1)           # one counting launch, outside the timed region

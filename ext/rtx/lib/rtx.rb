@@ -69,6 +69,8 @@ module RTX
   extern 'int rtx_tiles_rows_per_rank(int, int, int)'
   extern 'int rtx_render_tiles_device(void*, int, int, int, unsigned long long, void*, void*)'
   extern 'int rtx_render_tiles(void*, int, int, int, unsigned long long, void*)'
+  extern 'int rtx_render_tile_list_device(void*, void*, int, int, unsigned long long, void*, void*)'
+  extern 'int rtx_tile_rays(void*, void*, int)'
   extern 'int rtx_render_multi(void*, int, int, unsigned long long, void*, size_t)'
   extern 'int rtx_device_count()'
   extern 'int rtx_sync(void*, void*)'

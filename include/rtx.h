@@ -185,6 +185,22 @@ int32_t    rtx_tiles_rows_per_rank(int32_t height, int32_t tile_rows, int32_t nr
 rtx_status rtx_render_tiles_device(rtx_context* ctx, int32_t tile_rows, int32_t rank, int32_t nranks,
                                    uint64_t seed, double* d_packed, void* hip_stream);
 
+/* One rank's share given as an explicit list of `tile_rows`-row tiles (a
+ * cost-balanced split of camera.rb:53-65's bands, e.g. longest-processing-time
+ * over rtx_tile_rays): tiles[k] (host array, n entries; an index past the
+ * image bottom is padding) is stored at rows [k*tile_rows, (k+1)*tile_rows)
+ * of d_packed.  The list is copied to the device when it differs from the
+ * previous call's.  Same bits as any other split. */
+rtx_status rtx_render_tile_list_device(rtx_context* ctx, const int32_t* tiles, int32_t n, int32_t tile_rows,
+                                       uint64_t seed, double* d_packed, void* hip_stream);
+
+/* Rays traced per 8x8 tile (the tree records of its 64 x pre_sample_times
+ * camera samples' trees; extra samples not counted) in the last whole-frame
+ * render of this context with the bounce-level engine, row-major over the
+ * frame's ceil(width/8) x ceil(height/8) tiles: a measured work map for
+ * balancing tile splits.  Synchronous; zeros before such a render. */
+rtx_status rtx_tile_rays(rtx_context* ctx, int64_t* out, int32_t n);
+
 /* Host-buffer variant of rtx_render_tiles_device (synchronous): packed holds
  * rtx_tiles_rows_per_rank() * width * 3 doubles.  One call per worker of
  * Camera#render_fork (camera.rb:41-68) in a single-process, multi-GPU host. */

@@ -85,6 +85,8 @@ SIGNATURES = [
     ("rtx_tiles_rows_per_rank", _I, [_I, _I, _I]),
     ("rtx_render_tiles_device", _I, [_P, _I, _I, _I, _U64, _P, _P]),
     ("rtx_render_tiles", _I, [_P, _I, _I, _I, _U64, _DP]),
+    ("rtx_render_tile_list_device", _I, [_P, C.POINTER(C.c_int32), _I, _I, _U64, _P, _P]),
+    ("rtx_tile_rays", _I, [_P, C.POINTER(C.c_int64), _I]),
     ("rtx_render_multi", _I, [C.POINTER(_P), _I, _I, _U64, _DP, _SZ]),
     ("rtx_device_count", _I, []),
     ("rtx_sync", _I, [_P, _P]),

@@ -91,6 +91,11 @@ struct rtx_context {
   int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
   int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also run the raise walk of the covers they skip
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
+  uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
+  size_t tile_rays_n = 0;
+  int32_t* d_rowtiles = nullptr;     // rtx_render_tile_list_device: the tile list on the device
+  std::vector<int32_t> rowtiles;     // ... and the list it holds
+  size_t rowtiles_cap = 0;
   int64_t opt_kernel_events = 0;     // 1: HIP events around the ray-tree kernel launches (rtx_kernel_time)
   bool err_keys_rays = false;        // the device error keys of the last launch are ray indices (rtx_trace)
   // rtx_render_multi: this context's packed tiles; on the call's first context
@@ -397,6 +402,8 @@ void rtx_context_destroy(rtx_context* c) {
     if (ev) (void)hipEventDestroy(ev);
   hipFree(c->d_work);
   hipFree(c->d_lvstats);
+  hipFree(c->d_tile_rays);
+  hipFree(c->d_rowtiles);
   hipFree(c->d_multi);
   hipFree(c->d_gather);
   for (size_t k = 0; k < c->comms.size(); k++) {
@@ -418,7 +425,7 @@ static bool levels_engine(const rtx_context* c);
 // lv_ray_bytes 80 asked for a camera whose fields do not fit is refused, not
 // truncated.
 struct LvGeom {
-  size_t n0, G, ngrp, capg, lcap;
+  size_t n0, G, ngrp, capg, spill, lcap;
   int pb, rb, cb;
   bool small;
 };
@@ -432,13 +439,15 @@ static LvGeom lv_geom(const rtx_context* c, size_t n0) {
   g.n0 = n0;
   g.G = (size_t)64 * std::max(1, c->cam.pre);
   g.ngrp = (n0 + g.G - 1) / g.G;
-  // per group: lv_rec_pct % of its items (auto: 3200 %, from depth 6 6400 %: a
-  // tile of glass spheres makes up to 2^depth - 1 rays per sample), and at
-  // least the floor's 4 x lv_floor records spread over the groups
-  const int64_t pct = c->opt_lv_rec_pct > 0 ? c->opt_lv_rec_pct : (c->cam.depth <= 5 ? 3200 : 6400);
+  // per group: lv_rec_pct % of its items (auto 1600 %, 3200 % from depth 6:
+  // C2 averages 3.6 rays per sample, C4 9.6), and at least the floor's 4 x lv_floor records spread over the
+  // groups; a full region's children take records of the spill arena (8 per
+  // item: a tile of glass spheres makes up to (pt + 2)^depth rays per sample)
+  const int64_t pct = c->opt_lv_rec_pct > 0 ? c->opt_lv_rec_pct : (c->cam.depth <= 5 ? 1600 : 3200);
   const size_t fl = (size_t)c->opt_lv_floor;
   g.capg = std::max<size_t>({g.G + 1, g.G * (size_t)pct / 100, (4 * fl + g.ngrp - 1) / g.ngrp});
-  g.lcap = g.ngrp * g.capg;
+  g.spill = c->opt_lv_rec_pct > 0 ? 0 : std::max<size_t>(fl, 8 * n0);   // (lv_rec_pct set: no spill, tests force overflow)
+  g.lcap = g.ngrp * g.capg + g.spill;
   uint64_t v = 1;
   bool p32 = true;
   for (int l = 0; l < c->cam.depth && p32; l++) {
@@ -447,7 +456,7 @@ static LvGeom lv_geom(const rtx_context* c, size_t n0) {
   }
   g.pb = p32 ? std::max(1, bitlen(v - 1)) : 64;
   g.rb = std::max(1, bitlen(n0 > 0 ? n0 - 1 : 0));
-  g.cb = bitlen(g.capg);
+  g.cb = bitlen(g.lcap);                        // the record index (all ones: none)
   g.small = c->opt_lv_ray_bytes != 96 && p32 && g.pb + g.rb + g.cb <= 64;
   return g;
 }
@@ -1048,6 +1057,8 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_ray_dbl = geo.small ? 10 : 12;
   p.lv_grp_items = (uint32_t)geo.G;
   p.lv_grp_cap = (uint32_t)geo.capg;
+  p.lv_spill0 = (uint32_t)(geo.ngrp * geo.capg);
+  p.lv_spill_cap = (uint32_t)geo.spill;
   p.lv_tail_pb = geo.pb;
   p.lv_tail_rb = geo.rb;
   p.lv_last_level = c->cam.depth >= 1 ? c->cam.depth - 1 : -1;
@@ -1156,6 +1167,73 @@ rtx_status rtx_render_device(rtx_context* c, int32_t x0, int32_t y0, int32_t x1,
   p.nrows = y1 - y0;
   p.out = d_out;
   p.stride = row_stride;
+  if (x0 == 0 && y0 == 0 && x1 == c->cam.width && y1 == c->cam.height && levels_engine(c)) {
+    // the whole frame: the reduction records rays per 8x8 tile (rtx_tile_rays)
+    const size_t nt = (size_t)((x1 + 7) / 8) * ((y1 + 7) / 8);
+    if (nt > c->tile_rays_n) {
+      hipFree(c->d_tile_rays);
+      c->d_tile_rays = nullptr;
+      c->tile_rays_n = 0;
+      HIPCHK(c, hipMalloc(&c->d_tile_rays, nt * sizeof(uint32_t)));
+      HIPCHK(c, hipMemset(c->d_tile_rays, 0, nt * sizeof(uint32_t)));
+      c->tile_rays_n = nt;
+    }
+    p.tile_rays = c->d_tile_rays;
+  }
+  return render_region(c, p, false, maxs, (hipStream_t)stream);
+}
+
+rtx_status rtx_tile_rays(rtx_context* c, int64_t* out, int32_t n) {
+  if (!c || (!out && n > 0) || n < 0) return fail(c, RTX_EINVAL, "bad arguments");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint32_t> v(c->tile_rays_n);
+  if (c->d_tile_rays) {
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(v.data(), c->d_tile_rays, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  for (int k = 0; k < n; k++) out[k] = (size_t)k < v.size() ? (int64_t)v[k] : 0;
+  return RTX_OK;
+}
+
+rtx_status rtx_render_tile_list_device(rtx_context* c, const int32_t* tiles, int32_t n, int32_t tile_rows,
+                                       uint64_t seed, double* d_packed, void* stream) {
+  if (!c) return RTX_EINVAL;
+  if (n < 0 || (n > 0 && (!tiles || !d_packed)) || tile_rows <= 0) return fail(c, RTX_EINVAL, "bad tile list");
+  KParams p;
+  rtx_status s = prep(c, p, seed);
+  if (s) return s;
+  if (n == 0) return RTX_OK;
+  const int ntiles = (c->cam.height + tile_rows - 1) / tile_rows;
+  for (int k = 0; k < n; k++)
+    if (tiles[k] < 0) return fail(c, RTX_EINVAL, "tile %d: negative index %d", k, tiles[k]);
+  const int maxs = required_stack(c);
+  if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
+  if ((s = ensure_stack(c, p, maxs))) return s;
+  hipSetDevice(c->device);
+  if (c->rowtiles.size() != (size_t)n || !std::equal(c->rowtiles.begin(), c->rowtiles.end(), tiles)) {
+    if ((size_t)n > c->rowtiles_cap) {
+      hipFree(c->d_rowtiles);
+      c->d_rowtiles = nullptr;
+      c->rowtiles_cap = 0;
+      HIPCHK(c, hipMalloc(&c->d_rowtiles, (size_t)n * sizeof(int32_t)));
+      c->rowtiles_cap = (size_t)n;
+    }
+    c->rowtiles.assign(tiles, tiles + n);
+    // ordered before this call's launches on `stream` (a caller that changes
+    // the list while another stream's render still reads it must sync first)
+    HIPCHK(c, hipMemcpyAsync(c->d_rowtiles, c->rowtiles.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice,
+                             (hipStream_t)stream));
+  }
+  (void)ntiles;
+  p.x0 = 0;
+  p.nx = c->cam.width;
+  p.nrows = n * tile_rows;
+  p.tile_rows = tile_rows;
+  p.rank = 0;
+  p.nranks = 1;
+  p.row_tiles = c->d_rowtiles;
+  p.out = d_packed;
+  p.stride = (size_t)c->cam.width * 3;
   return render_region(c, p, false, maxs, (hipStream_t)stream);
 }
 

@@ -1248,7 +1248,8 @@ __device__ __forceinline__ unsigned long long px_key(int x, int y, int H, int ph
 __device__ __forceinline__ int row_to_y(const KParams& p, int row) {
   if (p.tile_rows == 0) return p.y0 + row;
   const int k = row / p.tile_rows;
-  return (k * p.nranks + p.rank) * p.tile_rows + (row - k * p.tile_rows);
+  const int t = p.row_tiles ? p.row_tiles[k] : k * p.nranks + p.rank;
+  return t * p.tile_rows + (row - k * p.tile_rows);
 }
 
 // Level-0 item k of a bounce-level batch (KParams lv_*): pass 0, the pre

@@ -30,7 +30,8 @@ struct LevelCtl {
   uint32_t dropped;                             // child rays that found no room (diagnostic)
   uint32_t hl_n;                                // highlight rays whose lit_area raise check is deferred (k_hl_raise)
   uint32_t xr_n;                                // shading hits whose covers' raise check is deferred (exact_raises)
-  uint32_t pad[27];                             // (pad[0]: the lanes-engine work counter of parts 1..)
+  uint32_t spill_n;                             // tree records taken from the spill arena (full group regions)
+  uint32_t pad[26];                             // (pad[0]: the lanes-engine work counter of parts 1..)
   uint32_t sc[LV_MAXL + 1][LV_SLICES * 32];     // rays allocated in slice s of level d: sc[d][32 s]
   uint32_t sh[LV_MAXL + 1][LV_SLICES * 32];     // split phases: hits of level d in slice s
   uint32_t claim[3][LV_MAXL + 1][LV_CLAIMS * 32]; // chunk claims: [launch kind: fused/trace, shadow, shade][level][j * 32]
@@ -49,6 +50,8 @@ struct KParams {
   uint64_t seed;
   int32_t x0, nx, nrows;           // columns [x0, x0+nx); packed output rows
   int32_t y0, tile_rows, rank, nranks;   // tile_rows == 0: rows y0 .. y0+nrows-1
+  const int32_t* row_tiles;        // non-null: packed tile k is image tile row_tiles[k] (rtx_render_tile_list_device)
+  uint32_t* tile_rays;             // non-null (whole-frame level renders): rays per 8x8 tile, written by the reduction
   double* out;
   size_t stride;                   // doubles per output row
   ErrState* err;
@@ -95,7 +98,8 @@ struct KParams {
   // tile's trees are one contiguous run the reduction streams.
   uint32_t* lv_grp;
   uint32_t lv_grp_items, lv_grp_cap;
-  int32_t lv_tail_pb, lv_tail_rb;  // 80-B ray record: bits of path and root in its tail word (the rest: record in group)
+  uint32_t lv_spill0, lv_spill_cap;  // a full region's children take records lv_spill0 + k, k < lv_spill_cap
+  int32_t lv_tail_pb, lv_tail_rb;  // 80-B ray record: bits of path and root in its tail word (the rest: the record)
   LevelCtl* lv_ctl;
   double* lv_stage[2];             // level d reads lv_stage[d & 1], writes lv_stage[(d + 1) & 1]
   char* lv_rec;

@@ -46,7 +46,8 @@ namespace rtx {
 // Capacity.  Children beyond their slice or tree records beyond their
 // group's region are not written; their camera sample is listed
 // (lv_redo_list) and re-rendered whole by the lanes engine (SRC_LIST), exact
-// either way.
+// either way.  A group region that fills up hands its children records of a
+// shared spill arena first (lv_spill0 + k).
 //
 // Tree records by group.  The records of the trees of one
 // pass-0 tile (its 64 x pre level-0 items, a group) live in one region of
@@ -57,7 +58,7 @@ namespace rtx {
 //
 // Staging ray record (p.lv_ray_dbl doubles per slot): o, d, att, then
 //   12 (96 B): {path}, {root item | record << 32, unused};
-//   10 (80 B): one tail word {path | root << pb | record in group << (pb + rb)}
+//   10 (80 B): one tail word {path | root << pb | record << (pb + rb)}
 //   (pb = lv_tail_pb, rb = lv_tail_rb: the host picks it when the three fit).
 // The RNG key (x, y, sample), needed only by the path-tracing children of a
 // level >= 1 ray, is decoded from the root (lv_ray_key).  A record index of
@@ -121,10 +122,7 @@ __device__ __forceinline__ void lv_hl_defer(const KParams& p, bool want, const R
   q[3] = make_double2(__builtin_bit_cast(double, (uint64_t)rec), 0.0);
 }
 
-// The group region of level-0 item `root` and the level-0 record of an item.
-__device__ __forceinline__ uint32_t lv_grp_base(const KParams& p, uint32_t root) {
-  return (root / p.lv_grp_items) * p.lv_grp_cap;
-}
+// The level-0 record of an item (the head of its group's region).
 __device__ __forceinline__ uint32_t lv_rec0(const KParams& p, uint32_t item) {
   const uint32_t g = item / p.lv_grp_items;
   return g * p.lv_grp_cap + (item - g * p.lv_grp_items);
@@ -140,8 +138,8 @@ __device__ __forceinline__ void lv_store_ray(const KParams& p, double* dst, cons
   q[3] = make_double2(att.x, att.y);
   if (p.lv_ray_dbl == RAY_DOUBLES_SMALL) {
     const uint32_t sh = (uint32_t)(p.lv_tail_pb + p.lv_tail_rb);
-    const uint64_t loc = rec == LV_NOREC ? ~0ull : (uint64_t)(rec - lv_grp_base(p, (uint32_t)root));
-    const uint64_t w = path | (uint64_t)(uint32_t)root << p.lv_tail_pb | loc << sh;
+    const uint64_t r64 = rec == LV_NOREC ? ~0ull : (uint64_t)rec;
+    const uint64_t w = path | (uint64_t)(uint32_t)root << p.lv_tail_pb | r64 << sh;
     q[4] = make_double2(att.z, __builtin_bit_cast(double, w));
     return;
   }
@@ -154,8 +152,8 @@ __device__ __forceinline__ void lv_tail_small(const KParams& p, uint64_t w, uint
   const uint32_t pb = (uint32_t)p.lv_tail_pb, rb = (uint32_t)p.lv_tail_rb;
   path = w & ((1ull << pb) - 1ull);
   root = (int)((w >> pb) & ((1ull << rb) - 1ull));
-  const uint64_t loc = w >> (pb + rb);
-  rec = loc == (~0ull >> (pb + rb)) ? LV_NOREC : lv_grp_base(p, (uint32_t)root) + (uint32_t)loc;
+  const uint64_t r64 = w >> (pb + rb);
+  rec = r64 == (~0ull >> (pb + rb)) ? LV_NOREC : (uint32_t)r64;
 }
 
 // A staged ray's path, root item and record from the record's last 16-B
@@ -596,9 +594,14 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
     if (nch > 0) {
       if (goff + (uint32_t)nch <= p.lv_grp_cap) {
         child0 = (uint32_t)root / p.lv_grp_items * p.lv_grp_cap + goff;
-      } else {                                // the group's region is full: re-render the sample
-        child0 = LV_NOREC;
-        lv_redo(p, root);
+      } else {                                // the group's region is full: the spill arena (rare)
+        const uint32_t s0 = atomicAdd(&p.lv_ctl->spill_n, (uint32_t)nch);
+        if (s0 + (uint32_t)nch <= p.lv_spill_cap) {
+          child0 = p.lv_spill0 + s0;
+        } else {                              // that too: re-render the sample
+          child0 = LV_NOREC;
+          lv_redo(p, root);
+        }
       }
     }
   }
@@ -1452,6 +1455,7 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
     const int item0 = slot * n_items;
     const uint32_t g0 = (uint32_t)slot * p.lv_grp_cap;           // the tile's group region
     const uint32_t used = min(p.lv_grp[slot], p.lv_grp_cap);
+    if (p.tile_rays && threadIdx.x == 0) p.tile_rays[p.lv_t0 + slot * p.lv_tstride] = used;   // (rtx_tile_rays)
     const bool staged = (int)used <= p.lv_fin_cap;               // uniform
     if (staged) {
       const unsigned long long tc0 = RTX_STAMPS ? stamp() : 0ull;
@@ -1475,8 +1479,10 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
       if (!ip.valid) continue;
       uint32_t e = 0;
       V3 c;
-      if (staged) {
-        auto at = [&](uint32_t i) { return (const char*)lrec + (size_t)(i - g0) * rb; };
+      if (staged) {                           // (a record in the spill arena is read where it is)
+        auto at = [&](uint32_t i) {
+          return i - g0 < used ? (const char*)lrec + (size_t)(i - g0) * rb : (const char*)p.lv_rec + (size_t)i * rb;
+        };
         c = SD > 16 ? lv_sample<false>(p, at, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
                     : lv_sample<false>(p, at, item0 + it, nlev, lo, hi, 256, SD, e);
       } else {
@@ -1622,6 +1628,7 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
     p.lv_ctl->dropped = 0;
     p.lv_ctl->hl_n = 0;
     p.lv_ctl->xr_n = 0;
+    p.lv_ctl->spill_n = 0;
     p.lv_ctl->lay_base[0] = 0;
     p.lv_ctl->lay_base[1] = v;
   }

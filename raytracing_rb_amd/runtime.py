@@ -124,6 +124,21 @@ class Renderer:
         self._check(self.lib.rtx_render_tiles_device(self.h, tile_rows, rank, nranks, seed, C.c_void_p(d_packed),
                                                      C.c_void_p(stream or 0)))
 
+    def render_tile_list_device(self, d_packed, tiles, tile_rows, seed=1, stream=None):
+        """The tile_rows-row tiles `tiles` (image tile indices; past the bottom: padding)
+        into packed rows k * tile_rows (rtx_render_tile_list_device)."""
+        t = np.ascontiguousarray(tiles, np.int32)
+        self._check(self.lib.rtx_render_tile_list_device(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), len(t),
+                                                         tile_rows, seed, C.c_void_p(d_packed),
+                                                         C.c_void_p(stream or 0)))
+
+    def tile_rays(self):
+        """Rays per 8x8 tile [ceil(H/8), ceil(W/8)] of the last whole-frame level render (rtx_tile_rays)."""
+        ty, tx = (self.height + 7) // 8, (self.width + 7) // 8
+        out = np.zeros(ty * tx, np.int64)
+        self._check(self.lib.rtx_tile_rays(self.h, out.ctypes.data_as(C.POINTER(C.c_int64)), len(out)))
+        return out.reshape(ty, tx)
+
     def get_option(self, key):
         v = C.c_int64()
         self._check(self.lib.rtx_get_option(self.h, key.encode(), C.byref(v)))

@@ -43,6 +43,51 @@ def unpack_index(height, tile_rows, nranks):
     return np.concatenate(src), np.concatenate(dst)
 
 
+def row_tile_costs(tile_rays, tile_rows):
+    """Per tile_rows-row tile: the rays of its 8x8 tiles (Renderer.tile_rays(),
+    [ceil(H/8), ceil(W/8)]); tile_rows must be a multiple of 8."""
+    if tile_rows % 8:
+        raise ValueError("cost-balanced tiles need tile_rows a multiple of 8")
+    m = tile_rows // 8
+    per_band = np.asarray(tile_rays, np.int64).sum(axis=1)
+    n = (len(per_band) + m - 1) // m
+    return np.array([per_band[k * m:(k + 1) * m].sum() for k in range(n)], np.int64)
+
+
+def lpt_plan(costs, nranks):
+    """Longest-processing-time split of tiles over ranks: tiles by decreasing
+    cost (ties: lower index first), each to the rank with the least total so
+    far (ties: lower rank).  Deterministic, so every rank computes the same
+    plan from the same costs.  Returns nranks lists of tile indices (each
+    ascending), padded to one length with len(costs) (past the bottom)."""
+    costs = np.asarray(costs, np.int64)
+    n = len(costs)
+    order = sorted(range(n), key=lambda t: (-int(costs[t]), t))
+    load = [0] * nranks
+    lists = [[] for _ in range(nranks)]
+    for t in order:
+        r = min(range(nranks), key=lambda k: (load[k], len(lists[k]), k))
+        lists[r].append(t)
+        load[r] += int(costs[t])
+    width = max(len(l) for l in lists)
+    return [sorted(l) + [n] * (width - len(l)) for l in lists]
+
+
+def plan_unpack_index(plan, height, tile_rows):
+    """(source row, image row) pairs of the rank-major concatenation of the packed
+    buffers of a tile-list plan (rows_per_rank = len(plan[0]) * tile_rows)."""
+    n = len(plan[0]) * tile_rows
+    src, dst = [], []
+    for r, tiles in enumerate(plan):
+        for k, t in enumerate(tiles):
+            for j in range(tile_rows):
+                y = t * tile_rows + j
+                if y < height:
+                    src.append(r * n + k * tile_rows + j)
+                    dst.append(y)
+    return np.array(src, np.int64), np.array(dst, np.int64)
+
+
 def unpack(gathered, height, tile_rows, nranks):
     """gathered: [nranks * rows_per_rank, W, 3] (numpy or torch) -> frame [H, W, 3]."""
     src, dst = unpack_index(height, tile_rows, nranks)
@@ -75,14 +120,16 @@ class DistributedFrame:
     the gather of frame i + 1 is issued (a collective waits for the stream it
     is issued from), so the single receive buffer is never overwritten early."""
 
-    def __init__(self, width, height, tile_rows, rank, nranks, device, buffers=1, force_collective=False):
+    def __init__(self, width, height, tile_rows, rank, nranks, device, buffers=1, force_collective=False, plan=None):
         import torch
         self.width, self.height = width, height
         self.tile_rows, self.rank, self.nranks = tile_rows, rank, nranks
+        # plan: per-rank tile lists (lpt_plan) instead of round-robin tiles
+        self.plan = plan
         # force_collective: issue the gather even with one rank (the GPU test of
         # the multi-rank path runs it under a 1-rank RCCL group)
         self.collective = nranks > 1 or force_collective
-        self.rows = rows_per_rank(height, tile_rows, nranks)
+        self.rows = len(plan[0]) * tile_rows if plan else rows_per_rank(height, tile_rows, nranks)
         self.bufs = [torch.zeros((self.rows, width, 3), dtype=torch.float64, device=device)
                      for _ in range(max(1, buffers))]
         self._i = 0
@@ -90,7 +137,7 @@ class DistributedFrame:
         self.gathered = None
         if rank == 0:
             self.gathered = torch.zeros((nranks * self.rows, width, 3), dtype=torch.float64, device=device)
-            src, dst = unpack_index(height, tile_rows, nranks)
+            src, dst = plan_unpack_index(plan, height, tile_rows) if plan else unpack_index(height, tile_rows, nranks)
             self.src = torch.as_tensor(src, device=device)
             self.dst = torch.as_tensor(dst, device=device)
             self.frame = torch.zeros((height, width, 3), dtype=torch.float64, device=device)
@@ -142,15 +189,16 @@ class PipelinedTiles:
     callback with frame i (the DistributedFrame's frame tensor, reused)."""
 
     def __init__(self, renderers, streams, width, height, tile_rows, rank, nranks, device, seed=1,
-                 force_collective=False, on_frame=None):
+                 force_collective=False, on_frame=None, plan=None):
         import torch
         self.rs, self.streams = renderers, streams
         self.F = len(renderers)
         assert len(streams) == self.F
         self.tile_rows, self.rank, self.nranks, self.seed = tile_rows, rank, nranks, seed
+        self.plan = plan
         self.stream = torch.cuda.current_stream(device)
         self.df = DistributedFrame(width, height, tile_rows, rank, nranks, device, buffers=self.F,
-                                   force_collective=force_collective)
+                                   force_collective=force_collective, plan=plan)
         self.pending = []
         self.free_ev = [None] * self.F
         self.on_frame = on_frame
@@ -179,14 +227,23 @@ class PipelinedTiles:
             self._finish_one()
         if self.free_ev[j] is not None:
             self.streams[j].wait_event(self.free_ev[j])
-        self.rs[j].render_tiles_device(self.df.bufs[j].data_ptr(), self.tile_rows, self.rank, self.nranks,
-                                       seed=self.seed, stream=self.streams[j].cuda_stream)
+        self.render_share(j)
         done = torch.cuda.Event()
         done.record(self.streams[j])
         while self.pending:
             self._finish_one()
         self.stream.wait_event(done)
         self.pending.append((self.df.gather_start(self.df.bufs[j]), j))
+
+    def render_share(self, j, buf=None):
+        """This rank's share of one frame into packed buffer j (or `buf`) on stream j."""
+        ptr = (self.df.bufs[j] if buf is None else buf).data_ptr()
+        if self.plan:
+            self.rs[j].render_tile_list_device(ptr, self.plan[self.rank], self.tile_rows, seed=self.seed,
+                                               stream=self.streams[j].cuda_stream)
+        else:
+            self.rs[j].render_tiles_device(ptr, self.tile_rows, self.rank, self.nranks, seed=self.seed,
+                                           stream=self.streams[j].cuda_stream)
 
     def drain(self):
         while self.pending:

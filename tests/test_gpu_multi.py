@@ -95,3 +95,44 @@ def test_bench_force_collective_one_rank():
     assert 0.0 < rb["render_ms"][0] < 100.0 and 0.0 <= rb["gather_ms"][0] < 100.0, rb
     assert line["n_gpus"] == 1 and "RCCL" in line["config"]["parallelism"]
     assert line["value"] > 0
+
+
+def test_lpt_tile_lists_reassemble_bit_exactly(gpu):
+    """rtx_tile_rays after a whole-frame render -> lpt_plan for 3 and 8 ranks;
+    every rank's tile list rendered with rtx_render_tile_list_device and
+    unpacked by the plan equals the whole frame bit for bit."""
+    import torch
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import Renderer
+    from raytracing_rb_amd.tiles import lpt_plan, plan_unpack_index, row_tile_costs
+    sd, cd = config.load_scene(os.path.join(SCENES, "c2_world.yml"), os.path.join(SCENES, "c2_camera.yml"),
+                               camera_overrides={"width": 320, "height": 181})
+    r = Renderer(sd, cd, device=0)
+    full = r.render(seed=1)
+    rays = r.tile_rays()
+    assert rays.shape == (23, 40) and rays.min() >= 256    # at least each tile's level-0 records
+    for n in (3, 8):
+        plan = lpt_plan(row_tile_costs(rays, 8), n)
+        rows = len(plan[0]) * 8
+        packed = torch.zeros((n * rows, cd.width, 3), dtype=torch.float64, device="cuda")
+        for k in range(n):
+            r.render_tile_list_device(packed[k * rows:(k + 1) * rows].data_ptr(), plan[k], 8, seed=1)
+        torch.cuda.synchronize()
+        r.sync()
+        src, dst = plan_unpack_index(plan, cd.height, 8)
+        frame = np.zeros_like(full)
+        frame[dst] = packed.cpu().numpy()[src]
+        assert np.array_equal(frame.view(np.uint64), full.view(np.uint64)), n
+    r.close()
+
+
+def test_bench_force_collective_lpt_plan():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-collective", "--balance", "lpt",
+                          "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-projection"],
+                         capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["gather_check"] == "bit-identical" and line["ranks"]["balance"] == "lpt"

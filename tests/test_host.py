@@ -264,6 +264,68 @@ def test_distributed_gather_gloo_world2():
     assert np.array_equal(frame, ref)
 
 
+# ------------------------------------------------------------------ cost-balanced tile lists
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_lpt_plan_covers_every_tile_once_and_balances(n):
+    costs = np.random.default_rng(n).integers(1, 1000, 135)
+    plan = tiles.lpt_plan(costs, n)
+    assert len(plan) == n and len({len(l) for l in plan}) == 1
+    real = sorted(t for l in plan for t in l if t < len(costs))
+    assert real == list(range(len(costs)))
+    loads = [sum(int(costs[t]) for t in l if t < len(costs)) for l in plan]
+    # LPT: no rank exceeds the mean by more than the largest single tile
+    assert max(loads) <= sum(loads) / n + costs.max()
+    assert plan == tiles.lpt_plan(costs, n)      # deterministic: every rank computes the same plan
+
+
+def test_row_tile_costs_sums_bands():
+    tr8 = np.arange(6 * 4).reshape(6, 4)          # 6 bands of 8x8 tiles, 4 across
+    assert list(tiles.row_tile_costs(tr8, 8)) == list(tr8.sum(axis=1))
+    assert list(tiles.row_tile_costs(tr8, 16)) == [tr8[0:2].sum(), tr8[2:4].sum(), tr8[4:6].sum()]
+    with pytest.raises(ValueError):
+        tiles.row_tile_costs(tr8, 4)
+
+
+def _gloo_plan_worker(rank, world, port, H, W, tr, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ntiles = (H + tr - 1) // tr
+    plan = tiles.lpt_plan(np.arange(ntiles)[::-1] % 5 + 1, world)
+    df = tiles.DistributedFrame(W, H, tr, rank, world, "cpu", plan=plan)
+    for k, t in enumerate(plan[rank]):          # a stub render: each row holds its image row index
+        for j in range(tr):
+            df.packed[k * tr + j] = float(t * tr + j)
+    frame = df.gather()
+    if rank == 0:
+        q.put(frame.numpy().copy())
+    dist.destroy_process_group()
+
+
+def test_distributed_gather_of_an_lpt_plan_gloo_world3():
+    """Per-rank tile lists (lpt_plan) instead of round-robin tiles: the gather's
+    unpack puts every packed row at its image row."""
+    import multiprocessing as mp
+    import socket
+    H, W, tr, world = 45, 3, 8, 3
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_plan_worker, args=(r, world, port, H, W, tr, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    frame = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(frame[:, :, 0], np.repeat(np.arange(H, dtype=np.float64)[:, None], W, 1))
+
+
 def _gloo_pipeline_worker(rank, world, port, H, W, tr, q):
     import torch
     import torch.distributed as dist
