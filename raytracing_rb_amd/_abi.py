@@ -139,7 +139,10 @@ def load_library(path=None):
             "librtx.so not found at %s — build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback)" % p)
     lib = C.CDLL(p)
+    in_tree = p == os.path.join(_HERE, "librtx.so")
     for name, res, args in SIGNATURES:
+        if not in_tree and not hasattr(lib, name):
+            continue                  # an older diagnostic build (tools/variants.py): what it exports
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
