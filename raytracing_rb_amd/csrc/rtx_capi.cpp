@@ -77,13 +77,13 @@ struct rtx_context {
   int64_t opt_engine = 1;            // 0: persistent lanes (per-lane LIFO ray tree), 1: bounce levels (default: faster, same bits)
   int64_t opt_lv_batch = 1 << 23;    // bounce levels: level-0 items (camera samples) per batch
   int64_t opt_lv_stage_pct = 300;    // bounce levels: ray records per staging buffer, % of the batch items
-  int64_t opt_lv_rec_pct = -1;       // bounce levels: tree records per group (tile), % of its items (-1 auto: 3200, 6400 from depth 6)
+  int64_t opt_lv_rec_pct = 1600;      // bounce levels: tree records of a batch (all levels), % of the batch items
   int64_t opt_lv_floor = 1 << 20;    // bounce levels: at least this many staging and 4x this many tree records
   int64_t opt_lv_split = 0;          // bounce levels: 1 = three phase launches per level (trace / shadow / shade)
   int64_t opt_lv_static = -1;        // bounce levels: % of a launch's chunks scheduled statically (-1 auto)
   int64_t opt_lv_compact = -1;       // bounce levels: 1 = park hits in an LDS ring and shade full waves, -1 auto (when it fits)
   int64_t opt_lv_grid_div = 1;       // bounce levels: persistent level grids = resident workgroups / this
-  int64_t opt_lv_fin_cap = 1024;     // bounce levels: a tile's tree records staged in LDS by the reduction when at most this many (0: never)
+  int64_t opt_lv_fin_cap = 0;        // bounce levels: tree records per tile gathered into LDS by the reduction (0: off; measured slower)
   int64_t opt_lv_fin_grid = 0;       // bounce levels: tree reduction blocks per CU (grid-stride over tiles), 0 = one block per tile
   int64_t opt_lv_redo_blocks = 8;    // bounce levels: workgroups of the overflow re-render launch (0: all resident)
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
@@ -417,62 +417,7 @@ void rtx_context_destroy(rtx_context* c) {
 }
 
 static bool levels_engine(const rtx_context* c);
-// Record geometry of one bounce-level batch: n0 level-0
-// items, groups of G = 64 x pre items (one pass-0 tile), each with a region
-// of capg tree records; and whether the 80-B staged ray record's tail word
-// holds {path, root, record in group}: path < (pt + 3)^trace_depth bits pb
-// (at most 32), root < n0 bits rb, record < capg bits cb (all ones = none).
-// lv_ray_bytes 80 asked for a camera whose fields do not fit is refused, not
-// truncated.
-struct LvGeom {
-  size_t n0, G, ngrp, capg, spill, lcap;
-  int pb, rb, cb;
-  bool small;
-};
-static int bitlen(uint64_t v) {
-  int b = 0;
-  while (v) b++, v >>= 1;
-  return b;
-}
-static LvGeom lv_geom(const rtx_context* c, size_t n0) {
-  LvGeom g{};
-  g.n0 = n0;
-  g.G = (size_t)64 * std::max(1, c->cam.pre);
-  g.ngrp = (n0 + g.G - 1) / g.G;
-  // per group: lv_rec_pct % of its items (auto 1600 %, 3200 % from depth 6:
-  // C2 averages 3.6 rays per sample, C4 9.6), and at least the floor's 4 x lv_floor records spread over the
-  // groups; a full region's children take records of the spill arena (8 per
-  // item: a tile of glass spheres makes up to (pt + 2)^depth rays per sample)
-  const int64_t pct = c->opt_lv_rec_pct > 0 ? c->opt_lv_rec_pct : (c->cam.depth <= 5 ? 1600 : 3200);
-  const size_t fl = (size_t)c->opt_lv_floor;
-  g.capg = std::max<size_t>({g.G + 1, g.G * (size_t)pct / 100, (4 * fl + g.ngrp - 1) / g.ngrp});
-  g.spill = c->opt_lv_rec_pct > 0 ? 0 : std::max<size_t>(fl, 8 * n0);   // (lv_rec_pct set: no spill, tests force overflow)
-  g.lcap = g.ngrp * g.capg + g.spill;
-  uint64_t v = 1;
-  bool p32 = true;
-  for (int l = 0; l < c->cam.depth && p32; l++) {
-    v *= (uint64_t)c->cam.pt + 3;
-    if (v > (1ull << 32)) p32 = false;
-  }
-  g.pb = p32 ? std::max(1, bitlen(v - 1)) : 64;
-  g.rb = std::max(1, bitlen(n0 > 0 ? n0 - 1 : 0));
-  g.cb = bitlen(g.lcap);                        // the record index (all ones: none)
-  g.small = c->opt_lv_ray_bytes != 96 && p32 && g.pb + g.rb + g.cb <= 64;
-  return g;
-}
-// the level-0 items of one batch of a region nx x nrows (render_levels)
-static size_t lv_batch_items(const rtx_context* c, int nx, int nrows, int* parts_out = nullptr,
-                             int* batch_tiles_out = nullptr) {
-  const int tiles = ((nx + 7) / 8) * ((nrows + 7) / 8);
-  const int per_tile = 64 * c->cam.pre;
-  const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_streams, tiles));
-  const int batch_tiles =
-      (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, (tiles + parts - 1) / parts));
-  if (parts_out) *parts_out = parts;
-  if (batch_tiles_out) *batch_tiles_out = batch_tiles;
-  return std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, c->cam.max_samples - c->cam.pre));
-}
-
+static bool lv_paths32(const rtx_context* c);
 
 rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
   if (!c || !key || !value) return RTX_EINVAL;
@@ -481,12 +426,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
     return RTX_OK;
   }
   if (!strcmp(key, "lv_ray_bytes_effective")) {   // read-only: the staged ray record of the next level render
-    if (!c->have_cam) {
-      *value = c->opt_lv_ray_bytes == 96 ? 96 : 80;
-    } else {
-      const LvGeom g = lv_geom(c, lv_batch_items(c, c->cam.width, c->cam.height));
-      *value = g.small ? 80 : 96;
-    }
+    *value = c->opt_lv_ray_bytes == 96 || (c->have_cam && !lv_paths32(c)) ? 96 : 80;
     return RTX_OK;
   }
   const struct { const char* k; int64_t v; } tab[] = {
@@ -554,8 +494,7 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     return RTX_OK;
   }
   if (!strcmp(key, "lv_stage_pct") || !strcmp(key, "lv_rec_pct")) {   // bounce-level buffer capacities
-    if ((value < 1 && !(value == -1 && !strcmp(key, "lv_rec_pct"))) || value > 10000)
-      return fail(c, RTX_EINVAL, "%s must be in [1, 10000]%s", key, strcmp(key, "lv_rec_pct") ? "" : " or -1 (auto)");
+    if (value < 1 || value > 10000) return fail(c, RTX_EINVAL, "%s must be in [1, 10000]", key);
     (!strcmp(key, "lv_stage_pct") ? c->opt_lv_stage_pct : c->opt_lv_rec_pct) = value;
     return RTX_OK;
   }
@@ -584,8 +523,8 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_lv_fin_grid = value;
     return RTX_OK;
   }
-  if (!strcmp(key, "lv_fin_cap")) {        // bounce levels: a tile's records staged in LDS by the reduction, 0 = never
-    if (value < 0 || value > 8192) return fail(c, RTX_EINVAL, "lv_fin_cap must be in [0, 8192]");
+  if (!strcmp(key, "lv_fin_cap")) {        // bounce levels: LDS tree records per tile in the reduction, 0 = off
+    if (value < 0 || value > 4096) return fail(c, RTX_EINVAL, "lv_fin_cap must be in [0, 4096]");
     c->opt_lv_fin_cap = value;
     return RTX_OK;
   }
@@ -960,6 +899,19 @@ static rtx_status prep(rtx_context* c, KParams& p, uint64_t seed) {
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // The bounce-level engine can take this camera: its levels and child slots.
+// 80-B ray records when a ray's path id fits 32 bits at every level: path
+// < (pt + 3)^trace_depth (the path ids of rtx_device.h emit / lv_finish).
+// lv_ray_bytes 80 asked for a camera whose paths do not fit is refused, not
+// truncated.
+static bool lv_paths32(const rtx_context* c) {
+  uint64_t v = 1;
+  for (int l = 0; l < c->cam.depth; l++) {
+    v *= (uint64_t)c->cam.pt + 3;
+    if (v > (1ull << 32)) return false;
+  }
+  return true;
+}
+
 static bool levels_engine(const rtx_context* c) {
   return c->opt_engine == 1 && c->cam.depth <= LV_MAXL && c->cam.pt + 2 <= 16 && c->scene.n_light <= 255;
 }
@@ -971,30 +923,31 @@ static bool levels_engine(const rtx_context* c) {
 // records (lv_rec_pct % x 32 B with one light), the re-render list.
 static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_t stream) {
   const size_t npx = (size_t)p.nx * p.nrows;
+  const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
+  const int per_tile = 64 * p.pre;
+  const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_streams, tiles));   // lv_streams (below)
+  const int batch_tiles =
+      (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, (tiles + parts - 1) / parts));
   // level-0 items of one batch: pass 0 (tiles) or pass 1 (>= one pixel's extra samples)
-  int parts = 1, batch_tiles = 1;                                   // lv_streams parts (below)
-  const size_t n0 = lv_batch_items(c, p.nx, p.nrows, &parts, &batch_tiles);
+  const size_t n0 = std::max((size_t)batch_tiles * per_tile, (size_t)std::max(0, p.max_samples - p.pre));
   const size_t fl = (size_t)c->opt_lv_floor;
   const size_t want = std::max<size_t>(std::max<size_t>(64, fl), n0 * (size_t)c->opt_lv_stage_pct / 100);
-  const LvGeom geo = lv_geom(c, n0);
-  const size_t lcap = geo.lcap;
+  const size_t lcap = std::max<size_t>(std::max(n0, 4 * fl), n0 * (size_t)c->opt_lv_rec_pct / 100);
   // queues of levels >= 1: LV_SLICES slices of 2^k slots (k rounded up)
   int slog2 = 0;
   while (((size_t)LV_SLICES << slog2) < want) slog2++;
   const size_t scap = (size_t)LV_SLICES << slog2;
   if (scap > UINT32_MAX / 2 || lcap > UINT32_MAX / 2)
     return fail(c, RTX_EINVAL, "bounce-level buffers exceed 2^31 records: lower lv_batch");
-  if (c->opt_lv_ray_bytes == 80 && !geo.small)
-    return fail(c, RTX_EINVAL,
-                "lv_ray_bytes 80: path (%d bits), root (%d) and record (%d) need more than 64 bits "
-                "((pt + 3)^trace_depth > 2^32, or a large batch)", geo.pb, geo.rb, geo.cb);
+  const bool path32 = lv_paths32(c);
+  if (c->opt_lv_ray_bytes == 80 && !path32)
+    return fail(c, RTX_EINVAL, "lv_ray_bytes 80: this camera's ray paths need 64 bits ((pt + 3)^trace_depth > 2^32)");
   const int rec_bytes = levels_rec_bytes(c->scene.n_light);
   // deferred highlight checks (k_hl_raise): room for 1/256 of the batch's tree
   // records (rays; C2 fires on ~0.1 % of them); a ray that finds the list full
   // has its sample re-rendered by the lanes engine (option lv_hl_cap: the size)
   const size_t hlcap = c->opt_lv_hl_cap > 0 ? (size_t)c->opt_lv_hl_cap : std::max<size_t>(4096, lcap / 256);
   const size_t sz_hlq = al256(hlcap * 64);
-  const size_t sz_grp = al256((geo.ngrp + 1) * 4);
   // exact_raises: the shading hits whose covers' raises k_hl_raise checks (1/4 of the records; overflow re-renders)
   const size_t xrcap = c->opt_exact_raises ? std::max<size_t>(4096, lcap / 4) : 0;
   const size_t sz_xrq = al256(xrcap * 32);
@@ -1014,7 +967,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // others' levels).  The extra-sample list and the statistics are shared
   // (appended / added atomically); each part has its own level buffers, its
   // own lanes-engine work counter and ray stacks for its overflow re-render.
-  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_grp + sz_xrq;
+  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_xrq;
   const size_t total = parts * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
@@ -1031,7 +984,6 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_area = split ? (double*)q : nullptr; q += sz_area;
     k.lv_hlq = (double*)q;                    q += sz_hlq;
     k.lv_hlq_cap = (uint32_t)hlcap;
-    k.lv_grp = (uint32_t*)q;                  q += sz_grp;
     k.lv_xrq = xrcap ? (double*)q : nullptr;
     k.lv_xrq_cap = (uint32_t)xrcap;
   };
@@ -1040,7 +992,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_compact = (int32_t)c->opt_lv_compact;
   p.lv_grid_div = (int32_t)c->opt_lv_grid_div;
   p.lv_redo_blocks = (int32_t)c->opt_lv_redo_blocks;
-  p.lv_fin_cap = (int32_t)c->opt_lv_fin_cap;   // (the launcher caps it to what one reduction block's LDS holds)
+  p.lv_fin_cap = (int32_t)c->opt_lv_fin_cap;   // the launcher turns it off when the rings do not fit LDS
   p.lv_fin_tiles = (int32_t)c->opt_lv_fin_grid;   // (blocks per CU here; the launcher sets the tile count)
   // Static chunks cost no atomics; dynamic claims balance rays of very
   // different cost.  Auto: all static while the sphere records fit one walk
@@ -1054,13 +1006,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   p.lv_hslice_log2 = hlog2;
   p.lv_lcap = (uint32_t)lcap;
   p.lv_rec_bytes = rec_bytes;
-  p.lv_ray_dbl = geo.small ? 10 : 12;
-  p.lv_grp_items = (uint32_t)geo.G;
-  p.lv_grp_cap = (uint32_t)geo.capg;
-  p.lv_spill0 = (uint32_t)(geo.ngrp * geo.capg);
-  p.lv_spill_cap = (uint32_t)geo.spill;
-  p.lv_tail_pb = geo.pb;
-  p.lv_tail_rb = geo.rb;
+  p.lv_ray_dbl = (c->opt_lv_ray_bytes == 96 || !path32) ? 12 : 10;
   p.lv_last_level = c->cam.depth >= 1 ? c->cam.depth - 1 : -1;
   p.lv_acc = c->d_lvstats;
   p.samples = nullptr;

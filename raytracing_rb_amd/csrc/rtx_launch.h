@@ -30,8 +30,7 @@ struct LevelCtl {
   uint32_t dropped;                             // child rays that found no room (diagnostic)
   uint32_t hl_n;                                // highlight rays whose lit_area raise check is deferred (k_hl_raise)
   uint32_t xr_n;                                // shading hits whose covers' raise check is deferred (exact_raises)
-  uint32_t spill_n;                             // tree records taken from the spill arena (full group regions)
-  uint32_t pad[26];                             // (pad[0]: the lanes-engine work counter of parts 1..)
+  uint32_t pad[27];                             // (pad[0]: the lanes-engine work counter of parts 1..)
   uint32_t sc[LV_MAXL + 1][LV_SLICES * 32];     // rays allocated in slice s of level d: sc[d][32 s]
   uint32_t sh[LV_MAXL + 1][LV_SLICES * 32];     // split phases: hits of level d in slice s
   uint32_t claim[3][LV_MAXL + 1][LV_CLAIMS * 32]; // chunk claims: [launch kind: fused/trace, shadow, shade][level][j * 32]
@@ -89,17 +88,8 @@ struct KParams {
   uint32_t lv_scap;                // ray records per staging buffer (levels >= 1): LV_SLICES << lv_slice_log2
   int32_t lv_slice_log2;           // slots per slice of a level's ray queue (log2)
   int32_t lv_hslice_log2;          // split phases: slots per slice of a level's hit queue (log2)
-  uint32_t lv_lcap;                // tree records in lv_rec (lv_grp_cap per group)
+  uint32_t lv_lcap;                // tree records in lv_rec
   int32_t lv_rec_bytes;
-  // Tree records by group: level-0 items k*G .. k*G+G-1
-  // (G = lv_grp_items = one pass-0 tile's 64 x pre samples) own records
-  // [k*C, (k+1)*C) (C = lv_grp_cap): their level-0 records first, then every
-  // descendant's, appended by the parents (lv_grp[k] = records in use).  A
-  // tile's trees are one contiguous run the reduction streams.
-  uint32_t* lv_grp;
-  uint32_t lv_grp_items, lv_grp_cap;
-  uint32_t lv_spill0, lv_spill_cap;  // a full region's children take records lv_spill0 + k, k < lv_spill_cap
-  int32_t lv_tail_pb, lv_tail_rb;  // 80-B ray record: bits of path and root in its tail word (the rest: the record)
   LevelCtl* lv_ctl;
   double* lv_stage[2];             // level d reads lv_stage[d & 1], writes lv_stage[(d + 1) & 1]
   char* lv_rec;
@@ -116,7 +106,7 @@ struct KParams {
   int32_t lv_last_level;           // trace_depth - 1 (-1 if trace_depth < 1): the level whose children are all
                                    // cut off, run by a k_level_c compiled for it
   int32_t lv_grid_div;             // level launches: persistent grid = resident workgroups / this (option lv_grid_div)
-  int32_t lv_fin_cap;              // tree reduction: a tile's records staged in LDS when they are at most this many (0: never)
+  int32_t lv_fin_cap;              // tree reduction: records of a tile gathered into LDS (0: walk from global memory)
   int32_t lv_fin_tiles;            // tree reduction pass 0: tiles of the batch (grid-stride loop when the grid is smaller)
   int32_t lv_redo_blocks;          // the lanes-engine re-render of overflowed samples: at most this many workgroups (0: all resident)
   int32_t lv_ray_dbl;              // staged ray record, doubles: 10 (80 B: path < 2^32, RNG key decoded from the root) or 12

@@ -43,30 +43,17 @@ namespace rtx {
 // refraction; local_lights' lit_area; path tracing / local_lighting), the walk
 // takes the first in tree order, and a >1 partial sum counts only without one.
 //
-// Capacity.  Children beyond their slice or tree records beyond their
-// group's region are not written; their camera sample is listed
-// (lv_redo_list) and re-rendered whole by the lanes engine (SRC_LIST), exact
-// either way.  A group region that fills up hands its children records of a
-// shared spill arena first (lv_spill0 + k).
-//
-// Tree records by group.  The records of the trees of one
-// pass-0 tile (its 64 x pre level-0 items, a group) live in one region of
-// lv_grp_cap records: the level-0 records first (item order), then every
-// descendant's, appended by its parent (lv_grp_alloc).  A record keeps its
-// first child's record index, so k_tree_finalize walks absolute indices and
-// reads a tile's trees as one contiguous run (streamed, or staged in LDS).
-//
-// Staging ray record (p.lv_ray_dbl doubles per slot): o, d, att, then
-//   12 (96 B): {path}, {root item | record << 32, unused};
-//   10 (80 B): one tail word {path | root << pb | record << (pb + rb)}
-//   (pb = lv_tail_pb, rb = lv_tail_rb: the host picks it when the three fit).
-// The RNG key (x, y, sample), needed only by the path-tracing children of a
-// level >= 1 ray, is decoded from the root (lv_ray_key).  A record index of
-// LV_NOREC (all ones) marks a ray whose group overflowed: its sample is
-// already listed for the re-render, the ray itself does nothing.
+// Capacity.  Children beyond their slice or tree records beyond the record
+// arena are not written; their camera sample is listed (lv_redo_list) and
+// re-rendered whole by the lanes engine (SRC_LIST), exact either way.
+// Staging ray record (p.lv_ray_dbl doubles per slot):
+//   12 (96 B): o, d, att, path, {root item, sample}, {x, y};
+//   10 (80 B): o, d, att, {path, root item} as two 32-bit words.  The host
+//   picks it when every path of the camera's trees fits 32 bits (path < (pt +
+//   3)^trace_depth <= 2^32); the RNG key (x, y, sample), needed only by the
+//   path-tracing children of a level >= 1 ray, is then decoded from the root.
 constexpr int RAY_DOUBLES = 12;
 constexpr int RAY_DOUBLES_SMALL = 10;
-constexpr uint32_t LV_NOREC = 0xffffffffu;
 constexpr int HIT_DOUBLES = 8;           // split hit record: hit, hit + delta, {ray, object | in}, {slot, raises}
 static_assert(RAY_DOUBLES * 8 == (int)RAY_BYTES && HIT_DOUBLES * 8 == (int)LV_HIT_BYTES, "record sizes");
 
@@ -122,73 +109,47 @@ __device__ __forceinline__ void lv_hl_defer(const KParams& p, bool want, const R
   q[3] = make_double2(__builtin_bit_cast(double, (uint64_t)rec), 0.0);
 }
 
-// The level-0 record of an item (the head of its group's region).
-__device__ __forceinline__ uint32_t lv_rec0(const KParams& p, uint32_t item) {
-  const uint32_t g = item / p.lv_grp_items;
-  return g * p.lv_grp_cap + (item - g * p.lv_grp_items);
-}
-
-// root: the level-0 item of the ray's tree; rec: the ray's tree record.
+// root: the level-0 item of the ray's tree; (x, y, sample): its RNG key.
 __device__ __forceinline__ void lv_store_ray(const KParams& p, double* dst, const Ray& r, V3 att, uint64_t path,
-                                             int root, uint32_t rec) {
+                                             int root, int x, int y, int sample) {
   double2* q = reinterpret_cast<double2*>(dst);
   q[0] = make_double2(r.o.x, r.o.y);
   q[1] = make_double2(r.o.z, r.d.x);
   q[2] = make_double2(r.d.y, r.d.z);
   q[3] = make_double2(att.x, att.y);
   if (p.lv_ray_dbl == RAY_DOUBLES_SMALL) {
-    const uint32_t sh = (uint32_t)(p.lv_tail_pb + p.lv_tail_rb);
-    const uint64_t r64 = rec == LV_NOREC ? ~0ull : (uint64_t)rec;
-    const uint64_t w = path | (uint64_t)(uint32_t)root << p.lv_tail_pb | r64 << sh;
-    q[4] = make_double2(att.z, __builtin_bit_cast(double, w));
+    q[4] = make_double2(att.z, __builtin_bit_cast(double, (uint64_t)(uint32_t)path | (uint64_t)(uint32_t)root << 32));
     return;
   }
   q[4] = make_double2(att.z, __builtin_bit_cast(double, path));
-  q[5] = make_double2(__builtin_bit_cast(double, (uint64_t)(uint32_t)root | (uint64_t)rec << 32), 0.0);
+  q[5] = make_double2(__builtin_bit_cast(double, (uint64_t)(uint32_t)root | (uint64_t)(uint32_t)sample << 32),
+                      __builtin_bit_cast(double, (uint64_t)(uint32_t)x | (uint64_t)(uint32_t)y << 32));
 }
 
-// Decode a small record's tail word.
-__device__ __forceinline__ void lv_tail_small(const KParams& p, uint64_t w, uint64_t& path, int& root, uint32_t& rec) {
-  const uint32_t pb = (uint32_t)p.lv_tail_pb, rb = (uint32_t)p.lv_tail_rb;
-  path = w & ((1ull << pb) - 1ull);
-  root = (int)((w >> pb) & ((1ull << rb) - 1ull));
-  const uint64_t r64 = w >> (pb + rb);
-  rec = r64 == (~0ull >> (pb + rb)) ? LV_NOREC : (uint32_t)r64;
-}
-
-// A staged ray's path, root item and record from the record's last 16-B
-// words (e = {att.z, .}; the 96-B record's q[5] is read here); the RNG key is
-// left -1 (decoded when needed, lv_ray_key).
+// A staged ray's path, root item and RNG key from the record's last 16-B
+// words (e = {att.z, .}, f: the 96-B record's last word, unread for 80 B).
 __device__ __forceinline__ void lv_ray_tail(const KParams& p, const double2* q, double2 e, uint64_t& path, int& root,
-                                            uint32_t& rec, int& x, int& y, int& sample) {
+                                            int& x, int& y, int& sample) {
   const uint64_t w = __builtin_bit_cast(uint64_t, e.y);
-  x = y = sample = -1;
   if (p.lv_ray_dbl == RAY_DOUBLES_SMALL) {
-    lv_tail_small(p, w, path, root, rec);
+    path = (uint32_t)w;
+    root = (int)(w >> 32);
+    x = y = sample = -1;                       // decoded when needed (lv_ray_key)
     return;
   }
+  const double2 f = q[5];
   path = w;
-  const uint64_t rs = __builtin_bit_cast(uint64_t, q[5].x);
+  const uint64_t rs = __builtin_bit_cast(uint64_t, f.x), xy = __builtin_bit_cast(uint64_t, f.y);
   root = (int)(uint32_t)rs;
-  rec = (uint32_t)(rs >> 32);
+  sample = (int)(rs >> 32);
+  x = (int)(uint32_t)xy;
+  y = (int)(xy >> 32);
 }
 
-// The root item and the record of the staged ray at `q`.
-__device__ __forceinline__ void lv_ray_root_rec(const KParams& p, const double2* q, int& root, uint32_t& rec) {
-  if (p.lv_ray_dbl == RAY_DOUBLES_SMALL) {
-    uint64_t path;
-    lv_tail_small(p, __builtin_bit_cast(uint64_t, q[4].y), path, root, rec);
-    return;
-  }
-  const uint64_t rs = __builtin_bit_cast(uint64_t, q[5].x);
-  root = (int)(uint32_t)rs;
-  rec = (uint32_t)(rs >> 32);
-}
+// The root item of the staged ray at `q` (its record-arena overflow).
 __device__ __forceinline__ int lv_ray_root(const KParams& p, const double2* q) {
-  int root;
-  uint32_t rec;
-  lv_ray_root_rec(p, q, root, rec);
-  return root;
+  const uint64_t w = __builtin_bit_cast(uint64_t, p.lv_ray_dbl == RAY_DOUBLES_SMALL ? q[4].y : q[5].x);
+  return p.lv_ray_dbl == RAY_DOUBLES_SMALL ? (int)(w >> 32) : (int)(uint32_t)w;
 }
 
 __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
@@ -421,14 +382,13 @@ __device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V
 }
 
 // The ray of a level's queue entry: a camera sample (level 0: `idx` = its
-// item, Camera#lens_func) or the staged child at slot `idx`; `rec` its tree
-// record.  `valid` false for the padding of an 8x8 tile.
-__device__ __forceinline__ void lv_ray(const KParams& p, int level, uint32_t idx, Item& cur, int& root, uint32_t& rec,
-                                       int& x, int& y, int& sample, bool& valid) {
+// item, Camera#lens_func) or the staged child at slot `idx`.  `valid` false
+// for the padding of an 8x8 tile.
+__device__ __forceinline__ void lv_ray(const KParams& p, int level, uint32_t idx, Item& cur, int& root, int& x, int& y,
+                                       int& sample, bool& valid) {
   valid = true;
   if (level == 0) {
     root = (int)idx;
-    rec = lv_rec0(p, idx);
     const ItemPos ip = decode_item(p, root);
     x = p.x0 + ip.px;
     y = row_to_y(p, ip.row);
@@ -447,39 +407,17 @@ __device__ __forceinline__ void lv_ray(const KParams& p, int level, uint32_t idx
   cur.ray.o = v3(a.x, a.y, b.x);
   cur.ray.d = v3(b.y, c.x, c.y);
   cur.att = v3(d.x, d.y, e.x);
-  lv_ray_tail(p, q, e, cur.path, root, rec, x, y, sample);
+  lv_ray_tail(p, q, e, cur.path, root, x, y, sample);
 }
 
 // The RNG key (x, y, sample) of a ray of tree `root` (lv_ray_tail leaves it
-// -1): decode_item of the root, as lv_ray does at level 0.
+// -1 for an 80-B record): decode_item of the root, as lv_ray does at level 0.
 __device__ __forceinline__ void lv_ray_key(const KParams& p, int root, int& x, int& y, int& sample) {
   if (x >= 0) return;
   const ItemPos ip = decode_item(p, root);
   x = p.x0 + ip.px;
   y = row_to_y(p, ip.row);
   sample = ip.sample;
-}
-
-// Records for the children of every lane with n > 0 in its sample's group
-// region g: one atomicAdd per distinct group of the wave (its lanes' counts
-// prefix-summed), issued here; the lane's first record is
-// __shfl(ret, lp & 63) + (lp >> 6), read later (the atomics' round trips
-// overlap the caller's arithmetic).  A wave's rays come from one tile at
-// level 0 and from a few at deeper levels, so the loop runs once or a few times.
-__device__ __forceinline__ void lv_grp_issue(const KParams& p, uint32_t g, uint32_t n, uint32_t& ret, uint32_t& lp) {
-  uint64_t rem = __ballot(n > 0);
-  while (rem) {
-    const int L = __builtin_ctzll(rem);
-    const uint32_t gL = (uint32_t)__builtin_amdgcn_readlane((int)g, L);
-    const bool mine = n > 0 && g == gL;
-    const uint64_t mm = __ballot(mine);
-    const uint32_t v = mine ? n : 0u;
-    const uint32_t incl = wave_scan_incl(v);
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    if ((int)__lane_id() == L) ret = atomicAdd(p.lv_grp + gL, tot);
-    if (mine) lp = (uint32_t)L | (incl - v) << 6;
-    rem &= ~mm;
-  }
 }
 
 // rt_map's tail once the lit areas are known (ray_tracer.rb:80-158): which
@@ -527,9 +465,6 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
   const int wtotal = __shfl(incl, 63);
   uint32_t wraw = 0;
   if (wtotal > 0 && __lane_id() == 0) wraw = atomicAdd(lv_slice_ctr(p.lv_ctl->sc[level + 1], slice), (uint32_t)wtotal);
-  // ... and their tree records in the sample's group region (read after the arithmetic too)
-  uint32_t gret = 0, glp = 0;
-  if (wtotal > 0) lv_grp_issue(p, (uint32_t)root / p.lv_grp_items, (uint32_t)nch, gret, glp);
   Ray refl, refr;
   bool has_refr = false;
   if (shade) {
@@ -588,35 +523,19 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
     }
   }
   const uint32_t off0 = (wtotal > 0 ? (uint32_t)__shfl((int)wraw, 0) : 0u) + (uint32_t)(incl - nch);
-  uint32_t child0 = 0;                        // the first child's tree record (k_tree_finalize)
-  if (wtotal > 0) {
-    const uint32_t goff = (uint32_t)__shfl((int)gret, (int)(glp & 63u)) + (glp >> 6);
-    if (nch > 0) {
-      if (goff + (uint32_t)nch <= p.lv_grp_cap) {
-        child0 = (uint32_t)root / p.lv_grp_items * p.lv_grp_cap + goff;
-      } else {                                // the group's region is full: the spill arena (rare)
-        const uint32_t s0 = atomicAdd(&p.lv_ctl->spill_n, (uint32_t)nch);
-        if (s0 + (uint32_t)nch <= p.lv_spill_cap) {
-          child0 = p.lv_spill0 + s0;
-        } else {                              // that too: re-render the sample
-          child0 = LV_NOREC;
-          lv_redo(p, root);
-        }
-      }
-    }
-  }
+  const uint32_t child0 = ((uint32_t)slice << log2cap) + off0;   // slot of the first child (k_tree_finalize)
   if (shade) {
     double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
-    uint32_t off = off0, crec = child0;
+    uint32_t off = off0;
     auto put = [&](const Ray& r, V3 att, uint64_t path) {
       if (off < cap)
-        lv_store_ray(p, outs + (size_t)(((uint32_t)slice << log2cap) + off) * p.lv_ray_dbl, r, att, path, root, crec);
+        lv_store_ray(p, outs + (size_t)(((uint32_t)slice << log2cap) + off) * p.lv_ray_dbl, r, att, path, root, x, y,
+                     sample);
       else {
         lv_redo(p, root);
         atomicAdd(&p.lv_ctl->dropped, 1u);
       }
       off++;
-      if (crec != LV_NOREC) crec++;
     };
     if (mask & 1u) put(refl, vmul(cur.att, v3p(m->refl_att)), cur.path * R + 1);
     if (has_refr) put(refr, vmul(cur.att, v3p(m->refr_att)), cur.path * R + 2);
@@ -651,9 +570,10 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
   }
   // Option exact_raises: local_lights' lit_area raises of the covers the
   // shadow walks skipped (factor 0), checked after the levels
-  // by k_hl_raise (an inline walk here cost the kernel registers even when off).
-  // Only a hit with no raise before local_lights' (errA, errS, errL) is listed:
-  // a raise found there replaces the record's (local_lighting's, or none).
+  // by k_hl_raise (an inline walk here cost the kernel registers and spills
+  // even when off).  Only a hit with no raise before local_lights' (errA,
+  // errS, errL) is listed: a raise found there replaces the record's
+  // (local_lighting's, or none).
   if (RTX_EXACT_RAISES && xr && p.exact_raises) {
     const bool want = shade && active && !((errA | errS | errL) & 0xffu);
     const uint64_t wm = __ballot(want);
@@ -688,6 +608,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
   lv_in_queue(p, level, in);
   if (in.chunks == 0) return;                 // uniform: before any barrier
   lv_stage_scene<SPH, BS>(p, lds_sph);
+  const uint32_t base = lv_base(p, level);
   const int depth = p.cam->depth - level;
   LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
   const int slice = sched.wave_id() & (LV_SLICES - 1);
@@ -711,17 +632,19 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
     // ---- the ray: a camera sample (level 0) or a staged child
     Item cur;
     int root = 0, x = 0, y = 0, sample = 0;
-    uint32_t ri = 0;                          // the ray's tree record
     bool alive = false;
     if (active) {
       bool valid;
-      lv_ray(p, level, level == 0 ? i : (s << p.lv_slice_log2) + off, cur, root, ri, x, y, sample, valid);
+      lv_ray(p, level, level == 0 ? i : (s << p.lv_slice_log2) + off, cur, root, x, y, sample, valid);
       if (level == 0) p.lv_redo_of[i] = -1;   // no overflow yet (lv_redo)
       active = valid;                         // tile padding: no record
       alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // rt_map's cutoff (ray_tracer.rb:52)
-      if (active && ri == LV_NOREC) active = alive = false;   // its group overflowed: the sample is re-rendered
+      if (active && base + i >= p.lv_lcap) {  // no room for this ray's record
+        lv_redo(p, root);
+        active = alive = false;
+      }
     }
-    char* rec = p.lv_rec + (size_t)ri * p.lv_rec_bytes;
+    char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
     double* leafp = reinterpret_cast<double*>(rec + 8);
 
     // ---- rt_map: highlights (ray_tracer.rb:60-75)
@@ -735,7 +658,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
       }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
-    lv_hl_defer(p, hl_defer, cur.ray, ri, [&] { return root; });
+    lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return root; });
     RTX_LV_STAMP(0)
     // ---- World#intersect (world.rb:37-59)
     const bool ext = alive && !fired;
@@ -845,7 +768,7 @@ constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMA
 template <int SPH, int BS, int RF, bool LAST>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
-  constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {level 0: item, else tree record, queue slot}
+  constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
   const SceneDev& S = p.scene;
   extern __shared__ float4 lds_sph[];
   char* lds = reinterpret_cast<char*>(lds_sph);
@@ -853,6 +776,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   lv_in_queue(p, level, in);
   if (in.chunks == 0) return;                 // uniform: before any barrier
   lv_stage_scene<SPH, BS>(p, lds_sph);
+  const uint32_t base = lv_base(p, level);
   const int depth = LAST ? 1 : p.cam->depth - level;   // LAST: the batch's last level, compiled apart
   LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
   const int slice = sched.wave_id() & (LV_SLICES - 1);
@@ -879,32 +803,32 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       uint32_t s, off, i;
       bool active = in.item(chunk, s, off, i);
       const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
-      // A staged child's first half needs its origin, direction and tree
-      // record only: the attenuation is read if a highlight fires, the root if
-      // the highlight list overflows (the second half reloads the rest), so
+      // A staged child's first half needs its origin and direction only: the
+      // attenuation is read if a highlight fires, the root if the ray
+      // overflows the record arena (the second half reloads the rest), so
       // the walk does not carry them.
       const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
       Item cur;
       int root = 0, x = 0, y = 0, sample = 0;
-      uint32_t ri = 0;                        // the ray's tree record
       bool alive = false;
       if (active) {
         bool valid = true;
         if (level == 0) {
-          lv_ray(p, level, slot, cur, root, ri, x, y, sample, valid);
+          lv_ray(p, level, slot, cur, root, x, y, sample, valid);
           p.lv_redo_of[i] = -1;
         } else {
           const double2 a = qs[0], b = qs[1], c = qs[2];
           cur.ray.o = v3(a.x, a.y, b.x);
           cur.ray.d = v3(b.y, c.x, c.y);
-          int rt;
-          lv_ray_root_rec(p, qs, rt, ri);
         }
         active = valid;
         alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // ray_tracer.rb:52
-        if (active && ri == LV_NOREC) active = alive = false;   // its group overflowed: the sample is re-rendered
+        if (active && base + i >= p.lv_lcap) {
+          lv_redo(p, level == 0 ? root : lv_ray_root(p, qs));
+          active = alive = false;
+        }
       }
-      char* rec = p.lv_rec + (size_t)ri * p.lv_rec_bytes;
+      char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
       double* leafp = reinterpret_cast<double*>(rec + 8);
       uint32_t errA = 0, errL = 0;
       int nleaf = 0;
@@ -920,7 +844,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
           leafp[3 * nleaf + 2] = c.z;
           nleaf++;
         }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
-      lv_hl_defer(p, hl_defer, cur.ray, ri, [&] { return level == 0 ? root : lv_ray_root(p, qs); });
+      lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return level == 0 ? root : lv_ray_root(p, qs); });
       RTX_LV_STAMP(0)
       const bool ext = alive && !fired;
       double best = S.max_distance, total = 0.0;
@@ -955,7 +879,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
           r[7 * LV_RING] = cur.ray.d.y;
           r[8 * LV_RING] = cur.ray.d.z;
         }
-        r[FI * LV_RING] = __builtin_bit_cast(double, (uint64_t)(level == 0 ? i : ri) | (uint64_t)slot << 32);
+        r[FI * LV_RING] = __builtin_bit_cast(double, (uint64_t)i | (uint64_t)slot << 32);
         r[(FI + 1) * LV_RING] = __builtin_bit_cast(
             double, (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) | (uint64_t)((errA & 0xffu) | (errL & 0xffu) << 8) << 32);
       }
@@ -971,7 +895,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     const bool shade = (uint32_t)lane < take;
     Item cur;
     V3 hit = v3(0.0, 0.0, 0.0);
-    uint32_t i = 0, ri = 0, errA = 0, errL = 0, errS = 0, errP = 0;
+    uint32_t i = 0, errA = 0, errL = 0, errS = 0, errP = 0;
     int besti = 0, root = 0, x = 0, y = 0, sample = 0;
     bool hin = true;
     if (shade) {
@@ -990,7 +914,6 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       errL = (uint32_t)(be >> 40) & 0xffu;
       if (level == 0) {                       // the camera sample: item i (lv_ray)
         root = (int)i;
-        ri = lv_rec0(p, i);
         const ItemPos ip = decode_item(p, root);
         x = p.x0 + ip.px;
         y = row_to_y(p, ip.row);
@@ -1010,12 +933,12 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         }
         const double2 d = q[3], e = q[4];
         cur.att = v3(d.x, d.y, e.x);
-        lv_ray_tail(p, q, e, cur.path, root, ri, x, y, sample);
+        lv_ray_tail(p, q, e, cur.path, root, x, y, sample);
       }
     }
     head = (head + take) & (LV_RING - 1);
     pend -= take;
-    char* rec = p.lv_rec + (size_t)ri * p.lv_rec_bytes;
+    char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
     RTX_LV_STAMP(4)
     V3 delta = hit, nrm = hit, nn = hit;
     double c = 0.0;
@@ -1117,6 +1040,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
   lv_in_queue(p, level, in);
   if (in.chunks == 0) return;                 // uniform: before any barrier
   lv_stage_scene<SPH, BS>(p, lds_sph);
+  const uint32_t base = lv_base(p, level);
   const int depth = p.cam->depth - level;
   LvSched sched(p.lv_ctl->claim[0][level], p.lv_static_pct);
   const int slice = sched.wave_id() & (LV_SLICES - 1);
@@ -1129,16 +1053,18 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
     bool alive = false;
     Item cur;
     int root = 0, x = 0, y = 0, sample = 0;
-    uint32_t ri = 0;                          // the ray's tree record
     if (active) {
       bool valid;
-      lv_ray(p, level, slot, cur, root, ri, x, y, sample, valid);
+      lv_ray(p, level, slot, cur, root, x, y, sample, valid);
       if (level == 0) p.lv_redo_of[i] = -1;   // no overflow yet (lv_redo)
       active = valid;                         // tile padding: no record
       alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // rt_map's cutoff (ray_tracer.rb:52)
-      if (active && ri == LV_NOREC) active = alive = false;   // its group overflowed: the sample is re-rendered
+      if (active && base + i >= p.lv_lcap) {  // no room for this ray's record
+        lv_redo(p, root);
+        active = alive = false;
+      }
     }
-    char* rec = p.lv_rec + (size_t)ri * p.lv_rec_bytes;
+    char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
     double* leafp = reinterpret_cast<double*>(rec + 8);
     uint32_t errA = 0, errL = 0;
     int nleaf = 0;
@@ -1150,7 +1076,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
       }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
-    lv_hl_defer(p, hl_defer, cur.ray, ri, [&] { return root; });
+    lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return root; });
     const bool ext = alive && !fired;
     double best = S.max_distance, total = 0.0;
     int besti = -1;
@@ -1172,7 +1098,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
       q[1] = make_double2(hit.z, qo.x);
       q[2] = make_double2(qo.y, qo.z);
       q[3] = make_double2(
-          __builtin_bit_cast(double, (uint64_t)ri | (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) << 32),
+          __builtin_bit_cast(double, (uint64_t)i | (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) << 32),
           __builtin_bit_cast(double, (uint64_t)slot | (uint64_t)((errA & 0xffu) | (errL & 0xffu) << 8) << 32));
     } else if (active) {
       uint32_t err = errA;
@@ -1210,7 +1136,8 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_shadow(KParams p, in
       bool in2 = true;
       uint32_t err = 0;
       lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, err);
-      if (RTX_EXACT_RAISES && p.exact_raises && !(err & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, L.radius)) seterr(err, ERR_DOMAIN);
+      if (RTX_EXACT_RAISES && p.exact_raises && !(err & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, L.radius))
+        seterr(err, ERR_DOMAIN);
       reinterpret_cast<double2*>(p.lv_area)[(size_t)hs * nL + li] =
           make_double2(tot, __builtin_bit_cast(double, (uint64_t)err));
     }
@@ -1223,6 +1150,7 @@ __device__ __forceinline__ void k_lv_shade_body(const KParams& p, int level) {
   LvQueue in;
   in.sliced(p.lv_ctl->sh[level], 1u << hlog2, 1u);
   if (in.chunks == 0) return;
+  const uint32_t base = lv_base(p, level);
   const int nL = S.n_light;
   LvSched sched(p.lv_ctl->claim[2][level], p.lv_static_pct);
   const int slice = sched.wave_id() & (LV_SLICES - 1);
@@ -1232,7 +1160,7 @@ __device__ __forceinline__ void k_lv_shade_body(const KParams& p, int level) {
     const bool shade = in.item(chunk, s, off, t);
     const uint32_t hs = (s << hlog2) + off;   // hit slot
     V3 hit = v3(0.0, 0.0, 0.0);
-    uint32_t ri = 0, errA = 0, errL = 0, errS = 0, errP = 0;
+    uint32_t i = 0, errA = 0, errL = 0, errS = 0, errP = 0;
     int besti = 0;
     bool hin = true;
     Item cur;
@@ -1242,15 +1170,15 @@ __device__ __forceinline__ void k_lv_shade_body(const KParams& p, int level) {
       const double2 a = q[0], b = q[1], d = q[3];
       hit = v3(a.x, a.y, b.x);
       const uint64_t ib = __builtin_bit_cast(uint64_t, d.x), se = __builtin_bit_cast(uint64_t, d.y);
-      ri = (uint32_t)ib;                      // (lv_ray gives the same record)
+      i = (uint32_t)ib;
       besti = (int)((uint32_t)(ib >> 32) & 0x7fffffffu);
       hin = (ib >> 63) != 0;
       errA = (uint32_t)(se >> 32) & 0xffu;
       errL = (uint32_t)(se >> 40) & 0xffu;
       bool valid;
-      lv_ray(p, level, (uint32_t)se, cur, root, ri, x, y, sample, valid);
+      lv_ray(p, level, (uint32_t)se, cur, root, x, y, sample, valid);
     }
-    char* rec = p.lv_rec + (size_t)ri * p.lv_rec_bytes;
+    char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
     V3 delta = hit, nrm = hit, nn = hit;
     double c = 0.0;
     if (shade) {
@@ -1290,38 +1218,43 @@ __global__ __launch_bounds__(BS_SHADE, RTX_LV_SHADE_WPS) void k_lv_shade(KParams
 }
 
 // ----------------------------------------------------------------- tree reduction
-// The batch's level statistics (rtx_level_stats), added by block 0 of the
-// reduction: every level launch of the batch has ended.
-__device__ __forceinline__ void lv_stats(const KParams& p, int nlev) {
+// The batch's level layout for the reductions: base[d] = first record of level
+// d, pex[d * 64 + s] = dense index of slice s's first ray at level d (d >= 1).
+// Block 0 also adds the batch's level statistics to lv_acc (rtx_level_stats):
+// every level launch of the batch has ended.
+__device__ __forceinline__ void lv_layout(const KParams& p, int nlev, uint32_t* base, uint32_t* pex) {
   const int t = (int)threadIdx.x;
+  for (int w = t; w < nlev * 64; w += (int)blockDim.x)
+    if (w >= 64) pex[w] = p.lv_ctl->lay_pex[w >> 6][w & 63];
+  if (t <= nlev && t <= LV_MAXL) base[t] = p.lv_ctl->lay_base[t];
   if (blockIdx.x == 0 && p.lv_acc) {
-    // atomic: the parts of a multi-stream render add into the same totals
+    // atomic: the two halves of a two-stream render add into the same totals
     if (t == 0) atomicAdd(&p.lv_acc[0], (unsigned long long)p.lv_ctl->redo_n);
     if (t == 1) atomicAdd(&p.lv_acc[1], (unsigned long long)p.lv_ctl->dropped);
-    if (t < nlev && t <= LV_MAXL)
+    if (t < nlev)
       atomicAdd(&p.lv_acc[2 + t], (unsigned long long)(p.lv_ctl->lay_base[t + 1] - p.lv_ctl->lay_base[t]));
   }
+  __syncthreads();
 }
 
-// Sum of one camera sample's tree (root record r0) in trace_sync's order:
-// pre-order, children in reverse slot order.  Returns the first raise
-// (rt_map's first, else rt_reduce's).  `at(i)` is record i (global memory, or
-// the tile's run staged in LDS).  The walk keeps one pending child range per
-// level below the root in lo[k * st] / hi[k * st], k < sd (LDS, word-major
-// over the block's threads, or a private array with st = 1).  PF: fetch a
-// node's children's headers as soon as it is read (global walks: the
-// dependent chain becomes the tree's depth, not its size).
-template <bool PF, typename At>
-__device__ __forceinline__ V3 lv_tree_sum(At&& at, uint32_t r0, int nlev, uint32_t* lo, uint32_t* hi, int st, int sd,
-                                          uint32_t& err_out) {
+// Sum of one camera sample's tree (level-0 item `root`) in trace_sync's
+// order: pre-order, children in reverse slot order.  Returns the first raise
+// (rt_map's first, else rt_reduce's).  The walk keeps one pending child range
+// per level below the root in lo[k * st] / hi[k * st], k < sd (LDS, word-major
+// over the block's threads, or a private array with st = 1).
+__device__ __forceinline__ V3 lv_tree_sum(const KParams& p, const uint32_t* base, const uint32_t* pex, int root,
+                                          int nlev, uint32_t* lo, uint32_t* hi, int st, int sd, uint32_t& err_out,
+                                          uint32_t& nvis) {
   int sp = 0;
   V3 sum = v3(0.0, 0.0, 0.0);
   uint32_t err = 0, pf = 0;
   bool gt1 = false;
   int lev = 0;
-  uint32_t q = r0;
+  uint32_t q = (uint32_t)root;
+  const uint32_t log2cap = (uint32_t)p.lv_slice_log2;
   while (true) {
-    const char* rec = at(q);
+    const char* rec = p.lv_rec + (size_t)(base[lev] + q) * p.lv_rec_bytes;
+    nvis++;                                    // (rays of the tile: rtx_tile_rays)
     const uint2 hdr = *reinterpret_cast<const uint2*>(rec);
     const double* lf = reinterpret_cast<const double*>(rec + 8);
     const double2 l01 = *reinterpret_cast<const double2*>(lf);   // the first leaf, with the header's sector
@@ -1338,11 +1271,17 @@ __device__ __forceinline__ V3 lv_tree_sum(At&& at, uint32_t r0, int nlev, uint32
     }
     const uint32_t nch = (uint32_t)__popc(hdr.x >> 16);
     if (nch && lev + 1 < nlev && sp < sd) {
-      const uint32_t c0 = hdr.y;               // the children's records: consecutive, in slot order
+      // the children's slot -> their dense index at level lev + 1
+      const uint32_t c0 = pex[(lev + 1) * 64 + (hdr.y >> log2cap)] + (hdr.y & ((1u << log2cap) - 1u));
       lo[sp * st] = c0;
       hi[sp * st] = c0 + nch;
       sp++;
-      if (PF) pf += *reinterpret_cast<const uint32_t*>(at(c0)) + *reinterpret_cast<const uint32_t*>(at(c0 + nch - 1));
+      // the children's records (contiguous, slot order) are fetched now, all
+      // at once: the walk's dependent chain becomes the tree's depth, not
+      // its size (the loads' values are consumed only at the end)
+      const char* r0 = p.lv_rec + (size_t)(base[lev + 1] + c0) * p.lv_rec_bytes;
+      pf += *reinterpret_cast<const uint32_t*>(r0) +
+            *reinterpret_cast<const uint32_t*>(r0 + (size_t)(nch - 1) * p.lv_rec_bytes);
     }
     // next: the last unvisited child of the deepest pending range (LIFO pop)
     while (sp > 0 && hi[(sp - 1) * st] == lo[(sp - 1) * st]) sp--;
@@ -1350,23 +1289,23 @@ __device__ __forceinline__ V3 lv_tree_sum(At&& at, uint32_t r0, int nlev, uint32
     q = --hi[(sp - 1) * st];
     lev = sp;
   }
-  if (PF) asm volatile("" : : "v"(pf));       // the prefetches' values, consumed
+  asm volatile("" : : "v"(pf));               // the prefetches' values, consumed
   err_out = err ? err : (gt1 ? (uint32_t)ERR_COLOR_GT1 : 0u);
   return sum;
 }
 
 // One camera sample's colour and first raise: its tree, or the lanes engine's
-// record when the sample was re-rendered (buffer overflow).
-template <bool PF, typename At>
-__device__ __forceinline__ V3 lv_sample(const KParams& p, At&& at, int item, int nlev, uint32_t* lo, uint32_t* hi,
-                                        int st, int sd, uint32_t& e) {
+// record when the sample overflowed the level buffers.
+__device__ __forceinline__ V3 lv_sample(const KParams& p, const uint32_t* base, const uint32_t* pex, int item,
+                                        int nlev, uint32_t* lo, uint32_t* hi, int st, int sd, uint32_t& e,
+                                        uint32_t& nvis) {
   const int r = p.lv_redo_of[item];
   if (r >= 0) {
     const double* q = p.lv_redo_smp + (size_t)r * 4;
     e = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
     return v3(q[0], q[1], q[2]);
   }
-  return lv_tree_sum<PF>(at, lv_rec0(p, (uint32_t)item), nlev, lo, hi, st, sd, e);
+  return lv_tree_sum(p, base, pex, item, nlev, lo, hi, st, sd, e, nvis);
 }
 
 // render_at's per-pixel stage of pass 0 (camera.rb:70-99) once a tile's
@@ -1421,101 +1360,260 @@ __device__ __forceinline__ void lv_tile_pixels(const KParams& p, const double* s
 }
 
 // Camera#render_at's reduction (camera.rb:70-99) of pass 0: one 256-thread
-// block per 8x8 tile of the batch (a record group).  The tile's trees are one
-// contiguous run of records (its group region, lv_grp records in use): when
-// they fit lv_fin_cap the block copies the run into LDS (coalesced 16-B loads,
-// several in flight per thread) and walks the trees there; else it walks them
-// in global memory.  The block's threads sum the tile's 64 x pre trees (item
-// order (pixel, sample)), park colour and raise in LDS, then 64 threads do the
-// pixels: mean in sample order, the variance test, then the pixel or
-// (max_sample_times > pre) an extra-list entry with the pre mean parked in
-// the output.  Dynamic LDS: SD * 2 words of walk stack per thread, 64 * pre
-// samples (28 B), then lv_fin_cap records.
-__host__ __device__ __forceinline__ size_t lv_fin_rec_off(int pre, int sd) {
-  return ((size_t)sd * 2 * 256 * 4 + (size_t)64 * pre * 28 + 15) & ~(size_t)15;
-}
-
+// block per 8x8 tile of the batch.  The block's threads sum the tile's
+// 64 x pre sample trees (item order (pixel, sample): a wave's trees are
+// neighbours), park colour and raise in LDS, then 64 threads do the pixels:
+// mean in sample order, the variance test, then the pixel or (max_sample_times
+// > pre) an extra-list entry with the pre mean parked in the output.
+// Dynamic LDS: nlev * 64 slice offsets, SD * 2 words of walk stack per thread,
+// then 64 * pre samples.
 template <int SD>
 __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
   extern __shared__ uint32_t lds_fin[];
+  uint32_t* pex = lds_fin;
   const unsigned long long ts0 = RTX_STAMPS ? stamp() : 0ull;   // RTX_STAMPS diagnostic build only
-  lv_stats(p, nlev);
-  const int pre = p.pre, rb = p.lv_rec_bytes;
-  uint32_t* lo = lds_fin + threadIdx.x;
+  __shared__ uint32_t trays;                   // the tile's rays (rtx_tile_rays)
+  if (threadIdx.x == 0) trays = 0;             // (lv_layout's barrier orders it before every add)
+  lv_layout(p, nlev, base, pex);               // once per block: every tile of the batch shares it
+  const unsigned long long ts1 = RTX_STAMPS ? stamp() : 0ull;
+  const int pre = p.pre;
+  uint32_t* lo = lds_fin + nlev * 64 + threadIdx.x;
   uint32_t* hi = lo + SD * 256;
-  double* scol = reinterpret_cast<double*>(lds_fin + (SD > 16 ? 0 : 2 * SD * 256));   // 64 * pre * 3
+  double* scol = reinterpret_cast<double*>(lds_fin + nlev * 64 + (SD > 16 ? 0 : 2 * SD * 256));   // 64 * pre * 3
   uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
-  char* lrec = reinterpret_cast<char*>(lds_fin) + lv_fin_rec_off(pre, SD > 16 ? 0 : SD);
   uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];  // deep trees: private stack
   const int n_items = 64 * pre;
-  // one block per tile, or (lv_fin_tiles > gridDim.x) a grid-stride loop over the batch's tiles
+  // one block per tile, or (lv_fin_tiles > gridDim.x) a grid-stride loop over
+  // the batch's tiles, so the layout above is read once per block
   const int n_tiles = p.lv_fin_tiles > (int)gridDim.x ? p.lv_fin_tiles : (int)gridDim.x;
-  unsigned long long tcopy = 0;
   for (int slot = blockIdx.x; slot < n_tiles; slot += gridDim.x) {
     const int item0 = slot * n_items;
-    const uint32_t g0 = (uint32_t)slot * p.lv_grp_cap;           // the tile's group region
-    const uint32_t used = min(p.lv_grp[slot], p.lv_grp_cap);
-    if (p.tile_rays && threadIdx.x == 0) p.tile_rays[p.lv_t0 + slot * p.lv_tstride] = used;   // (rtx_tile_rays)
-    const bool staged = (int)used <= p.lv_fin_cap;               // uniform
-    if (staged) {
-      const unsigned long long tc0 = RTX_STAMPS ? stamp() : 0ull;
-      const uint4* src = reinterpret_cast<const uint4*>(p.lv_rec + (size_t)g0 * rb);
-      uint4* dst = reinterpret_cast<uint4*>(lrec);
-      const int nq = (int)(used * (uint32_t)rb / 16);
-      int w = (int)threadIdx.x;
-      for (; w + 3 * 256 < nq; w += 4 * 256) {                   // 4 loads in flight per thread
-        const uint4 v0 = src[w], v1 = src[w + 256], v2 = src[w + 512], v3 = src[w + 768];
-        dst[w] = v0;
-        dst[w + 256] = v1;
-        dst[w + 512] = v2;
-        dst[w + 768] = v3;
-      }
-      for (; w < nq; w += 256) dst[w] = src[w];
-      __syncthreads();
-      if (RTX_STAMPS) tcopy += stamp() - tc0;
-    }
+    uint32_t nvis = 0;
     for (int it = (int)threadIdx.x; it < n_items; it += 256) {
       const ItemPos ip = decode_item(p, item0 + it);
       if (!ip.valid) continue;
       uint32_t e = 0;
-      V3 c;
-      if (staged) {                           // (a record in the spill arena is read where it is)
-        auto at = [&](uint32_t i) {
-          return i - g0 < used ? (const char*)lrec + (size_t)(i - g0) * rb : (const char*)p.lv_rec + (size_t)i * rb;
-        };
-        c = SD > 16 ? lv_sample<false>(p, at, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
-                    : lv_sample<false>(p, at, item0 + it, nlev, lo, hi, 256, SD, e);
-      } else {
-        auto at = [&](uint32_t i) { return (const char*)p.lv_rec + (size_t)i * rb; };
-        c = SD > 16 ? lv_sample<true>(p, at, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e)
-                    : lv_sample<true>(p, at, item0 + it, nlev, lo, hi, 256, SD, e);
-      }
+      const V3 c = SD > 16 ? lv_sample(p, base, pex, item0 + it, nlev, lo_p, hi_p, 1, LV_MAXL, e, nvis)
+                           : lv_sample(p, base, pex, item0 + it, nlev, lo, hi, 256, SD, e, nvis);
       scol[3 * it] = c.x;
       scol[3 * it + 1] = c.y;
       scol[3 * it + 2] = c.z;
       serr[it] = e;
     }
+    if (p.tile_rays) atomicAdd(&trays, nvis);
     __syncthreads();
+    if (p.tile_rays && threadIdx.x == 0) {    // rtx_tile_rays
+      p.tile_rays[p.lv_t0 + slot * p.lv_tstride] = trays;
+      trays = 0;
+    }
     lv_tile_pixels(p, scol, serr, slot);
-    __syncthreads();                           // scol / serr / the staged records are reused by the next tile
+    __syncthreads();                           // scol / serr / trays are reused by the next tile
   }
-  if (RTX_STAMPS) {                           // copy / whole block (wave lifetime parts), waves
+  if (RTX_STAMPS) {                           // layout / walks + pixels (wave lifetime parts), waves
     const unsigned long long ts2 = stamp();
     if (__lane_id() == 0) {
-      atomicAdd(&rtx_stamps[11], tcopy);
-      atomicAdd(&rtx_stamps[12], ts2 - ts0);
+      atomicAdd(&rtx_stamps[11], ts1 - ts0);
+      atomicAdd(&rtx_stamps[12], ts2 - ts1);
       atomicAdd(&rtx_stamps[13], 1ull);
     }
   }
+}
+
+// The same reduction with the tile's trees gathered into LDS first (option
+// lv_fin_cap > 0).  k_tree_finalize's walks are chains of dependent global
+// loads, one per visited record (the next record is known only once the
+// current one has arrived), and a wave runs as many steps as its largest
+// tree: the kernel spent ~80 % of its wave time waiting (r03k).  Here the
+// block copies its 64 x pre trees into LDS level by level: level 0 is the
+// tile's items, and level d + 1 is the children of level d, placed by a block
+// prefix count over the parents in LDS order (so a parent's children stay
+// contiguous and in slot order, as in the level queues) and loaded by the
+// parent's thread; every load of a level is in flight at once, so the
+// block waits nlev round trips in all.  Then each thread walks its trees in
+// LDS exactly as lv_tree_sum does (pre-order, children in reverse slot order,
+// the same additions in the same order: the same bits).  A tile whose trees
+// do not fit `cap` records falls back to the global walk (lv_tree_sum).
+//
+// Dynamic LDS: nlev * 64 slice offsets | 64 * pre colours (24 B) + raises
+// (4 B) | SD * 256 walk-stack words | cap first-child indices (u16) | cap
+// records (lv_rec_bytes each; the fallback's walk stacks alias them).
+__host__ __device__ __forceinline__ size_t lv_fin_g_rec_off(int nlev, int pre, int sd, int cap) {
+  const size_t o = (size_t)nlev * 64 * 4;
+  return (((o + 7) & ~(size_t)7) + (size_t)64 * pre * 28 + (size_t)sd * 256 * 4 + (size_t)cap * 2 + 15) &
+         ~(size_t)15;
+}
+
+// lv_tree_sum over the tree copied into LDS (record `root` of level 0).  The
+// pending child ranges (lo | hi << 16) are LDS words stk[k * 256], k < SD
+// (a register array indexed by the stack depth would live in scratch).
+template <int SD>
+__device__ __forceinline__ V3 lv_tree_sum_lds(const char* recs, const uint16_t* kid, uint32_t* stk, int rb, int root,
+                                              int nlev, uint32_t& err_out) {
+  int sp = 0;
+  V3 sum = v3(0.0, 0.0, 0.0);
+  uint32_t err = 0;
+  bool gt1 = false;
+  int lev = 0;
+  uint32_t q = (uint32_t)root;
+  while (true) {
+    const char* rec = recs + (size_t)q * rb;
+    const uint32_t hx = *reinterpret_cast<const uint32_t*>(rec);
+    const double* lf = reinterpret_cast<const double*>(rec + 8);
+    if (!err) err = hx & 0xffu;
+    const int nleaf = (int)(hx >> 8 & 0xffu);
+    for (int k = 0; k < nleaf; k++) {         // rt_reduce (ray_tracer.rb:292-298), in emission order
+      sum = vadd(sum, v3(lf[3 * k], lf[3 * k + 1], lf[3 * k + 2]));
+      if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) gt1 = true;
+    }
+    const uint32_t nch = (uint32_t)__popc(hx >> 16);
+    if (nch && lev + 1 < nlev && sp < SD) {
+      const uint32_t c0 = kid[q];
+      stk[sp * 256] = c0 | (c0 + nch) << 16;
+      sp++;
+    }
+    // next: the last unvisited child of the deepest pending range (LIFO pop)
+    uint32_t e = 0;
+    while (sp > 0) {
+      e = stk[(sp - 1) * 256];
+      if ((e & 0xffffu) != e >> 16) break;
+      sp--;
+    }
+    if (sp == 0) break;
+    e -= 1u << 16;
+    stk[(sp - 1) * 256] = e;
+    q = e >> 16;
+    lev = sp;
+  }
+  err_out = err ? err : (gt1 ? (uint32_t)ERR_COLOR_GT1 : 0u);
+  return sum;
+}
+
+template <int SD>
+__global__ __launch_bounds__(256) void k_tree_finalize_g(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
+  __shared__ uint32_t wpart[4];
+  extern __shared__ uint32_t lds_fin[];
+  uint32_t* pex = lds_fin;
+  const unsigned long long ts0 = RTX_STAMPS ? stamp() : 0ull;   // RTX_STAMPS diagnostic build only
+  lv_layout(p, nlev, base, pex);
+  const unsigned long long ts1 = RTX_STAMPS ? stamp() : 0ull;
+  const int pre = p.pre, cap = p.lv_fin_cap, rb = p.lv_rec_bytes;
+  const int n_items = 64 * pre;
+  const int item0 = blockIdx.x * n_items;
+  const int tid = (int)threadIdx.x, wave = tid >> 6, lane = (int)__lane_id();
+  char* lb = reinterpret_cast<char*>(lds_fin);
+  double* scol = reinterpret_cast<double*>(lb + (((size_t)nlev * 64 * 4 + 7) & ~(size_t)7));
+  uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
+  uint32_t* stk = serr + n_items + tid;
+  uint16_t* kid = reinterpret_cast<uint16_t*>(serr + n_items + SD * 256);
+  char* recs = lb + lv_fin_g_rec_off(nlev, pre, SD, cap);
+  const int nq = rb >> 4;                      // 16-B words per record
+  const uint32_t log2cap = (uint32_t)p.lv_slice_log2, smask = (1u << log2cap) - 1u;
+  bool fits = n_items <= cap;
+  // ---- level 0: the tile's items (padding and re-rendered samples: no tree)
+  if (fits) {
+    for (int it = tid; it < n_items; it += 256) {
+      const int item = item0 + it;
+      uint4* dst = reinterpret_cast<uint4*>(recs + (size_t)it * rb);
+      if (decode_item(p, item).valid && p.lv_redo_of[item] < 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(p.lv_rec + (size_t)(base[0] + item) * rb);
+        for (int w = 0; w < nq; w++) dst[w] = src[w];
+      } else {
+        dst[0] = make_uint4(0u, 0u, 0u, 0u);   // no leaves, no children
+      }
+    }
+  }
+  __syncthreads();
+  // ---- level d + 1: the children of level d's records [lo, hi)
+  int lo = 0, hi = n_items;
+  for (int d = 0; fits && d + 1 < nlev; d++) {
+    const int n = hi - lo;
+    const int m = (n + 255) >> 8;              // parents per thread, a contiguous run
+    const int a = lo + tid * m, b = min(a + m, hi);
+    uint32_t cnt = 0;
+    for (int k = a; k < b; k++) cnt += (uint32_t)__popc(*reinterpret_cast<const uint32_t*>(recs + (size_t)k * rb) >> 16);
+    const uint32_t incl = wave_scan_incl(cnt);
+    if (lane == 63) wpart[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const uint32_t v = wpart[w];
+      before += w < wave ? v : 0u;
+      total += v;
+    }
+    __syncthreads();                           // wpart is reused by the next level
+    if (total == 0) break;
+    if (hi + (int)total > cap) {               // uniform: the tile's trees do not fit
+      fits = false;
+      break;
+    }
+    uint32_t pos = (uint32_t)hi + before + incl - cnt;
+    for (int k = a; k < b; k++) {
+      const uint2 hdr = *reinterpret_cast<const uint2*>(recs + (size_t)k * rb);
+      const uint32_t nch = (uint32_t)__popc(hdr.x >> 16);
+      kid[k] = (uint16_t)pos;
+      if (!nch) continue;
+      // the children's slot -> their dense index at level d + 1 (as lv_tree_sum)
+      const uint32_t c0 = pex[(d + 1) * 64 + (hdr.y >> log2cap)] + (hdr.y & smask);
+      const uint4* src = reinterpret_cast<const uint4*>(p.lv_rec + (size_t)(base[d + 1] + c0) * rb);
+      uint4* dst = reinterpret_cast<uint4*>(recs + (size_t)pos * rb);
+      for (uint32_t w = 0; w < nch * (uint32_t)nq; w++) dst[w] = src[w];
+      pos += nch;
+    }
+    __syncthreads();
+    lo = hi;
+    hi += (int)total;
+  }
+  const unsigned long long tsg = RTX_STAMPS ? stamp() : 0ull;
+  // ---- the sums, in trace_sync's order
+  uint32_t* slo = reinterpret_cast<uint32_t*>(recs) + tid;   // fallback walk stacks (alias the records)
+  uint32_t* shi = slo + SD * 256;
+  if (!fits) __syncthreads();                  // every thread is past its last read of the records
+  for (int it = tid; it < n_items; it += 256) {
+    const int item = item0 + it;
+    if (!decode_item(p, item).valid) continue;
+    uint32_t e = 0;
+    V3 c;
+    const int r = p.lv_redo_of[item];
+    if (r >= 0) {
+      const double* q = p.lv_redo_smp + (size_t)r * 4;
+      e = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
+      c = v3(q[0], q[1], q[2]);
+    } else if (fits) {
+      c = lv_tree_sum_lds<SD>(recs, kid, stk, rb, it, nlev, e);
+    } else {
+      uint32_t nv = 0;
+      c = lv_tree_sum(p, base, pex, item, nlev, slo, shi, 256, SD, e, nv);
+    }
+    scol[3 * it] = c.x;
+    scol[3 * it + 1] = c.y;
+    scol[3 * it + 2] = c.z;
+    serr[it] = e;
+  }
+  if (RTX_STAMPS) {                           // layout / gather + walks, waves; gather part in [14]
+    const unsigned long long ts2 = stamp();
+    if (__lane_id() == 0) {
+      atomicAdd(&rtx_stamps[11], ts1 - ts0);
+      atomicAdd(&rtx_stamps[12], ts2 - ts1);
+      atomicAdd(&rtx_stamps[13], 1ull);
+      atomicAdd(&rtx_stamps[14], tsg - ts1);
+    }
+  }
+  __syncthreads();
+  lv_tile_pixels(p, scol, serr, blockIdx.x);
 }
 
 // Pass 1: one thread per extra-list entry of the batch: (pre mean * pre +
 // the extra samples in order) / max_sample_times.
 template <int SD>
 __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev) {
+  __shared__ uint32_t base[LV_MAXL + 1];
   extern __shared__ uint32_t lds_fin[];
-  lv_stats(p, nlev);
-  uint32_t* lo = lds_fin + threadIdx.x;
+  uint32_t* pex = lds_fin;
+  lv_layout(p, nlev, base, pex);
+  uint32_t* lo = lds_fin + nlev * 64 + threadIdx.x;
   uint32_t* hi = lo + SD * 256;
   uint32_t lo_p[SD > 16 ? LV_MAXL : 1], hi_p[SD > 16 ? LV_MAXL : 1];
   const int t = blockIdx.x * 256 + (int)threadIdx.x;
@@ -1526,17 +1624,16 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
   const CameraDev& cam = *p.cam;
   if (y >= cam.height) return;
   const int x = p.x0 + px_;
-  const int pre = p.pre, n_extra = p.max_samples - pre, rb = p.lv_rec_bytes;
+  const int pre = p.pre, n_extra = p.max_samples - pre;
   double* o = p.out + (size_t)row * p.stride + (size_t)px_ * 3;
   const V3 avg = v3(o[0], o[1], o[2]);         // the pre mean parked by pass 0
   V3 cv = v3(0.0, 0.0, 0.0);
   uint32_t err = 0;
-  auto at = [&](uint32_t i) { return (const char*)p.lv_rec + (size_t)i * rb; };
   for (int j = 0; j < n_extra; j++) {
-    uint32_t e = 0;
+    uint32_t e = 0, nv = 0;
     const int item = t * n_extra + j;
-    cv = vadd(cv, SD > 16 ? lv_sample<true>(p, at, item, nlev, lo_p, hi_p, 1, LV_MAXL, e)
-                          : lv_sample<true>(p, at, item, nlev, lo, hi, 256, SD, e));
+    cv = vadd(cv, SD > 16 ? lv_sample(p, base, pex, item, nlev, lo_p, hi_p, 1, LV_MAXL, e, nv)
+                          : lv_sample(p, base, pex, item, nlev, lo, hi, 256, SD, e, nv));
     if (!err) err = e;
   }
   const V3 r = vdiv(vadd(vsc(avg, (double)pre), cv), (double)p.max_samples);
@@ -1596,7 +1693,7 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p) {
 }
 
 static hipError_t launch_hl_raise(const KParams& q, hipStream_t s) {
-  if (q.scene.n_light == 0 || !q.lv_hlq) return hipSuccess;   // (the hl and, with exact_raises, the xr list)
+  if (q.scene.n_light == 0 || !q.lv_hlq) return hipSuccess;
   const size_t lds = (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
   int cus = 0, per_cu = 0;
   hipError_t e = launch_fit(reinterpret_cast<const void*>(k_hl_raise), 256, lds, cus, per_cu);
@@ -1628,7 +1725,6 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
     p.lv_ctl->dropped = 0;
     p.lv_ctl->hl_n = 0;
     p.lv_ctl->xr_n = 0;
-    p.lv_ctl->spill_n = 0;
     p.lv_ctl->lay_base[0] = 0;
     p.lv_ctl->lay_base[1] = v;
   }
@@ -1644,10 +1740,6 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
     (&p.lv_ctl->sc[0][0])[w] = 0;
     (&p.lv_ctl->sh[0][0])[w] = 0;
   }
-  // every group region starts with its level-0 records (the last group may be partial: its unused
-  // level-0 slots are never read)
-  const int ngrp = (n0_max + (int)p.lv_grp_items - 1) / (int)p.lv_grp_items;
-  for (int w = t; w < ngrp; w += nt) p.lv_grp[w] = p.lv_grp_items;
   const int cwords = (nlev < LV_MAXL + 1 ? nlev : LV_MAXL + 1) * LV_CLAIMS * 32;
   for (int w = t; w < cwords; w += nt)
     for (int k = 0; k < 3; k++) (&p.lv_ctl->claim[k][0][0])[w] = 0;
@@ -1791,18 +1883,11 @@ static hipError_t launch_shade(const KParams& p, int level, long cap_items, hipS
 }
 
 template <int SD>
-static hipError_t launch_finalize_sd(KParams q, int nlev, int n, hipStream_t s) {
-  const size_t stack = SD > 16 ? 0 : (size_t)SD * 2 * 256 * 4;
+static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStream_t s) {
+  const size_t stack = (size_t)nlev * 64 * 4 + (SD > 16 ? 0 : (size_t)SD * 2 * 256 * 4);
   if (q.lv_pass == 0) {                        // n = tiles of the batch
-    // a tile's run of records staged in LDS when it has at most lv_fin_cap
-    // records (capped to what fits one block next to its stacks and samples)
-    const size_t off = lv_fin_rec_off(q.pre, SD > 16 ? 0 : SD);
-    const size_t room = off < LDS_TOTAL_BYTES - 1024 ? (LDS_TOTAL_BYTES - 1024 - off) / (size_t)q.lv_rec_bytes : 0;
-    q.lv_fin_cap = (int32_t)std::min<size_t>((size_t)std::max(0, q.lv_fin_cap), room);
-    const size_t lds = off + (size_t)q.lv_fin_cap * q.lv_rec_bytes;
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tree_finalize<SD>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const size_t lds = ((stack + 7) & ~(size_t)7) + (size_t)64 * q.pre * 28;
+    KParams r = q;
     long grid = n;
     if (q.lv_fin_tiles > 0) {                  // lv_fin_grid blocks per CU, grid-stride over the tiles
       int dev = 0, cus = 0;
@@ -1810,17 +1895,44 @@ static hipError_t launch_finalize_sd(KParams q, int nlev, int n, hipStream_t s) 
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
         grid = std::min<long>(n, (long)cus * q.lv_fin_tiles);
     }
-    q.lv_fin_tiles = n;
-    hipLaunchKernelGGL(k_tree_finalize<SD>, dim3((unsigned)grid), dim3(256), lds, s, q, nlev);
+    r.lv_fin_tiles = n;
+    hipLaunchKernelGGL(k_tree_finalize<SD>, dim3((unsigned)grid), dim3(256), lds, s, r, nlev);
   } else {                                     // n = extra-list entries of the batch
     hipLaunchKernelGGL(k_tree_finalize_extra<SD>, dim3((unsigned)((n + 255) / 256)), dim3(256), stack, s, q, nlev);
   }
   return hipGetLastError();
 }
 
+// Pass 0 with the trees gathered into LDS (lv_fin_cap > 0; register walk
+// stacks of SD entries, nlev - 1 <= SD).
+template <int SD>
+static hipError_t launch_finalize_g(KParams q, int nlev, int n, hipStream_t s) {
+  // at most as many records as fit a CU's LDS next to the rest
+  // (the kernel's static LDS, and 16 B for the alignment of the record area)
+  hipFuncAttributes fa{};
+  size_t stat = 16 * 1024;
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_tree_finalize_g<SD>)) == hipSuccess)
+    stat = fa.sharedSizeBytes;
+  const size_t fixed = lv_fin_g_rec_off(nlev, q.pre, SD, 0) + stat + 16;
+  const long fit = fixed < LDS_TOTAL_BYTES ? (long)((LDS_TOTAL_BYTES - fixed) / (q.lv_rec_bytes + 2)) : 0;
+  q.lv_fin_cap = (int32_t)std::min<long>(q.lv_fin_cap, fit);
+  const size_t recs = (size_t)q.lv_fin_cap * q.lv_rec_bytes;
+  const size_t lds = lv_fin_g_rec_off(nlev, q.pre, SD, q.lv_fin_cap) + std::max(recs, (size_t)SD * 2 * 256 * 4);
+  if (lds + stat > LDS_TOTAL_BYTES) return launch_finalize_sd<16>(q, nlev, n, s);   // (pre too large: the walk)
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tree_finalize_g<SD>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_tree_finalize_g<SD>, dim3((unsigned)n), dim3(256), lds, s, q, nlev);
+  return hipGetLastError();
+}
+
 static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t s) {
+  if (q.lv_pass == 0 && q.lv_fin_cap > 0) {
+    if (nlev <= 5) return launch_finalize_g<4>(q, nlev, n, s);
+    if (nlev <= 9) return launch_finalize_g<8>(q, nlev, n, s);
+  }
   // a walk keeps one pending child range per level below the root: nlev - 1
-  // entries; the smaller stack lets more blocks share a CU
+  // entries; the smaller stack lets 8 blocks share a CU (C2, depth 5) instead of 6
   if (nlev <= 5) return launch_finalize_sd<4>(q, nlev, n, s);
   if (nlev <= 8) return launch_finalize_sd<8>(q, nlev, n, s);
   if (nlev <= 16) return launch_finalize_sd<16>(q, nlev, n, s);

@@ -427,7 +427,7 @@ def test_two_streams_c2_full_frame_and_kernel_time(gpu):
     assert launches == 10 and 0.5 < ms < 50.0, (ms, launches)   # union of the two halves' level launches
 
 
-# ---- tree reduction with a tile's run of records staged in LDS (option lv_fin_cap)
+# ---- tree reduction with the tile's trees gathered into LDS (option lv_fin_cap)
 @pytest.mark.parametrize("world,camera,ov", [
     ("c2_world.yml", "c2_camera.yml", dict(width=120, height=70)),
     ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, monte_carlo_diffusion_times=3, trace_depth=6)),
@@ -435,11 +435,9 @@ def test_two_streams_c2_full_frame_and_kernel_time(gpu):
                                              variant_threshold=0.0)),
 ])
 def test_gathered_reduction_changes_no_bit(gpu, world, camera, ov):
-    """lv_fin_cap: a tile's records staged in LDS when at most this many (1024,
-    the default), every tile staged (4096, capped to what LDS holds), caps that
-    make some or every tile walk its records in global memory (300, 100: below
-    a tile's own level-0 records), and the global walk alone (0) render the
-    same bits as the lanes engine."""
+    """lv_fin_cap: LDS gather (default), a cap that makes some tiles fall back
+    to the global walk, one below a tile's level 0 (every tile falls back), and
+    the global walk alone (0) render the same bits as the lanes engine."""
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=4)
     for cap in (1024, 4096, 300, 100, 0):

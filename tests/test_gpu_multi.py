@@ -110,7 +110,7 @@ def test_lpt_tile_lists_reassemble_bit_exactly(gpu):
     r = Renderer(sd, cd, device=0)
     full = r.render(seed=1)
     rays = r.tile_rays()
-    assert rays.shape == (23, 40) and rays.min() >= 256    # at least each tile's level-0 records
+    assert rays.shape == (23, 40) and rays.min() > 0       # every tile traced its camera samples at least
     for n in (3, 8):
         plan = lpt_plan(row_tile_costs(rays, 8), n)
         rows = len(plan[0]) * 8
