@@ -948,8 +948,9 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // has its sample re-rendered by the lanes engine (option lv_hl_cap: the size)
   const size_t hlcap = c->opt_lv_hl_cap > 0 ? (size_t)c->opt_lv_hl_cap : std::max<size_t>(4096, lcap / 256);
   const size_t sz_hlq = al256(hlcap * 64);
-  // exact_raises: the shading hits whose covers' raises k_hl_raise checks (1/4 of the records; overflow re-renders)
-  const size_t xrcap = c->opt_exact_raises ? std::max<size_t>(4096, lcap / 4) : 0;
+  // exact_raises: the shading hits whose covers' raises k_hl_raise checks, at most one per record (with
+  // 1/4 of the records C4's deep levels overflowed: 15 M samples re-rendered, 49 s per frame, r07g)
+  const size_t xrcap = c->opt_exact_raises ? std::max<size_t>(4096, lcap) : 0;
   const size_t sz_xrq = al256(xrcap * 32);
   const size_t sz_ctl = al256(sizeof(LevelCtl)), sz_redo = al256(n0 * 4), sz_smp = al256(n0 * 32),
                sz_stage = al256(scap * RAY_BYTES), sz_rec = al256(lcap * (size_t)rec_bytes),
