@@ -294,14 +294,19 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
 /* read-only key: "engine_effective" (the engine the next render of the uploaded scene and camera runs:
          "engine", except that the bounce-level engine falls back to the lanes engine for trace_depth > 64,
          monte_carlo_diffusion_times > 14 or more than 255 lights), "lv_ray_bytes_effective" (80 or 96: the
-         staged ray record of the next bounce-level render).
+         staged ray record of the next bounce-level render), "sph_mode_effective" (where the next bounce-level
+         render's walks read the spheres: 0 linear walk, records in LDS; 1 linear, scalar loads; 2 hierarchy in
+         LDS; 3 hierarchy by scalar loads; 4 nodes in LDS, leaf records global; 5 hierarchy and exact records in
+         LDS; 6 nodes and 16-bit leaf records in LDS).
    keys: "bvh" (0 ordered linear walk, 1 hierarchy from "bvh_min" spheres,
          2 always; every choice renders the same bits), "bvh_min" [32], "bvh_sah" (1 [default] binned-SAH hierarchy
          unless it would not fit LDS where the median one does, 0 median; at the next upload), "sphere_src" (0 LDS
          staging, 1 scalar loads, 2 hierarchy nodes in LDS and leaf records from global memory, 3 the hierarchy and
-         the binary64 records of the exact sphere test in LDS (2 and 3: bounce-level engine; the lanes engine
-         stages as 0), -1 [default] auto: 3 when that and the hit ring fit LDS, 2 for a hierarchy whose staging leaves
-         no LDS for a hit ring, else 0;
+         the binary64 records of the exact sphere test in LDS, 4 the nodes and 16-bit quantized leaf records in LDS
+         with 16-bit traversal stacks (2, 3 and 4: bounce-level engine; the lanes engine stages as 0; 4 falls back
+         to 2 when the scene's records cannot be quantized conservatively), -1 [default] auto: 3 when that and the
+         hit ring fit LDS, 0 when the hierarchy and a hit ring do, else 4 when that and the compact hit ring fit,
+         else 2 when the nodes and the compact ring fit, else 0;
          every choice renders the same bits), "lds_stack" (ray-stack entries per lane kept in LDS,
          -1 = as many as fit), "force_stack" (per-lane ray-stack bucket), "postpone" (hierarchy walks
          still running in fewer lanes of a wave than this are postponed; -1 [default] = 16 from 64 nodes, 0 never), "tile_order" (1 expensive

@@ -70,7 +70,8 @@ struct rtx_context {
   int64_t opt_bvh = 1;               // 0: ordered linear walk; 1: hierarchy from opt_bvh_min spheres; 2: always
   int64_t opt_bvh_sah = RTX_BVH_SAH;  // hierarchy splits: 1 binned SAH, 0 median (applies at the next upload)
   int64_t opt_bvh_min = 32;         // C2 (64 spheres): hierarchy 16.0 ms vs ordered walk 17.8 ms
-  int64_t opt_sphere_src = -1;       // 0: LDS staging (measured faster), 1: scalar loads, 2: nodes LDS + leaves global, -1 auto
+  int64_t opt_sphere_src = -1;       // 0: LDS staging (measured faster), 1: scalar loads, 2: nodes LDS + leaves global,
+                                     // 3: + exact records in LDS, 4: quantized leaves in LDS, -1 auto
   int64_t opt_postpone = -1;         // query_bvh postponing threshold in lanes (-1: auto by hierarchy size)
   int64_t opt_tile_order = -1;       // 1: expensive tiles first (k_tile_cost/k_tile_sort), 0: natural order, -1: auto
   int64_t opt_lds_stack = 0;         // ray-stack entries per lane in LDS (-1: as many as fit; 0 measured fastest)
@@ -418,11 +419,20 @@ void rtx_context_destroy(rtx_context* c) {
 
 static bool levels_engine(const rtx_context* c);
 static bool lv_paths32(const rtx_context* c);
+static int sph_mode(const rtx_context* c);
 
 rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
   if (!c || !key || !value) return RTX_EINVAL;
   if (!strcmp(key, "engine_effective")) {   // read-only: the engine the next render of this camera runs
     *value = c->have_cam && c->have_scene ? (levels_engine(c) ? 1 : 0) : c->opt_engine;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "sph_mode_effective")) {   // read-only: the SphMode of the next bounce-level render's walks
+    if (!c->have_scene) return fail(c, RTX_EINVAL, "sph_mode_effective: no scene uploaded");
+    const int m = c->opt_sphere_src == -1
+                      ? levels_auto_mode(c->scene, sph_mode(c), (int)c->opt_lv_compact, (int)c->opt_lv_split)
+                      : sph_mode(c);
+    *value = resolve_mode(c->scene, m);
     return RTX_OK;
   }
   if (!strcmp(key, "lv_ray_bytes_effective")) {   // read-only: the staged ray record of the next level render
@@ -562,8 +572,9 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_kernel_events = value != 0;
     return RTX_OK;
   }
-  if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads; 2: hierarchy nodes in LDS, leaves global; -1 auto
-    if (value < -1 || value > 3) return fail(c, RTX_EINVAL, "sphere_src must be -1, 0, 1, 2 or 3");
+  if (!strcmp(key, "sphere_src")) {        // 0: LDS staging; 1: scalar loads; 2: hierarchy nodes in LDS, leaves global;
+                                           // 3: + exact records in LDS; 4: quantized leaf records in LDS; -1 auto
+    if (value < -1 || value > 4) return fail(c, RTX_EINVAL, "sphere_src must be -1, 0, 1, 2, 3 or 4");
     c->opt_sphere_src = value;
     return RTX_OK;
   }
@@ -591,6 +602,70 @@ static void put_plane(std::vector<double>& g, V3 P, V3 F, V3 U, double uu, doubl
   put3(g, vnorm(U, err));
   g.push_back(uu);
   g.push_back(vu);
+}
+
+// 16-bit pre-test records of the hierarchy's leaves (SPH_BVH_QLDS, DESIGN.md
+// §3.15): per leaf 8 words, {x 0..3}, {y 0..3}, {z 0..3}, {r 0..3} as 16-bit
+// pairs (slot u in the low half of word 2k for u = 0, 2).  The device decodes
+// center axis a as fmaf(q, step[a], org[a]) and the radius as q * rstep, in
+// float32, the operations repeated here: a decoded center lies e from the true
+// one (exact, in binary64) and the decoded radius is at least R + e, so the
+// decoded ball holds the true one and the §2.1 pre-test stays conservative;
+// its "wholly behind" half also needs e below half its margin (m S).
+struct QuantLeaves {
+  std::vector<uint32_t> rec;
+  float org[3] = {0.0f, 0.0f, 0.0f}, step[3] = {1.0f, 1.0f, 1.0f}, rstep = 1.0f;
+  bool ok = false;
+  double max_err = 0.0;
+};
+
+static QuantLeaves quantize_leaves(const Bvh4Builder& bb, float sph_scale) {
+  QuantLeaves ql;
+  const size_t n_slots = bb.slot64.size();
+  ql.rec.assign(n_slots * 2, 0u);
+  double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  for (const Sphere64& s : bb.slot64) {
+    if (!(s.r >= 0.0)) continue;                  // padding slot
+    for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], s.c[a]), hi[a] = std::max(hi[a], s.c[a]);
+  }
+  if (!(lo[0] <= hi[0])) return ql;               // no spheres
+  for (int a = 0; a < 3; a++) {
+    ql.org[a] = (float)lo[a];
+    const float st = (float)((hi[a] - lo[a]) / 65535.0 * (1.0 + 1e-6));
+    ql.step[a] = st > 0.0f ? st : 1.0f;
+  }
+  std::vector<double> grown(n_slots, 0.0);        // R + e per slot
+  double max_r = 0.0;
+  for (size_t k = 0; k < n_slots; k++) {
+    const Sphere64& s = bb.slot64[k];
+    if (!(s.r >= 0.0)) continue;
+    double e2 = 0.0;
+    for (int a = 0; a < 3; a++) {
+      double qd = std::nearbyint((s.c[a] - (double)ql.org[a]) / (double)ql.step[a]);
+      qd = std::min(65535.0, std::max(0.0, qd));
+      const uint32_t qv = (uint32_t)qd;
+      const double dec = (double)std::fmaf((float)qv, ql.step[a], ql.org[a]);
+      e2 += (dec - s.c[a]) * (dec - s.c[a]);
+      const size_t w = (k / BVH_LEAF) * 8 + (size_t)a * 2 + (k % BVH_LEAF) / 2;
+      ql.rec[w] |= qv << (16 * (k % 2));
+    }
+    const double e = std::sqrt(e2) * (1.0 + 1e-9);
+    ql.max_err = std::max(ql.max_err, e);
+    grown[k] = (s.r + e) * (1.0 + 1e-12);
+    max_r = std::max(max_r, grown[k]);
+  }
+  if (!std::isfinite(max_r)) return ql;
+  ql.rstep = max_r > 0.0 ? (float)(max_r / 65535.0 * (1.0 + 1e-6)) : 1.0f;
+  for (size_t k = 0; k < n_slots; k++) {
+    if (!(bb.slot64[k].r >= 0.0)) continue;
+    double qd = std::ceil(grown[k] / (double)ql.rstep);
+    while (qd <= 65535.0 && (double)((float)qd * ql.rstep) < grown[k]) qd += 1.0;
+    if (qd > 65535.0) return ql;
+    const size_t w = (k / BVH_LEAF) * 8 + 6 + (k % BVH_LEAF) / 2;
+    ql.rec[w] |= (uint32_t)qd << (16 * (k % 2));
+  }
+  ql.ok = ql.max_err <= 0.5 * CULL_M * (double)sph_scale;
+  return ql;
 }
 
 rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
@@ -705,6 +780,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
     }
   }
   const Bvh4Builder& bb = *bbp;
+  const QuantLeaves ql = quantize_leaves(bb, sph_scale);
   for (int k = 0; k < 16; k++) sph32.push_back(0.0f);   // 4 padding records: group loads stay in bounds
   std::vector<LightDev> lights(sd->n_lights);
   for (int i = 0; i < sd->n_lights; i++) {
@@ -760,6 +836,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   HIPCHK(c, up(bb.nodes.data(), bb.nodes.size() * sizeof(Bvh4Node), &ptr)); S.bvh = (const Bvh4Node*)ptr;
   HIPCHK(c, up(bb.slot32.data(), bb.slot32.size() * sizeof(float), &ptr)); S.bvh_sph32 = (const float*)ptr;
   HIPCHK(c, up(bb.slot64.data(), bb.slot64.size() * sizeof(Sphere64), &ptr)); S.bvh_sph64 = (const Sphere64*)ptr;
+  HIPCHK(c, up(ql.rec.data(), ql.rec.size() * sizeof(uint32_t), &ptr)); S.bvh_q = (const uint32_t*)ptr;
   HIPCHK(c, up(bb.slot_obj.data(), bb.slot_obj.size() * sizeof(int32_t), &ptr)); S.bvh_obj = (const int32_t*)ptr;
   HIPCHK(c, up(sph_obj.data(), sph_obj.size() * sizeof(int32_t), &ptr)); S.sph_obj = (const int32_t*)ptr;
   HIPCHK(c, up(lights.data(), lights.size() * sizeof(LightDev), &ptr));  S.light = (const LightDev*)ptr;
@@ -779,6 +856,9 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   S.sse = sd->soft_shadow_exponent;
   S.sph_scale = sph_scale;
   S.sse_is_two = sd->soft_shadow_exponent == 2.0;     // glibc pow(x, 2.0) == x*x
+  for (int a = 0; a < 3; a++) S.q_org[a] = ql.org[a], S.q_step[a] = ql.step[a];
+  S.q_rstep = ql.rstep;
+  S.q_ok = ql.ok && S.n_nodes <= 32767 && (int64_t)S.n_slots <= 32767;   // references fit int16 stack entries
   HIPCHK(c, hipMemcpy(c->d_scene, &S, sizeof S, hipMemcpyHostToDevice));
   c->have_scene = true;
   return RTX_OK;
@@ -841,7 +921,8 @@ static int required_stack(const rtx_context* c) {
 static int sph_mode(const rtx_context* c) {
   const bool bvh = c->opt_bvh == 2 || (c->opt_bvh == 1 && c->scene.n_sphere >= c->opt_bvh_min);
   if (bvh && c->scene.bvh_root != BVH_NONE)
-    return c->opt_sphere_src == 3   ? SPH_BVH_LDSX
+    return c->opt_sphere_src == 4   ? SPH_BVH_QLDS
+           : c->opt_sphere_src == 3 ? SPH_BVH_LDSX
            : c->opt_sphere_src == 2 ? SPH_BVH_MIX
            : c->opt_sphere_src == 1 ? SPH_BVH_GLOBAL
                                     : SPH_BVH_LDS;
@@ -1039,9 +1120,9 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   KernelEvents kev{c->ev, 0, rtx_context::MAX_EV};
   if (c->opt_kernel_events && !c->ev[0])
     for (int k = 0; k < 2 * rtx_context::MAX_EV; k++) HIPCHK(c, hipEventCreate(&c->ev[k]));
-  // sphere_src auto: C4-sized hierarchies keep their nodes in LDS and read
-  // their leaves from global memory, which leaves room for the hit rings
-  // (r05b: C4 410 -> 386 ms, same bits)
+  // sphere_src auto: C4-sized hierarchies keep their nodes and 16-bit leaf
+  // records in LDS next to the hit rings (SPH_BVH_QLDS; before round 4 the
+  // leaves came from global memory, SPH_BVH_MIX, r05b: C4 410 -> 386 ms)
   const int mode = c->opt_sphere_src == -1 ? levels_auto_mode(c->scene, sph_mode(c), (int)c->opt_lv_compact,
                                                               (int)c->opt_lv_split)
                                            : sph_mode(c);

@@ -15,7 +15,6 @@ namespace rtx {
 
 constexpr double PI = 3.141592653589793;   // Math::PI == M_PI
 constexpr double EPS = 1e-5;               // Alex::EPSILON (src/libs/algebra.rb:2)
-constexpr float CULL_M = 2e-5f;            // pre-test margin (exact culls)
 typedef float F2 __attribute__((ext_vector_type(2)));   // packed FP32 pair (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32)
 
 struct Ray {
@@ -525,6 +524,42 @@ __device__ __forceinline__ void walk_planes_boxes(const SceneDev& S, bool ext, V
   }
 }
 
+// A leaf's 4 pre-test records as {x0..x3}, {y0..y3}, {z0..z3}, {R^2 0..3}:
+// float32 records (LDS or global), or the 16-bit records of SPH_BVH_QLDS
+// decoded with the host's operations (quantize_leaves in rtx_capi.cpp: a
+// decoded ball holds the true one).
+struct QLeaf {
+  const uint4* q;            // 2 per leaf
+  float ox, oy, oz, sx, sy, sz, rs;
+};
+
+// SPH_BVH_QLDS's 16-bit traversal stacks (stride BS entries): lane l of a wave
+// owns the low (l < 32) or high half of dword l mod 32 of each 128-B row, so
+// each 32-lane group of a stack access meets 32 banks.
+__device__ __forceinline__ int16_t* qstack(char* lds, const KParams& p) {
+  const int t = (int)threadIdx.x;
+  return reinterpret_cast<int16_t*>(lds + p.lds_stack) + (t & ~63) + ((t & 31) << 1) + ((t >> 5) & 1);
+}
+
+__device__ __forceinline__ void leaf_records(const float4* l, int v, float4& cx, float4& cy, float4& cz, float4& cw) {
+  const int slot0 = (v >> 2) * BVH_LEAF;
+  cx = l[slot0], cy = l[slot0 + 1], cz = l[slot0 + 2], cw = l[slot0 + 3];
+}
+
+__device__ __forceinline__ void leaf_records(const QLeaf& l, int v, float4& cx, float4& cy, float4& cz, float4& cw) {
+  const uint4 a = l.q[(v >> 2) * 2], b = l.q[(v >> 2) * 2 + 1];
+  auto lo = [](uint32_t w) { return (float)(w & 0xffffu); };
+  auto hi = [](uint32_t w) { return (float)(w >> 16); };
+  cx = make_float4(__builtin_fmaf(lo(a.x), l.sx, l.ox), __builtin_fmaf(hi(a.x), l.sx, l.ox),
+                   __builtin_fmaf(lo(a.y), l.sx, l.ox), __builtin_fmaf(hi(a.y), l.sx, l.ox));
+  cy = make_float4(__builtin_fmaf(lo(a.z), l.sy, l.oy), __builtin_fmaf(hi(a.z), l.sy, l.oy),
+                   __builtin_fmaf(lo(a.w), l.sy, l.oy), __builtin_fmaf(hi(a.w), l.sy, l.oy));
+  cz = make_float4(__builtin_fmaf(lo(b.x), l.sz, l.oz), __builtin_fmaf(hi(b.x), l.sz, l.oz),
+                   __builtin_fmaf(lo(b.y), l.sz, l.oz), __builtin_fmaf(hi(b.y), l.sz, l.oz));
+  const float r0 = lo(b.z) * l.rs, r1 = hi(b.z) * l.rs, r2 = lo(b.w) * l.rs, r3 = hi(b.w) * l.rs;
+  cw = make_float4(r0 * r0, r1 * r1, r2 * r2, r3 * r3);
+}
+
 // One leaf (reference lf < 0): the §2.1 pre-test of its spheres, the exact
 // test for those not ruled out, then the nearest-hit update or the cover list.
 template <int BS, typename LP, typename XP, typename OP>
@@ -535,10 +570,10 @@ __device__ __forceinline__ void walk_leaf(int lf, LP leaf4, XP x64, OP xobj, con
   const int v = ~lf;
   const int slot0 = (v >> 2) * BVH_LEAF;
   const int cnt = (v & 3) + 1;
-  // the leaf's 4 records as {x0..x3}, {y0..y3}, {z0..z3}, {R^2 0..3}: the
-  // pre-test of §2.1 on two spheres per packed FP32 instruction (the same
+  // the pre-test of §2.1 on two spheres per packed FP32 instruction (the same
   // operations as the per-sphere form in query())
-  const float4 cx = leaf4[slot0], cy = leaf4[slot0 + 1], cz = leaf4[slot0 + 2], cw = leaf4[slot0 + 3];
+  float4 cx, cy, cz, cw;
+  leaf_records(leaf4, v, cx, cy, cz, cw);
   uint32_t keep = 0;
   const F2 po = {s.ox, s.ox}, poy = {s.oy, s.oy}, poz = {s.oz, s.oz};
   const F2 pdx = {s.dx, s.dx}, pdy = {s.dy, s.dy}, pdz = {s.dz, s.dz}, pdd = {s.dd, s.dd};
@@ -604,8 +639,8 @@ __device__ __forceinline__ void walk_covers(const SceneDev& S, V3 o, V3 d, V3 L,
 // resume = true; meanwhile the wave's other lanes shade and start new
 // queries instead of idling.  Every lane visits the same nodes and leaves in
 // the same order either way, so the result is unchanged.
-template <int BS, bool PP, typename NP, typename LP, typename XP, typename OP>
-__device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4, XP x64, OP xobj, int* stk, int* ci,
+template <int BS, bool PP, typename NP, typename LP, typename XP, typename OP, typename SP>
+__device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4, XP x64, OP xobj, SP stk, int* ci,
                                           double* cv,
                                           bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
                                           V3& bhit, bool& bin, double& total, uint32_t& err, int& ref, int& sp,
@@ -801,10 +836,10 @@ __device__ __forceinline__ bool raise_sphere(const RaiseAxis& a, float cx, float
 // Does World#lit_area(T, L, radius) raise?  `nodes`/`leaf4`/`x64` are the
 // hierarchy (LDS or global; nullptr: every sphere in record order), `stk`
 // this lane's traversal stack (stride BS entries, free while this runs).
-// Rare (highlight rays) or optional (exact_raises), so out of line: its
-// registers stay out of the level kernels' allocation.
+// (stk: int or, SPH_BVH_QLDS, int16_t entries.)
+template <typename SP>
 __device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Node* nodes, const float4* leaf4,
-                                             const Sphere64* x64, int* stk, int bs, V3 T, V3 L, double radius) {
+                                                const Sphere64* x64, SP stk, int bs, V3 T, V3 L, double radius) {
   if (!(radius > 0.0) || S.n_sphere == 0) return false;   // r1 <= 0: no d with |R - r1| < d < r1 + R
   const V3 lt = vsub(L, T);
   RaiseAxis a;
@@ -866,6 +901,9 @@ __device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Nod
 template <int SPH, int BS>
 __device__ __forceinline__ bool raises_walk(const KParams& p, char* lds, V3 T, V3 L, double radius) {
   const SceneDev& S = p.scene;
+  if (SPH == SPH_BVH_QLDS)                     // (the float32 leaf records from global memory)
+    return lit_area_raises(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(S.bvh_sph32),
+                           S.bvh_sph64, qstack(lds, p), BS, T, L, radius);
   int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
   if (SPH == SPH_BVH_LDS || SPH == SPH_BVH_LDSX)
     return lit_area_raises(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
@@ -877,7 +915,7 @@ __device__ __forceinline__ bool raises_walk(const KParams& p, char* lds, V3 T, V
   if (SPH == SPH_BVH_GLOBAL)
     return lit_area_raises(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, stk, BS, T, L,
                            radius);
-  return lit_area_raises(S, nullptr, nullptr, nullptr, nullptr, 0, T, L, radius);
+  return lit_area_raises(S, nullptr, nullptr, nullptr, (int*)nullptr, 0, T, L, radius);
 }
 
 // ----------------------------------------------------------------- shading
@@ -1304,10 +1342,11 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   size_t off = 0;
   if (mode == SPH_LIN_LDS) off = (size_t)(S.n_sphere + 4) * 16;
   p.lds_x64 = p.lds_xobj = p.lds_mat = p.lds_sphr = -1;
-  if (mode == SPH_BVH_LDS || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) {
+  if (mode == SPH_BVH_LDS || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX || mode == SPH_BVH_QLDS) {
     off = (size_t)S.n_nodes * sizeof(Bvh4Node);
     p.lds_leaf = (int32_t)off;
-    if (mode != SPH_BVH_MIX) off += (size_t)S.n_slots * 16;
+    if (mode == SPH_BVH_QLDS) off += (size_t)S.n_slots * 8;   // 16-bit records
+    else if (mode != SPH_BVH_MIX) off += (size_t)S.n_slots * 16;
     if (mode == SPH_BVH_LDSX) {
       p.lds_x64 = (int32_t)off;
       off += (size_t)S.n_slots * sizeof(Sphere64);
@@ -1323,8 +1362,8 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   off = (off + 15) & ~(size_t)15;
   p.lds_stack = (int32_t)off;
   p.lds_cov = (int32_t)off;
-  if (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) {
-    off += (size_t)S.bvh_stack * bs * 4;
+  if (sph_is_bvh(mode)) {
+    off += (size_t)S.bvh_stack * bs * (mode == SPH_BVH_QLDS ? 2 : 4);   // QLDS: int16 entries
     off = (off + 15) & ~(size_t)15;
     p.lds_cov = (int32_t)off;
     off += (size_t)COVER_K * bs * 12;
@@ -1332,9 +1371,7 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   // the bottom of every lane's ray stack, as many entries as fit the budget
   off = (off + 15) & ~(size_t)15;
   p.lds_items = (int32_t)off;
-  const size_t budget = (mode == SPH_BVH_LDS || mode == SPH_BVH_GLOBAL || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX)
-                            ? LDS_TOTAL_BYTES
-                            : LDS_LIN_BLOCK_BYTES;
+  const size_t budget = sph_is_bvh(mode) ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
   const size_t per = (size_t)ITEM_WORDS * 8 * bs;
   int slots = budget > off ? (int)((budget - off) / per) : 0;
   if (slots > p.stk_slots_max) slots = p.stk_slots_max;

@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256) void k_path_trace(KParams p) {
   V3 sum = v3(0.0, 0.0, 0.0);
   if (it.depth > 0 && !(vr(it.att) < 0.0001) &&
       !highlights<false>(S, it, sum, err, [&](V3 T, V3 L, double rad) {
-        return lit_area_raises(S, nullptr, nullptr, nullptr, nullptr, 0, T, L, rad);   // (ordered linear walk)
+        return lit_area_raises(S, nullptr, nullptr, nullptr, (int*)nullptr, 0, T, L, rad);   // (ordered linear walk)
       })) {
     double best = S.max_distance, total = 0.0;
     int besti = -1;
@@ -680,6 +680,12 @@ size_t bvh_lds_bytes(int n_nodes, int n_slots, int bvh_stack) {
 size_t bvh_lds_budget() { return LDS_TOTAL_BYTES; }
 
 int resolve_mode(const SceneDev& S, int mode) {
+  if (mode == SPH_BVH_QLDS) {                  // nodes + 16-bit leaf records + 16-bit stacks, when conservative
+    const size_t need = (size_t)S.n_nodes * sizeof(Bvh4Node) + (size_t)S.n_slots * 8 +
+                        (size_t)S.bvh_stack * BS_BVH * 2 + (size_t)COVER_K * BS_BVH * 12 + 64;
+    if (S.q_ok && need <= LDS_TOTAL_BYTES) return mode;
+    mode = SPH_BVH_MIX;
+  }
   if (mode == SPH_BVH_LDSX) {                  // the staged hierarchy plus its exact records
     const size_t need = bvh_lds_bytes(S.n_nodes, S.n_slots, S.bvh_stack) + (size_t)S.n_slots * (sizeof(Sphere64) + 4) +
                         16 + (size_t)S.n_obj * sizeof(Material) + (size_t)S.n_sphere * sizeof(Sphere64);
@@ -821,7 +827,7 @@ hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t 
   const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
   if (tiles == 0) return hipSuccess;
   KevScope kscope(count ? nullptr : kev);
-  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) mode = SPH_BVH_LDS;   // (the lanes engine stages the whole hierarchy or none)
+  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX || mode == SPH_BVH_QLDS) mode = SPH_BVH_LDS;   // (the lanes engine stages the whole hierarchy or none)
   if (count) mode = (mode == SPH_LIN_LDS || mode == SPH_BVH_LDS) ? SPH_LIN_LDS : SPH_LIN_SCALAR;
   mode = resolve_mode(p.scene, mode);
   hipError_t e = hipMemsetAsync(p.extra_count, 0, sizeof(int32_t), s);
@@ -853,7 +859,7 @@ hipError_t launch_render(KParams p, int mode, bool count, int maxs, hipStream_t 
 // could not hold (SRC_LIST; k_level_begin already zeroed its work counter).
 hipError_t launch_redo(const KParams& q, int mode, int maxs, int n, hipStream_t s) {
   g_work_zeroed = true;
-  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) mode = resolve_mode(q.scene, SPH_BVH_LDS);   // (see launch_render)
+  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX || mode == SPH_BVH_QLDS) mode = resolve_mode(q.scene, SPH_BVH_LDS);   // (see launch_render)
   const hipError_t e = launch_src<SRC_LIST>(q, mode, false, maxs, n, s);
   g_work_zeroed = false;
   return e;
@@ -861,7 +867,7 @@ hipError_t launch_redo(const KParams& q, int mode, int maxs, int n, hipStream_t 
 
 hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s) {
   if (p.nrays == 0) return hipSuccess;
-  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX) mode = SPH_BVH_LDS;   // (see launch_render)
+  if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX || mode == SPH_BVH_QLDS) mode = SPH_BVH_LDS;   // (see launch_render)
   mode = resolve_mode(p.scene, mode);
   switch (maxs) {
     case 8: return launch_mode<false, 8, SRC_RAYS>(p, mode, p.nrays, s);

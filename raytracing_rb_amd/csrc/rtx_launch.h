@@ -129,7 +129,15 @@ enum SphMode : int {
   SPH_BVH_LDSX = 5,      // as SPH_BVH_LDS, and the binary64 sphere records of the exact test with their
                          // object indices staged too (bounce-level engine only, small hierarchies: no
                          // global load inside the walk; the lanes engine walks it as SPH_BVH_LDS)
+  SPH_BVH_QLDS = 6,      // four-wide ball hierarchy, nodes + 16-bit quantized leaf records (SceneDev::bvh_q)
+                         // in LDS, 16-bit traversal stacks (bounce-level engine only, hierarchies too big for
+                         // SPH_BVH_LDS next to a hit ring, e.g. C4; the lanes engine walks it as SPH_BVH_LDS)
 };
+
+// Sphere modes that walk the ball hierarchy.
+constexpr bool sph_is_bvh(int m) {
+  return m == SPH_BVH_LDS || m == SPH_BVH_GLOBAL || m == SPH_BVH_MIX || m == SPH_BVH_LDSX || m == SPH_BVH_QLDS;
+}
 
 // HIP event pairs recorded on the launch stream around every ray-tree kernel
 // launch of one render call (option "kernel_events", rtx_kernel_time).

@@ -323,10 +323,13 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
   if (SPH == SPH_LIN_LDS) {
     for (int i = threadIdx.x; i < S.n_sphere + 4; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.sph32)[i];
     __syncthreads();
-  } else if (SPH == SPH_BVH_LDS || SPH == SPH_BVH_MIX || SPH == SPH_BVH_LDSX) {
+  } else if (SPH == SPH_BVH_LDS || SPH == SPH_BVH_MIX || SPH == SPH_BVH_LDSX || SPH == SPH_BVH_QLDS) {
     const int nn = S.n_nodes * (int)(sizeof(Bvh4Node) / 16);
     for (int i = threadIdx.x; i < nn; i += BS) lds_sph[i] = reinterpret_cast<const float4*>(S.bvh)[i];
-    if (SPH != SPH_BVH_MIX) {
+    if (SPH == SPH_BVH_QLDS) {
+      uint4* q = reinterpret_cast<uint4*>(lds + p.lds_leaf);
+      for (int i = threadIdx.x; i < S.n_slots / 2; i += BS) q[i] = reinterpret_cast<const uint4*>(S.bvh_q)[i];
+    } else if (SPH != SPH_BVH_MIX) {
       float4* leaf = reinterpret_cast<float4*>(lds + p.lds_leaf);
       for (int i = threadIdx.x; i < S.n_slots; i += BS) leaf[i] = reinterpret_cast<const float4*>(S.bvh_sph32)[i];
     }
@@ -361,7 +364,13 @@ __device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V
     double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
     int q_ref = BVH_NONE, q_sp = 0, q_ncov = 0;
     bool q_ovf = false;
-    if (SPH == SPH_BVH_LDS)
+    if (SPH == SPH_BVH_QLDS) {
+      const QLeaf ql = {reinterpret_cast<const uint4*>(lds + p.lds_leaf), S.q_org[0], S.q_org[1], S.q_org[2],
+                        S.q_step[0], S.q_step[1], S.q_step[2], S.q_rstep};
+      query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), ql, S.bvh_sph64, S.bvh_obj,
+                           qstack(lds, p), cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref,
+                           q_sp, q_ncov, q_ovf, false, 0);
+    } else if (SPH == SPH_BVH_LDS)
       query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
                            S.bvh_sph64, S.bvh_obj, stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total,
                            err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
@@ -1766,6 +1775,10 @@ int levels_auto_mode(const SceneDev& S, int mode, int compact, int split) {
   if (nodes + leaves + exact + walk + waves * LV_RING_WAVE_BYTES <= LDS_TOTAL_BYTES) return SPH_BVH_LDSX;
   if (nodes + leaves + walk + waves * LV_RING_WAVE_BYTES <= LDS_TOTAL_BYTES) return mode;   // LDS + full ring
   if (nodes + leaves + walk + waves * LV_RING_WAVE_BYTES_SMALL <= LDS_TOTAL_BYTES) return mode;   // + compact ring
+  // C4: the leaves as 16-bit records, 16-bit stacks (+ alignment)
+  const size_t walk16 = (size_t)S.bvh_stack * BS_BVH * 2 + (size_t)COVER_K * BS_BVH * 12 + 64;
+  if (S.q_ok && nodes + (size_t)S.n_slots * 8 + walk16 + 32 + waves * LV_RING_WAVE_BYTES_SMALL <= LDS_TOTAL_BYTES)
+    return SPH_BVH_QLDS;
   if (nodes + walk + waves * LV_RING_WAVE_BYTES_SMALL <= LDS_TOTAL_BYTES) return SPH_BVH_MIX;
   return mode;
 }
@@ -1818,7 +1831,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   size_t lds = lds_layout(q, SPH, BS);
   auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
   if (kind == 0 && q.lv_compact != 0) {        // hit compaction when the rings fit next to the walk's LDS
-    constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL || SPH == SPH_BVH_MIX || SPH == SPH_BVH_LDSX;
+    constexpr bool BVH = sph_is_bvh(SPH);
     const size_t ring = (lds + 15) & ~(size_t)15, budget = BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
     const size_t need = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES;
     const size_t need_small = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES_SMALL;
@@ -1849,7 +1862,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
 template <int SPH>
 static hipError_t launch_level(const KParams& p, int kind, int level, long cap_items, hipStream_t s,
                                KernelEvents* kev) {
-  constexpr bool BVH = SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL || SPH == SPH_BVH_MIX || SPH == SPH_BVH_LDSX;
+  constexpr bool BVH = sph_is_bvh(SPH);
   constexpr int FBS = RTX_LV_FUSED_BS ? RTX_LV_FUSED_BS : (BVH ? BS_BVH : BS_LIN);
   if (kind == 0) return launch_level_bs<SPH, FBS>(p, kind, level, cap_items, s, kev);
   if (BVH) {
@@ -1870,6 +1883,7 @@ static hipError_t launch_level_mode(const KParams& p, int mode, int kind, int le
     case SPH_BVH_GLOBAL: return launch_level<SPH_BVH_GLOBAL>(p, kind, level, cap, s, kev);
     case SPH_BVH_MIX: return launch_level<SPH_BVH_MIX>(p, kind, level, cap, s, kev);
     case SPH_BVH_LDSX: return launch_level<SPH_BVH_LDSX>(p, kind, level, cap, s, kev);
+    case SPH_BVH_QLDS: return launch_level<SPH_BVH_QLDS>(p, kind, level, cap, s, kev);
   }
   return hipErrorInvalidValue;
 }

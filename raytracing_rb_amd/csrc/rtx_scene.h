@@ -55,6 +55,7 @@ struct Sphere64 {
 // compare (distance, object index) lexicographically and shadow covers are
 // subtracted in object order (rtx_kernels.hip).
 constexpr int BVH_LEAF = 4;
+constexpr float CULL_M = 2e-5f;            // pre-test margin (exact culls)
 constexpr int32_t BVH_NONE = 0x7fffffff;
 constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); more -> ordered re-walk
 struct Bvh4Node {
@@ -107,6 +108,7 @@ struct SceneDev {
   const Bvh4Node* bvh;    // n_nodes nodes, root = 0
   const float* bvh_sph32; // 16 floats per leaf (4 slots): {cx 0..3}, {cy 0..3}, {cz 0..3}, {R^2 0..3}
   const Sphere64* bvh_sph64; // binary64 record per slot
+  const uint32_t* bvh_q;  // 8 words per leaf: 16-bit quantized pre-test records {x 0..3}, {y}, {z}, {r} (SPH_BVH_QLDS)
   const int32_t* bvh_obj; // slot -> global (YAML) object index (-1 = padding)
   const int32_t* sph_obj; // sphere record -> global (YAML) object index
   const LightDev* light;
@@ -120,6 +122,11 @@ struct SceneDev {
   double sse;             // soft_shadow_exponent
   float sph_scale;        // max over spheres of |C|_1 + R (pre-test margin scale)
   int32_t sse_is_two;     // pow(area, 2.0) == area*area (glibc, checked)
+  // bvh_q decoding: center axis a = fmaf(q, q_step[a], q_org[a]), radius = q * q_rstep
+  // (>= R + the center's decoding error); q_ok: the records are conservative
+  // for the pre-test and every reference fits a 16-bit traversal stack
+  float q_org[3], q_step[3], q_rstep;
+  int32_t q_ok;
 };
 
 struct CameraDev {

@@ -58,7 +58,8 @@ def c4_world():
 def test_bvh_bit_identical_to_ordered_walk(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lin = _render(sd, cd, BVH_OFF)
-    for src in (0, 1, 2, 3):                    # staged in LDS / scalar loads / nodes LDS + leaves global / all + exact records
+    # staged in LDS / scalar loads / nodes LDS + leaves global / all + exact records / 16-bit leaf records
+    for src in (0, 1, 2, 3, 4):
         assert _same_bits(_render(sd, cd, BVH_ALWAYS, src), lin), src
 
 
@@ -74,11 +75,28 @@ def test_c4_bvh_matches_golden_and_linear(gpu, c4_world):
     _check(fb, z["frame"], z["status"] == 0, min_exact=0.8)
     assert _same_bits(_render(sd, cd, BVH_OFF), fb)
     assert _same_bits(_render(sd, cd, BVH_ALWAYS, 1), fb)
+    assert _same_bits(_render(sd, cd, BVH_ALWAYS, 4), fb)
 
 
 def test_c4_bvh_linear_agree_larger(gpu, c4_world):
     sd, cd = _scene(c4_world, "c4_camera.yml", width=256, height=144, pre_sample_times=2, max_sample_times=2)
-    assert _same_bits(_render(sd, cd, BVH_ALWAYS), _render(sd, cd, BVH_OFF))
+    lin = _render(sd, cd, BVH_OFF)
+    assert _same_bits(_render(sd, cd, BVH_ALWAYS), lin)
+    assert _same_bits(_render(sd, cd, BVH_ALWAYS, 4), lin)
+
+
+def test_c4_quantized_leaves_chosen(gpu, c4_world):
+    """sphere_src auto on C4 stages the nodes and 16-bit leaf records in LDS
+    next to the compact hit ring (SPH_BVH_QLDS = 6); a scene too small to need
+    it keeps the float records (C2: 5, hierarchy + exact records)."""
+    from raytracing_rb_amd.runtime import Renderer
+    sd, cd = _scene(c4_world, "c4_camera.yml", width=64, height=36)
+    r = Renderer(sd, cd, device=0)
+    assert r.get_option("sph_mode_effective") == 6
+    r.set_option("sphere_src", 2)
+    assert r.get_option("sph_mode_effective") == 4
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=64, height=36)
+    assert Renderer(sd, cd, device=0).get_option("sph_mode_effective") == 5
 
 
 # ---------------------------------------------------------------- edge cases
@@ -164,7 +182,7 @@ def test_bvh_edge_scenes_bit_identical(gpu, tmp_path):
     for name, world in _edge_scenes(tmp_path).items():
         sd, cd = _scene(world, "c2_camera.yml", width=160, height=90, pre_sample_times=2, max_sample_times=2)
         lin = _render(sd, cd, BVH_OFF)
-        for src in (0, 1, 2, 3):
+        for src in (0, 1, 2, 3, 4):
             assert _same_bits(_render(sd, cd, BVH_ALWAYS, src), lin), (name, src)
 
 

@@ -254,7 +254,7 @@ def test_compaction_bit_identical(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=3)
     for compact in (0, 1, 2):                   # 2: the compact ring (the ray re-derived in the second half)
-        for src in (-1, 3):                     # 3: the exact sphere records staged in LDS too
+        for src in (-1, 3, 4):                  # 3: the exact sphere records staged in LDS too; 4: 16-bit leaf records
             r = _renderer(sd, cd, 1, lv_compact=compact, sphere_src=src)
             assert _same(r.render(seed=3), lanes), (compact, src)
         st = r.level_stats()
@@ -306,7 +306,7 @@ def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
     assert _same(_renderer(sd, cd, 1, lv_compact=1, sphere_src=0).render(seed=2), lanes)
     # the hierarchy's nodes in LDS and its leaves read from global memory
     # (sphere_src 2) leave room for the compact ring: k_level_c on C4
-    for src in (1, 2):
+    for src in (1, 2, 4):                       # 4: nodes and 16-bit leaf records in LDS (the auto choice)
         for compact in (0, 1, 2):
             assert _same(_renderer(sd, cd, 1, sphere_src=src, lv_compact=compact).render(seed=2), lanes), (src, compact)
 

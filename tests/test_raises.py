@@ -216,7 +216,8 @@ def test_oracle_raises_on_local_lights_factor0_cover(oracle_lib, tmp_path, case)
 
 # ------------------------------------------------------------------ GPU
 ENGINES = [(0, {}), (1, {}), (1, dict(lv_split=1)), (1, dict(lv_compact=0)), (1, dict(lv_compact=2)),
-           (0, dict(bvh=2)), (1, dict(bvh=2)), (1, dict(bvh=2, sphere_src=2)), (1, dict(bvh=0)),
+           (0, dict(bvh=2)), (1, dict(bvh=2)), (1, dict(bvh=2, sphere_src=2)), (1, dict(bvh=2, sphere_src=4)),
+           (1, dict(bvh=0)), (1, dict(bvh=2, sphere_src=4, lv_split=1)),
            (1, dict(lv_hl_cap=1)), (1, dict(lv_hl_cap=1, lv_split=1))]   # deferred-check list overflow: re-render
 
 
