@@ -91,6 +91,8 @@ struct rtx_context {
   int64_t opt_lv_ray_bytes = 0;      // bounce levels: staged ray record, 0 auto (80 B when every path fits 32 bits), 80, 96
   int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
   int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also run the raise walk of the covers they skip
+  int64_t opt_lv_refill = 0;         // k_level_c: refill lanes whose walk ended while fewer than this many walk (0 off)
+  int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
   size_t tile_rays_n = 0;
@@ -449,7 +451,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
       {"lv_redo_blocks", c->opt_lv_redo_blocks}, {"lv_fin_cap", c->opt_lv_fin_cap},
       {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
-      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}};
+      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_refill", c->opt_lv_refill}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -541,6 +543,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_hl_cap")) {         // bounce levels: deferred highlight-check list entries, 0 auto
     if (value < 0 || value > (1 << 26)) return fail(c, RTX_EINVAL, "lv_hl_cap must be in [0, 2^26]");
     c->opt_lv_hl_cap = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_refill")) {         // k_level_c: lanes take new rays while fewer than this many walk (0 off)
+    if (value < 0 || value > 64) return fail(c, RTX_EINVAL, "lv_refill must be in [0, 64]");
+    c->opt_lv_refill = value;
     return RTX_OK;
   }
   if (!strcmp(key, "exact_raises")) {      // every shadow walk also checks the skipped covers' acos raises
@@ -1049,7 +1056,13 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // others' levels).  The extra-sample list and the statistics are shared
   // (appended / added atomically); each part has its own level buffers, its
   // own lanes-engine work counter and ray stacks for its overflow re-render.
-  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_xrq;
+  // lv_refill: one save area per resident wave of k_level_c (2 per SIMD, 4 SIMDs per CU) for the walks
+  // suspended across a shading half
+  if (!c->n_cus) HIPCHK(c, hipDeviceGetAttribute(&c->n_cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  const size_t save_waves = c->opt_lv_refill > 0 ? (size_t)c->n_cus * 8 : 0;
+  const size_t sz_save =
+      al256(save_waves * ((size_t)LV_SAVE_DBL * 64 * 8 + (size_t)std::max(1, c->scene.bvh_stack) * 64 * 4));
+  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_xrq + sz_save;
   const size_t total = parts * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
@@ -1066,8 +1079,11 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_area = split ? (double*)q : nullptr; q += sz_area;
     k.lv_hlq = (double*)q;                    q += sz_hlq;
     k.lv_hlq_cap = (uint32_t)hlcap;
-    k.lv_xrq = xrcap ? (double*)q : nullptr;
+    k.lv_xrq = xrcap ? (double*)q : nullptr;  q += sz_xrq;
     k.lv_xrq_cap = (uint32_t)xrcap;
+    k.lv_save = save_waves ? (double*)q : nullptr;
+    k.lv_save_waves = (int32_t)save_waves;
+    k.lv_refill = (int32_t)c->opt_lv_refill;
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;

@@ -113,6 +113,11 @@ struct KParams {
   int32_t exact_raises;            // 1: every shadow walk (local_lights) also runs lit_area_raises (option exact_raises)
   uint32_t lv_hlq_cap;             // entries of lv_hlq
   double* lv_hlq;                  // highlight rays of the batch whose lit_area raise k_hl_raise checks (8 doubles each)
+  int32_t lv_refill;               // k_level_c: lanes whose nearest-hit walk ended take new rays while fewer than
+                                   // this many still walk (0: one chunk of 64 rays per wave at a time; option lv_refill)
+  int32_t lv_save_waves;           // waves the walk save area holds (the launcher caps a refill grid to it)
+  double* lv_save;                 // per wave: suspended walks saved across a shading half (LV_SAVE_DBL * 64 doubles
+                                   // + bvh_stack * 64 ints)
   uint32_t lv_xrq_cap;             // entries of lv_xrq (0 without exact_raises)
   double* lv_xrq;                  // exact_raises: shading hits whose local_lights raises k_hl_raise checks (4 doubles each)
 };
@@ -133,6 +138,10 @@ enum SphMode : int {
                          // in LDS, 16-bit traversal stacks (bounce-level engine only, hierarchies too big for
                          // SPH_BVH_LDS next to a hit ring, e.g. C4; the lanes engine walks it as SPH_BVH_LDS)
 };
+
+// Suspended nearest-hit walk of k_level_c (option lv_refill): doubles per lane
+// before its traversal stack (LV_SAVE_DBL * 64 doubles, then bvh_stack * 64 ints per wave).
+constexpr int LV_SAVE_DBL = 13;
 
 // Sphere modes that walk the ball hierarchy.
 constexpr bool sph_is_bvh(int m) {

@@ -190,9 +190,14 @@ struct LvQueue {
   // chunk c (< chunks) -> this lane's slice s, offset within the slice, dense
   // index; valid false past the slice's count.  All lanes must call it.
   __device__ __forceinline__ bool item(uint32_t c, uint32_t& s, uint32_t& off, uint32_t& dense_i) const {
+    return item_k(c, __lane_id(), s, off, dense_i);
+  }
+  // the same for ray k (< 64) of chunk c instead of the lane's own (lv_refill)
+  __device__ __forceinline__ bool item_k(uint32_t c, uint32_t k, uint32_t& s, uint32_t& off,
+                                         uint32_t& dense_i) const {
     s = (uint32_t)__popcll(__ballot(cin <= c));
     const uint32_t first = s ? (uint32_t)__shfl((int)cin, (int)s - 1) : 0u;
-    off = (c - first) * 64u + __lane_id();
+    off = (c - first) * 64u + k;
     dense_i = (uint32_t)__shfl((int)pex, (int)s) + off;
     return off < (uint32_t)__shfl((int)cnt, (int)s);
   }
@@ -388,6 +393,50 @@ __device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V
                            cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf,
                            false, 0);
   }
+}
+
+// The nearest-hit walk, resumable (k_level_c with option lv_refill): returns
+// false when fewer than `postpone` lanes of the wave still walk, the walk
+// kept in ref / sp (+ the lane's LDS stack) and best / besti / hit / hin;
+// resume = true continues it (query_bvh's postponing: every lane visits the
+// same nodes and leaves in the same order, so the result is unchanged).
+template <int SPH, int BS>
+__device__ __forceinline__ bool lv_walk_ext_pp(const KParams& p, char* lds, V3 o, V3 d, double& best, int& besti,
+                                               V3& hit, bool& hin, uint32_t& err, int& ref, int& sp, bool resume,
+                                               int postpone) {
+  const SceneDev& S = p.scene;
+  int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
+  double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
+  int ncov = 0;
+  bool ovf = false;
+  double total = 0.0;
+  const Bvh4Node* nodes = reinterpret_cast<const Bvh4Node*>(lds);
+  if (SPH == SPH_BVH_QLDS) {
+    const QLeaf ql = {reinterpret_cast<const uint4*>(lds + p.lds_leaf), S.q_org[0], S.q_org[1], S.q_org[2],
+                      S.q_step[0], S.q_step[1], S.q_step[2], S.q_rstep};
+    return query_bvh<BS, true>(S, nodes, ql, S.bvh_sph64, S.bvh_obj, qstack(lds, p), cov_i, cov_v, true, o, d, hit,
+                               0.0, best, besti, hit, hin, total, err, ref, sp, ncov, ovf, resume, postpone);
+  }
+  int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
+  const float4* leaf4 = reinterpret_cast<const float4*>(lds + p.lds_leaf);
+  if (SPH == SPH_BVH_LDSX)
+    return query_bvh<BS, true>(S, nodes, leaf4, reinterpret_cast<const Sphere64*>(lds + p.lds_x64),
+                               reinterpret_cast<const int32_t*>(lds + p.lds_xobj), stk, cov_i, cov_v, true, o, d, hit,
+                               0.0, best, besti, hit, hin, total, err, ref, sp, ncov, ovf, resume, postpone);
+  return query_bvh<BS, true>(S, nodes, leaf4, S.bvh_sph64, S.bvh_obj, stk, cov_i, cov_v, true, o, d, hit, 0.0, best,
+                             besti, hit, hin, total, err, ref, sp, ncov, ovf, resume, postpone);   // SPH_BVH_LDS
+}
+
+// Stack entry e of this lane's nearest-hit walk in LDS (lv_refill's save / restore).
+template <int SPH, int BS>
+__device__ __forceinline__ int lv_stack_get(const KParams& p, char* lds, int e) {
+  if (SPH == SPH_BVH_QLDS) return qstack(lds, p)[e * BS];
+  return (reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x)[e * BS];
+}
+template <int SPH, int BS>
+__device__ __forceinline__ void lv_stack_set(const KParams& p, char* lds, int e, int v) {
+  if (SPH == SPH_BVH_QLDS) qstack(lds, p)[e * BS] = (int16_t)v;
+  else (reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x)[e * BS] = v;
 }
 
 // The ray of a level's queue entry: a camera sample (level 0: `idx` = its
@@ -774,7 +823,7 @@ constexpr int LV_RING_FIELDS_SMALL = 5;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
 constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMALL * 8;
 
-template <int SPH, int BS, int RF, bool LAST>
+template <int SPH, int BS, int RF, bool LAST, bool REFILL>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
   constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
@@ -793,6 +842,18 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * ((size_t)LV_RING * RF * 8));
   uint32_t head = 0, pend = 0;                // wave-uniform: first parked slot, parked hits
   bool got = true;
+  // lv_refill: the wave's pool (rays rf_next.. of chunk rf_chunk) and the
+  // lane's nearest-hit walk (rf_has: one is running or suspended)
+  uint32_t rf_chunk = 0, rf_next = 64;
+  bool rf_has = false, rf_started = false;
+  V3 rf_o = v3(0.0, 0.0, 0.0), rf_d = rf_o, rf_hit = rf_o;
+  double rf_best = 0.0;
+  int rf_besti = -1, rf_ref = BVH_NONE, rf_sp = 0;
+  bool rf_hin = true;
+  uint32_t rf_i = 0, rf_slot = 0, rf_errA = 0, rf_errL = 0;
+  double* const rf_sv = REFILL ? p.lv_save + (size_t)(blockIdx.x * (BS / 64) + (threadIdx.x >> 6)) *
+                                                 ((size_t)LV_SAVE_DBL * 64 + (size_t)S.bvh_stack * 32)
+                               : nullptr;
 
   unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
   unsigned long long nA = 0, nE = 0, nS = 0;
@@ -803,101 +864,243 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     t0 = t1;             \
   }
   while (true) {
-    uint32_t chunk = 0;
-    if (got) got = sched.claim(in.chunks, chunk);   // (never again once exhausted)
-    if (RTX_STAMPS) t0 = stamp();
-    if (got) {
-      if (RTX_STAMPS) nchunks++;
-      // ---- first half: the ray, rt_map's cutoff, highlights, World#intersect
-      uint32_t s, off, i;
-      bool active = in.item(chunk, s, off, i);
-      const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
-      // A staged child's first half needs its origin and direction only: the
-      // attenuation is read if a highlight fires, the root if the ray
-      // overflows the record arena (the second half reloads the rest), so
-      // the walk does not carry them.
-      const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
-      Item cur;
-      int root = 0, x = 0, y = 0, sample = 0;
-      bool alive = false;
-      if (active) {
-        bool valid = true;
-        if (level == 0) {
-          lv_ray(p, level, slot, cur, root, x, y, sample, valid);
-          p.lv_redo_of[i] = -1;
-        } else {
-          const double2 a = qs[0], b = qs[1], c = qs[2];
-          cur.ray.o = v3(a.x, a.y, b.x);
-          cur.ray.d = v3(b.y, c.x, c.y);
+    bool rf_saved = false;                    // lv_refill: suspended walks saved below
+    if constexpr (!REFILL) {
+      uint32_t chunk = 0;
+      if (got) got = sched.claim(in.chunks, chunk);   // (never again once exhausted)
+      if (RTX_STAMPS) t0 = stamp();
+      if (got) {
+        if (RTX_STAMPS) nchunks++;
+        // ---- first half: the ray, rt_map's cutoff, highlights, World#intersect
+        uint32_t s, off, i;
+        bool active = in.item(chunk, s, off, i);
+        const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
+        // A staged child's first half needs its origin and direction only: the
+        // attenuation is read if a highlight fires, the root if the ray
+        // overflows the record arena (the second half reloads the rest), so
+        // the walk does not carry them.
+        const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
+        Item cur;
+        int root = 0, x = 0, y = 0, sample = 0;
+        bool alive = false;
+        if (active) {
+          bool valid = true;
+          if (level == 0) {
+            lv_ray(p, level, slot, cur, root, x, y, sample, valid);
+            p.lv_redo_of[i] = -1;
+          } else {
+            const double2 a = qs[0], b = qs[1], c = qs[2];
+            cur.ray.o = v3(a.x, a.y, b.x);
+            cur.ray.d = v3(b.y, c.x, c.y);
+          }
+          active = valid;
+          alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // ray_tracer.rb:52
+          if (active && base + i >= p.lv_lcap) {
+            lv_redo(p, level == 0 ? root : lv_ray_root(p, qs));
+            active = alive = false;
+          }
         }
-        active = valid;
-        alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // ray_tracer.rb:52
-        if (active && base + i >= p.lv_lcap) {
-          lv_redo(p, level == 0 ? root : lv_ray_root(p, qs));
-          active = alive = false;
+        char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
+        double* leafp = reinterpret_cast<double*>(rec + 8);
+        uint32_t errA = 0, errL = 0;
+        int nleaf = 0;
+        bool fired = false, hl_defer = false;
+        if (alive)
+          fired = highlight_leaves_att(S, cur.ray, [&] {
+            if (level == 0) return cur.att;
+            const double2 d = qs[3], e = qs[4];
+            return v3(d.x, d.y, e.x);
+          }, [&](V3 c) {
+            leafp[3 * nleaf] = c.x;
+            leafp[3 * nleaf + 1] = c.y;
+            leafp[3 * nleaf + 2] = c.z;
+            nleaf++;
+          }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
+        lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return level == 0 ? root : lv_ray_root(p, qs); });
+        RTX_LV_STAMP(0)
+        const bool ext = alive && !fired;
+        double best = S.max_distance, total = 0.0;
+        int besti = -1;
+        V3 hit = v3(0.0, 0.0, 0.0);
+        bool hin = true;
+        if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
+        const bool shade = ext && besti >= 0;
+        if (RTX_STAMPS) {
+          nA += __popcll(__ballot(active));
+          nE += __popcll(__ballot(ext));
+          nS += __popcll(__ballot(shade));
+        }
+        RTX_LV_STAMP(1)
+        if (active && !shade) {                 // the ray ends here: its record (k_level's, no children)
+          const uint32_t err = errA ? errA : errL;
+          *reinterpret_cast<uint2*>(rec) = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8), 0u);
+        }
+        // park the hits: slot head + pend + (rank among the wave's hits)
+        const uint64_t hm = __ballot(shade);
+        if (shade) {
+          const uint32_t k = (head + pend + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))) & (LV_RING - 1);
+          double* r = ring + k;
+          r[0 * LV_RING] = hit.x;
+          r[1 * LV_RING] = hit.y;
+          r[2 * LV_RING] = hit.z;
+          if (RF == LV_RING_FIELDS) {
+            r[3 * LV_RING] = cur.ray.o.x;
+            r[4 * LV_RING] = cur.ray.o.y;
+            r[5 * LV_RING] = cur.ray.o.z;
+            r[6 * LV_RING] = cur.ray.d.x;
+            r[7 * LV_RING] = cur.ray.d.y;
+            r[8 * LV_RING] = cur.ray.d.z;
+          }
+          r[FI * LV_RING] = __builtin_bit_cast(double, (uint64_t)i | (uint64_t)slot << 32);
+          r[(FI + 1) * LV_RING] = __builtin_bit_cast(
+              double, (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) | (uint64_t)((errA & 0xffu) | (errL & 0xffu) << 8) << 32);
+        }
+        pend += (uint32_t)__popcll(hm);
+        RTX_LV_STAMP(4)
+      }
+      if (pend < 64 && (got || pend == 0)) {
+        if (!got) break;                        // no chunk left and nothing parked
+        continue;                               // not a full wave of hits yet
+      }
+    } else {
+      // ---- first half with refill (option lv_refill): a
+      // lane whose walk ended (or whose ray needs none) takes the next ray of
+      // the wave's pool, the current chunk, claiming the next chunk when it
+      // runs out; the walks run until fewer than lv_refill lanes still walk.
+      while (true) {
+        const uint64_t needm = __ballot(!rf_has);
+        if (needm == 0) break;
+        if (rf_next >= 64u) {                 // pool empty: the next chunk
+          if (!got) break;
+          got = sched.claim(in.chunks, rf_chunk);
+          if (!got) break;
+          rf_next = 0;
+        }
+        const uint32_t k = rf_next + (uint32_t)__popcll(needm & ((1ull << lane) - 1ull));
+        const bool take = !rf_has && k < 64u;
+        rf_next += (uint32_t)__popcll(needm);
+        if (rf_next > 64u) rf_next = 64u;
+        uint32_t s, off, i;
+        bool active = in.item_k(rf_chunk, take ? k : 0u, s, off, i) && take;
+        const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
+        const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
+        Item cur;
+        int root = 0, x = 0, y = 0, sample = 0;
+        bool alive = false;
+        if (active) {
+          bool valid = true;
+          if (level == 0) {
+            lv_ray(p, level, slot, cur, root, x, y, sample, valid);
+            p.lv_redo_of[i] = -1;
+          } else {
+            const double2 a = qs[0], b = qs[1], c = qs[2];
+            cur.ray.o = v3(a.x, a.y, b.x);
+            cur.ray.d = v3(b.y, c.x, c.y);
+          }
+          active = valid;
+          alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // ray_tracer.rb:52
+          if (active && base + i >= p.lv_lcap) {
+            lv_redo(p, level == 0 ? root : lv_ray_root(p, qs));
+            active = alive = false;
+          }
+        }
+        char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
+        double* leafp = reinterpret_cast<double*>(rec + 8);
+        uint32_t errA = 0;
+        int nleaf = 0;
+        bool fired = false, hl_defer = false;
+        if (alive)
+          fired = highlight_leaves_att(S, cur.ray, [&] {
+            if (level == 0) return cur.att;
+            const double2 d = qs[3], e = qs[4];
+            return v3(d.x, d.y, e.x);
+          }, [&](V3 c) {
+            leafp[3 * nleaf] = c.x;
+            leafp[3 * nleaf + 1] = c.y;
+            leafp[3 * nleaf + 2] = c.z;
+            nleaf++;
+          }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
+        lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return level == 0 ? root : lv_ray_root(p, qs); });
+        const bool ext = alive && !fired;
+        if (active && !ext)                   // the ray ends here without a walk: its record
+          *reinterpret_cast<uint2*>(rec) = make_uint2((errA & 0xffu) | ((uint32_t)nleaf << 8), 0u);
+        if (ext) {
+          rf_has = true;
+          rf_started = false;
+          rf_o = cur.ray.o;
+          rf_d = cur.ray.d;
+          rf_i = i;
+          rf_slot = slot;
+          rf_errA = errA;
+          rf_errL = 0;
+          rf_best = S.max_distance;
+          rf_besti = -1;
+          rf_hit = v3(0.0, 0.0, 0.0);
+          rf_hin = true;
         }
       }
-      char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
-      double* leafp = reinterpret_cast<double*>(rec + 8);
-      uint32_t errA = 0, errL = 0;
-      int nleaf = 0;
-      bool fired = false, hl_defer = false;
-      if (alive)
-        fired = highlight_leaves_att(S, cur.ray, [&] {
-          if (level == 0) return cur.att;
-          const double2 d = qs[3], e = qs[4];
-          return v3(d.x, d.y, e.x);
-        }, [&](V3 c) {
-          leafp[3 * nleaf] = c.x;
-          leafp[3 * nleaf + 1] = c.y;
-          leafp[3 * nleaf + 2] = c.z;
-          nleaf++;
-        }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
-      lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return level == 0 ? root : lv_ray_root(p, qs); });
-      RTX_LV_STAMP(0)
-      const bool ext = alive && !fired;
-      double best = S.max_distance, total = 0.0;
-      int besti = -1;
-      V3 hit = v3(0.0, 0.0, 0.0);
-      bool hin = true;
-      if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL);
-      const bool shade = ext && besti >= 0;
-      if (RTX_STAMPS) {
-        nA += __popcll(__ballot(active));
-        nE += __popcll(__ballot(ext));
-        nS += __popcll(__ballot(shade));
+      const bool exhausted = !got && rf_next >= 64u;   // wave-uniform: no ray left to take
+      bool done = false;
+      if (rf_has) {
+        done = lv_walk_ext_pp<SPH, BS>(p, lds, rf_o, rf_d, rf_best, rf_besti, rf_hit, rf_hin, rf_errL, rf_ref, rf_sp,
+                                       rf_started, exhausted ? 0 : p.lv_refill);
+        rf_started = true;
       }
-      RTX_LV_STAMP(1)
-      if (active && !shade) {                 // the ray ends here: its record (k_level's, no children)
-        const uint32_t err = errA ? errA : errL;
-        *reinterpret_cast<uint2*>(rec) = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8), 0u);
+      const bool fin = rf_has && done;
+      const bool shade = fin && rf_besti >= 0;
+      if (fin && !shade) {                    // the ray ends here: its record
+        const uint32_t err = rf_errA ? rf_errA : rf_errL;
+        *reinterpret_cast<uint2*>(p.lv_rec + (size_t)(base + rf_i) * p.lv_rec_bytes) = make_uint2(err & 0xffu, 0u);
       }
-      // park the hits: slot head + pend + (rank among the wave's hits)
       const uint64_t hm = __ballot(shade);
       if (shade) {
         const uint32_t k = (head + pend + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))) & (LV_RING - 1);
         double* r = ring + k;
-        r[0 * LV_RING] = hit.x;
-        r[1 * LV_RING] = hit.y;
-        r[2 * LV_RING] = hit.z;
+        r[0 * LV_RING] = rf_hit.x;
+        r[1 * LV_RING] = rf_hit.y;
+        r[2 * LV_RING] = rf_hit.z;
         if (RF == LV_RING_FIELDS) {
-          r[3 * LV_RING] = cur.ray.o.x;
-          r[4 * LV_RING] = cur.ray.o.y;
-          r[5 * LV_RING] = cur.ray.o.z;
-          r[6 * LV_RING] = cur.ray.d.x;
-          r[7 * LV_RING] = cur.ray.d.y;
-          r[8 * LV_RING] = cur.ray.d.z;
+          r[3 * LV_RING] = rf_o.x;
+          r[4 * LV_RING] = rf_o.y;
+          r[5 * LV_RING] = rf_o.z;
+          r[6 * LV_RING] = rf_d.x;
+          r[7 * LV_RING] = rf_d.y;
+          r[8 * LV_RING] = rf_d.z;
         }
-        r[FI * LV_RING] = __builtin_bit_cast(double, (uint64_t)i | (uint64_t)slot << 32);
+        r[FI * LV_RING] = __builtin_bit_cast(double, (uint64_t)rf_i | (uint64_t)rf_slot << 32);
         r[(FI + 1) * LV_RING] = __builtin_bit_cast(
-            double, (uint64_t)((uint32_t)besti | (hin ? 0x80000000u : 0u)) | (uint64_t)((errA & 0xffu) | (errL & 0xffu) << 8) << 32);
+            double, (uint64_t)((uint32_t)rf_besti | (rf_hin ? 0x80000000u : 0u)) |
+                        (uint64_t)((rf_errA & 0xffu) | (rf_errL & 0xffu) << 8) << 32);
       }
       pend += (uint32_t)__popcll(hm);
-      RTX_LV_STAMP(4)
-    }
-    if (pend < 64 && (got || pend == 0)) {
-      if (!got) break;                        // no chunk left and nothing parked
-      continue;                               // not a full wave of hits yet
+      rf_has = rf_has && !done;
+      const bool flush = exhausted && __ballot(rf_has) == 0;
+      if (pend < 64 && !(flush && pend > 0)) {
+        if (flush) break;                     // no ray left, no walk running, nothing parked
+        continue;                             // not a full wave of hits yet
+      }
+      // the shading half below walks with this lane's LDS stack: save the suspended walks
+      rf_saved = __ballot(rf_has) != 0;
+      if (rf_saved && rf_has) {
+        double* v = rf_sv + lane;
+        v[0 * 64] = rf_o.x;
+        v[1 * 64] = rf_o.y;
+        v[2 * 64] = rf_o.z;
+        v[3 * 64] = rf_d.x;
+        v[4 * 64] = rf_d.y;
+        v[5 * 64] = rf_d.z;
+        v[6 * 64] = rf_best;
+        v[7 * 64] = rf_hit.x;
+        v[8 * 64] = rf_hit.y;
+        v[9 * 64] = rf_hit.z;
+        v[10 * 64] = __builtin_bit_cast(double, (uint64_t)rf_i | (uint64_t)rf_slot << 32);
+        v[11 * 64] = __builtin_bit_cast(double, (uint64_t)(uint32_t)rf_besti |
+                                                    (uint64_t)((rf_errA & 0xffu) | (rf_errL & 0xffu) << 8 |
+                                                               (rf_hin ? 0x10000u : 0u)) << 32);
+        v[12 * 64] = __builtin_bit_cast(double, (uint64_t)(uint32_t)rf_ref | (uint64_t)(uint32_t)rf_sp << 32);
+        int* st = reinterpret_cast<int*>(rf_sv + LV_SAVE_DBL * 64) + lane;
+        for (int e = 0; e < rf_sp; e++) st[e * 64] = lv_stack_get<SPH, BS>(p, lds, e);
+      }
     }
     // ---- second half on up to 64 parked hits (64, except the final flush)
     const uint32_t take = pend < 64 ? pend : 64u;
@@ -994,6 +1197,35 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec, 0,
               errA, errS, errL, errP, m, LAST);
     RTX_LV_STAMP(5)
+    if constexpr (REFILL) {                   // the suspended walks back (every path assigns them)
+      if (rf_saved && rf_has) {
+        const double* v = rf_sv + lane;
+        rf_o = v3(v[0 * 64], v[1 * 64], v[2 * 64]);
+        rf_d = v3(v[3 * 64], v[4 * 64], v[5 * 64]);
+        rf_best = v[6 * 64];
+        rf_hit = v3(v[7 * 64], v[8 * 64], v[9 * 64]);
+        const uint64_t w10 = __builtin_bit_cast(uint64_t, v[10 * 64]), w11 = __builtin_bit_cast(uint64_t, v[11 * 64]),
+                       w12 = __builtin_bit_cast(uint64_t, v[12 * 64]);
+        rf_i = (uint32_t)w10;
+        rf_slot = (uint32_t)(w10 >> 32);
+        rf_besti = (int)(uint32_t)w11;
+        rf_errA = (uint32_t)(w11 >> 32) & 0xffu;
+        rf_errL = (uint32_t)(w11 >> 40) & 0xffu;
+        rf_hin = ((w11 >> 48) & 1u) != 0;
+        rf_ref = (int)(uint32_t)w12;
+        rf_sp = (int)(uint32_t)(w12 >> 32);
+        const int* st = reinterpret_cast<const int*>(rf_sv + LV_SAVE_DBL * 64) + lane;
+        for (int e = 0; e < rf_sp; e++) lv_stack_set<SPH, BS>(p, lds, e, st[e * 64]);
+      } else {
+        rf_o = rf_d = rf_hit = v3(0.0, 0.0, 0.0);
+        rf_best = 0.0;
+        rf_i = rf_slot = rf_errA = rf_errL = 0;
+        rf_besti = -1;
+        rf_hin = true;
+        rf_ref = BVH_NONE;
+        rf_sp = 0;
+      }
+    }
   }
 #undef RTX_LV_STAMP
   if (RTX_STAMPS && __lane_id() == 0) {
@@ -1010,9 +1242,9 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS, int RF, bool LAST>
+template <int SPH, int BS, int RF, bool LAST, bool REFILL>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
-  k_level_c_body<SPH, BS, RF, LAST>(p, level);
+  k_level_c_body<SPH, BS, RF, LAST, REFILL>(p, level);
   lv_level_done(p, level + 1);
 }
 
@@ -1821,6 +2053,16 @@ static hipError_t launch_timed(K kern, long blocks, int bs, size_t lds, hipStrea
   return e;
 }
 
+// k_level_c for a level: the batch's last level compiled apart; with refill
+// (option lv_refill) for the sphere modes it is compiled for (C2's and C4's).
+template <int SPH, int BS, int RF>
+static void (*level_c_kernel(bool last, bool refill))(KParams, int) {
+  if constexpr (SPH == SPH_BVH_LDSX || SPH == SPH_BVH_QLDS) {
+    if (refill) return last ? k_level_c<SPH, BS, RF, true, true> : k_level_c<SPH, BS, RF, false, true>;
+  }
+  return last ? k_level_c<SPH, BS, RF, true, false> : k_level_c<SPH, BS, RF, false, false>;
+}
+
 // kind: 0 k_level (fused), 1 k_lv_trace, 2 k_lv_shadow.  Persistent: as many
 // workgroups as fit at once, never more than cap_items need.
 template <int SPH, int BS>
@@ -1830,6 +2072,8 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   q.stk_slots_max = 0;                         // no ray stack in this engine
   size_t lds = lds_layout(q, SPH, BS);
   auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
+  bool refill = (SPH == SPH_BVH_LDSX || SPH == SPH_BVH_QLDS) && kind == 0 && q.lv_compact != 0 && q.lv_refill > 0 &&
+                q.lv_save && q.lv_save_waves >= BS / 64;
   if (kind == 0 && q.lv_compact != 0) {        // hit compaction when the rings fit next to the walk's LDS
     constexpr bool BVH = sph_is_bvh(SPH);
     const size_t ring = (lds + 15) & ~(size_t)15, budget = BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
@@ -1838,18 +2082,20 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
     if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
-      kern = level == q.lv_last_level ? k_level_c<SPH, BS, LV_RING_FIELDS, true> : k_level_c<SPH, BS, LV_RING_FIELDS, false>;
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level, refill);
     } else if (BVH && need_small <= budget) {  // the compact ring (C4-sized hierarchies)
       q.lds_ring = (int32_t)ring;
       lds = need_small;
-      kern = level == q.lv_last_level ? k_level_c<SPH, BS, LV_RING_FIELDS_SMALL, true>
-                                      : k_level_c<SPH, BS, LV_RING_FIELDS_SMALL, false>;
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, refill);
+    } else {
+      refill = false;
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)
   const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(kern), BS, lds, cus, per_cu);
   if (e != hipSuccess) return e;
-  const long grid = std::max<long>(1, (long)cus * per_cu / std::max(1, q.lv_grid_div));
+  long grid = std::max<long>(1, (long)cus * per_cu / std::max(1, q.lv_grid_div));
+  if (refill) grid = std::min<long>(grid, std::max(1, q.lv_save_waves / (BS / 64)));   // one save area per wave
   return launch_timed(kern, std::min<long>((cap_items + BS - 1) / BS, grid), BS, lds, s, kev, q, level);
 }
 

@@ -277,6 +277,37 @@ def test_compaction_batches_overflow_schedule(gpu, opts):
             assert r.level_stats()["redo"] > 0
 
 
+# ---- refill (option lv_refill: lanes whose nearest-hit walk ended take new rays, walks saved across shading)
+@pytest.mark.parametrize("world,camera,ov", SCENES_SMALL)
+def test_refill_bit_identical(gpu, world, camera, ov):
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=6)
+    for refill in (1, 16, 40, 64):
+        for compact in (1, 2):
+            r = _renderer(sd, cd, 1, lv_compact=compact, lv_refill=refill)
+            assert _same(r.render(seed=6), lanes), (refill, compact)
+            st = r.level_stats()
+            assert st["redo"] == 0 and st["dropped"] == 0
+
+
+def test_refill_c4_and_overflow(gpu):
+    """C4 (16-bit leaf records, compact ring) and C2 with the record arena and
+    queue slices overflowing into the re-render, under refill; same bits."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_scenes
+    make_scenes.ensure_c4()
+    sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=64, height=36)
+    lanes = _renderer(sd, cd, 0).render(seed=2)
+    for refill in (8, 32):
+        assert _same(_renderer(sd, cd, 1, lv_refill=refill).render(seed=2), lanes), refill
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
+    lanes = _renderer(sd, cd, 0).render(seed=5)
+    for opts in (dict(lv_stage_pct=5, lv_floor=0), dict(lv_rec_pct=101, lv_floor=0), dict(lv_batch=512)):
+        r = _renderer(sd, cd, 1, lv_refill=24, **opts)
+        assert _same(r.render(seed=5), lanes), opts
+
+
 def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
     """Raise sites keep their order through the ring (full and compact); C4's
     staged hierarchy leaves no LDS for a ring: with sphere_src 0 the option
