@@ -851,9 +851,11 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   int rf_besti = -1, rf_ref = BVH_NONE, rf_sp = 0;
   bool rf_hin = true;
   uint32_t rf_i = 0, rf_slot = 0, rf_errA = 0, rf_errL = 0;
-  double* const rf_sv = REFILL ? p.lv_save + (size_t)(blockIdx.x * (BS / 64) + (threadIdx.x >> 6)) *
-                                                 ((size_t)LV_SAVE_DBL * 64 + (size_t)S.bvh_stack * 32)
-                               : nullptr;
+  // (wave-uniform values kept in scalar registers: the shading half runs at the VGPR limit)
+  double* const rf_sv =
+      REFILL ? p.lv_save + (size_t)(blockIdx.x * (BS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) *
+                               ((size_t)LV_SAVE_DBL * 64 + (size_t)S.bvh_stack * 32)
+             : nullptr;
 
   unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
   unsigned long long nA = 0, nE = 0, nS = 0;
@@ -974,12 +976,12 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
           if (!got) break;
           got = sched.claim(in.chunks, rf_chunk);
           if (!got) break;
+          rf_chunk = __builtin_amdgcn_readfirstlane(rf_chunk);
           rf_next = 0;
         }
         const uint32_t k = rf_next + (uint32_t)__popcll(needm & ((1ull << lane) - 1ull));
         const bool take = !rf_has && k < 64u;
-        rf_next += (uint32_t)__popcll(needm);
-        if (rf_next > 64u) rf_next = 64u;
+        rf_next = __builtin_amdgcn_readfirstlane(min(64u, rf_next + (uint32_t)__popcll(needm)));
         uint32_t s, off, i;
         bool active = in.item_k(rf_chunk, take ? k : 0u, s, off, i) && take;
         const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
