@@ -92,6 +92,7 @@ struct rtx_context {
   int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
   int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also run the raise walk of the covers they skip
   int64_t opt_lv_refill = 0;         // k_level_c: refill lanes whose walk ended while fewer than this many walk (0 off)
+  int64_t opt_lv_refill_save = 0;    // 1: refill walks suspended across the shading half (saved); 0: finished first
   int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
@@ -451,7 +452,8 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
       {"lv_redo_blocks", c->opt_lv_redo_blocks}, {"lv_fin_cap", c->opt_lv_fin_cap},
       {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
-      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_refill", c->opt_lv_refill}};
+      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_refill", c->opt_lv_refill},
+      {"lv_refill_save", c->opt_lv_refill_save}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -548,6 +550,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_refill")) {         // k_level_c: lanes take new rays while fewer than this many walk (0 off)
     if (value < 0 || value > 64) return fail(c, RTX_EINVAL, "lv_refill must be in [0, 64]");
     c->opt_lv_refill = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_refill_save")) {    // refill: suspend walks across the shading half (1) or finish them (0)
+    if (value != 0 && value != 1) return fail(c, RTX_EINVAL, "lv_refill_save must be 0 or 1");
+    c->opt_lv_refill_save = value;
     return RTX_OK;
   }
   if (!strcmp(key, "exact_raises")) {      // every shadow walk also checks the skipped covers' acos raises
@@ -1059,7 +1066,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // lv_refill: one save area per resident wave of k_level_c (2 per SIMD, 4 SIMDs per CU) for the walks
   // suspended across a shading half
   if (!c->n_cus) HIPCHK(c, hipDeviceGetAttribute(&c->n_cus, hipDeviceAttributeMultiprocessorCount, c->device));
-  const size_t save_waves = c->opt_lv_refill > 0 ? (size_t)c->n_cus * 8 : 0;
+  const size_t save_waves = c->opt_lv_refill > 0 && c->opt_lv_refill_save ? (size_t)c->n_cus * 8 : 0;
   const size_t sz_save =
       al256(save_waves * ((size_t)LV_SAVE_DBL * 64 * 8 + (size_t)std::max(1, c->scene.bvh_stack) * 64 * 4));
   const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_xrq + sz_save;
@@ -1084,6 +1091,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_save = save_waves ? (double*)q : nullptr;
     k.lv_save_waves = (int32_t)save_waves;
     k.lv_refill = (int32_t)c->opt_lv_refill;
+    k.lv_refill_save = (int32_t)c->opt_lv_refill_save;
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;

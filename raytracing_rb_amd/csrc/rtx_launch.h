@@ -115,6 +115,7 @@ struct KParams {
   double* lv_hlq;                  // highlight rays of the batch whose lit_area raise k_hl_raise checks (8 doubles each)
   int32_t lv_refill;               // k_level_c: lanes whose nearest-hit walk ended take new rays while fewer than
                                    // this many still walk (0: one chunk of 64 rays per wave at a time; option lv_refill)
+  int32_t lv_refill_save;          // 1: walks suspended across a shading half (saved to lv_save); 0: they finish first
   int32_t lv_save_waves;           // waves the walk save area holds (the launcher caps a refill grid to it)
   double* lv_save;                 // per wave: suspended walks saved across a shading half (LV_SAVE_DBL * 64 doubles
                                    // + bvh_stack * 64 ints)

@@ -969,7 +969,11 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       // lane whose walk ended (or whose ray needs none) takes the next ray of
       // the wave's pool, the current chunk, claiming the next chunk when it
       // runs out; the walks run until fewer than lv_refill lanes still walk.
-      while (true) {
+      // Once 64 hits are parked the running walks finish first (no refill,
+      // no postponing), so the shading half starts with no walk suspended
+      // (lv_refill_save = 1: walks suspended across it, saved to lv_save).
+      const bool drain = !p.lv_refill_save && pend >= 64u;
+      while (!drain) {
         const uint64_t needm = __ballot(!rf_has);
         if (needm == 0) break;
         if (rf_next >= 64u) {                 // pool empty: the next chunk
@@ -1045,7 +1049,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       bool done = false;
       if (rf_has) {
         done = lv_walk_ext_pp<SPH, BS>(p, lds, rf_o, rf_d, rf_best, rf_besti, rf_hit, rf_hin, rf_errL, rf_ref, rf_sp,
-                                       rf_started, exhausted ? 0 : p.lv_refill);
+                                       rf_started, exhausted || drain ? 0 : p.lv_refill);
         rf_started = true;
       }
       const bool fin = rf_has && done;
@@ -1077,6 +1081,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       pend += (uint32_t)__popcll(hm);
       rf_has = rf_has && !done;
       const bool flush = exhausted && __ballot(rf_has) == 0;
+      if (pend >= 64 && !p.lv_refill_save && __ballot(rf_has) != 0) continue;   // finish the walks first
       if (pend < 64 && !(flush && pend > 0)) {
         if (flush) break;                     // no ray left, no walk running, nothing parked
         continue;                             // not a full wave of hits yet
@@ -2075,7 +2080,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   size_t lds = lds_layout(q, SPH, BS);
   auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
   bool refill = (SPH == SPH_BVH_LDSX || SPH == SPH_BVH_QLDS) && kind == 0 && q.lv_compact != 0 && q.lv_refill > 0 &&
-                q.lv_save && q.lv_save_waves >= BS / 64;
+                (!q.lv_refill_save || (q.lv_save && q.lv_save_waves >= BS / 64));
   if (kind == 0 && q.lv_compact != 0) {        // hit compaction when the rings fit next to the walk's LDS
     constexpr bool BVH = sph_is_bvh(SPH);
     const size_t ring = (lds + 15) & ~(size_t)15, budget = BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
@@ -2097,7 +2102,8 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(kern), BS, lds, cus, per_cu);
   if (e != hipSuccess) return e;
   long grid = std::max<long>(1, (long)cus * per_cu / std::max(1, q.lv_grid_div));
-  if (refill) grid = std::min<long>(grid, std::max(1, q.lv_save_waves / (BS / 64)));   // one save area per wave
+  if (refill && q.lv_refill_save)                // one save area per wave
+    grid = std::min<long>(grid, std::max(1, q.lv_save_waves / (BS / 64)));
   return launch_timed(kern, std::min<long>((cap_items + BS - 1) / BS, grid), BS, lds, s, kev, q, level);
 }
 

@@ -282,10 +282,10 @@ def test_compaction_batches_overflow_schedule(gpu, opts):
 def test_refill_bit_identical(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=6)
-    for refill in (1, 16, 40, 64):
+    for refill, save in ((1, 0), (16, 0), (40, 0), (64, 0), (16, 1), (64, 1)):
         for compact in (1, 2):
-            r = _renderer(sd, cd, 1, lv_compact=compact, lv_refill=refill)
-            assert _same(r.render(seed=6), lanes), (refill, compact)
+            r = _renderer(sd, cd, 1, lv_compact=compact, lv_refill=refill, lv_refill_save=save)
+            assert _same(r.render(seed=6), lanes), (refill, save, compact)
             st = r.level_stats()
             assert st["redo"] == 0 and st["dropped"] == 0
 
@@ -299,13 +299,14 @@ def test_refill_c4_and_overflow(gpu):
     make_scenes.ensure_c4()
     sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=64, height=36)
     lanes = _renderer(sd, cd, 0).render(seed=2)
-    for refill in (8, 32):
-        assert _same(_renderer(sd, cd, 1, lv_refill=refill).render(seed=2), lanes), refill
+    for refill, save in ((8, 0), (32, 0), (32, 1)):
+        assert _same(_renderer(sd, cd, 1, lv_refill=refill, lv_refill_save=save).render(seed=2), lanes), refill
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
     lanes = _renderer(sd, cd, 0).render(seed=5)
     for opts in (dict(lv_stage_pct=5, lv_floor=0), dict(lv_rec_pct=101, lv_floor=0), dict(lv_batch=512)):
-        r = _renderer(sd, cd, 1, lv_refill=24, **opts)
-        assert _same(r.render(seed=5), lanes), opts
+        for save in (0, 1):
+            r = _renderer(sd, cd, 1, lv_refill=24, lv_refill_save=save, **opts)
+            assert _same(r.render(seed=5), lanes), (opts, save)
 
 
 def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
