@@ -1897,14 +1897,29 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
 // World#high_lights for one listed ray, now with lit_area_raises for every
 // light that fires (in light order, after that light's own cos raise, as
 // rt_map meets them), and rewrites the raise byte of the ray's record.  The
-// walk reads the hierarchy from global memory (L2-resident) with its stack in
-// LDS (bvh_stack words per thread).  Grid-stride over the device-side count.
-__global__ __launch_bounds__(256) void k_hl_raise(KParams p) {
+// walk reads the hierarchy from LDS when the launcher staged it (`stage`:
+// small hierarchies, C2) or from global memory (L2-resident), its stack in
+// LDS (bvh_stack words per thread).  Grid-stride over the device-side count;
+// workgroups with no entry leave before staging.
+__global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
   extern __shared__ int lds_hl[];
   const SceneDev& S = p.scene;
   const uint32_t n = p.lv_ctl->hl_n < p.lv_hlq_cap ? p.lv_ctl->hl_n : p.lv_hlq_cap;
+  const uint32_t nx = p.lv_ctl->xr_n < p.lv_xrq_cap ? p.lv_ctl->xr_n : p.lv_xrq_cap;
+  if (blockIdx.x * 256u >= (n > nx ? n : nx)) return;   // uniform per workgroup
   const Bvh4Node* nodes = S.bvh_root != BVH_NONE ? S.bvh : nullptr;
+  const float4* leaf4 = reinterpret_cast<const float4*>(S.bvh_sph32);
   int* stk = lds_hl + threadIdx.x;
+  if (stage && nodes) {
+    float4* l = reinterpret_cast<float4*>(lds_hl);
+    const int nn = S.n_nodes * (int)(sizeof(Bvh4Node) / 16);
+    for (int k = threadIdx.x; k < nn; k += 256) l[k] = reinterpret_cast<const float4*>(S.bvh)[k];
+    for (int k = threadIdx.x; k < S.n_slots; k += 256) l[nn + k] = leaf4[k];
+    __syncthreads();
+    nodes = reinterpret_cast<const Bvh4Node*>(l);
+    leaf4 = l + nn;
+    stk += (nn + S.n_slots) * 4;
+  }
   for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
     const double2* q = reinterpret_cast<const double2*>(p.lv_hlq + (size_t)e * HLQ_DOUBLES);
     const double2 a = q[0], b = q[1], c = q[2], d = q[3];
@@ -1914,14 +1929,12 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p) {
     const uint32_t rec = (uint32_t)__builtin_bit_cast(uint64_t, d.x);
     uint32_t err = 0;
     highlight_leaves_att(S, r, [] { return v3(0.0, 0.0, 0.0); }, [](V3) {}, err, [&](V3 T, V3 L, double rad) {
-      return lit_area_raises(S, nodes, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, stk, 256, T, L,
-                             rad);
+      return lit_area_raises(S, nodes, leaf4, S.bvh_sph64, stk, 256, T, L, rad);
     });
     uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)rec * p.lv_rec_bytes);
     *h = (*h & ~0xffu) | (err & 0xffu);
   }
   // exact_raises: every light's lit_area from a listed hit's target (world.rb:72-80)
-  const uint32_t nx = p.lv_ctl->xr_n < p.lv_xrq_cap ? p.lv_ctl->xr_n : p.lv_xrq_cap;
   for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < nx; e += gridDim.x * 256) {
     const double2* q = reinterpret_cast<const double2*>(p.lv_xrq + (size_t)e * 4);
     const double2 a = q[0], b = q[1];
@@ -1930,8 +1943,7 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p) {
     bool raised = false;
     for (int l = 0; l < S.n_light && !raised; l++) {
       const LightDev& L = S.light[l];
-      raised = lit_area_raises(S, nodes, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, stk, 256, T,
-                               v3p(L.pos), L.radius);
+      raised = lit_area_raises(S, nodes, leaf4, S.bvh_sph64, stk, 256, T, v3p(L.pos), L.radius);
     }
     if (raised) {
       uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + off);
@@ -1942,11 +1954,15 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p) {
 
 static hipError_t launch_hl_raise(const KParams& q, hipStream_t s) {
   if (q.scene.n_light == 0 || !q.lv_hlq) return hipSuccess;
-  const size_t lds = (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
+  // the hierarchy staged in LDS when small (C2: 2.3 KB; every workgroup with entries copies it)
+  const size_t hier = (size_t)q.scene.n_nodes * sizeof(Bvh4Node) + (size_t)q.scene.n_slots * 16;
+  const int stage = q.scene.bvh_root != BVH_NONE && hier <= 16 * 1024 ? 1 : 0;
+  const size_t lds = (stage ? hier : 0) + (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
   int cus = 0, per_cu = 0;
   hipError_t e = launch_fit(reinterpret_cast<const void*>(k_hl_raise), 256, lds, cus, per_cu);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_hl_raise, dim3((unsigned)std::max(1, cus * std::min(per_cu, 4))), dim3(256), lds, s, q);
+  hipLaunchKernelGGL(k_hl_raise, dim3((unsigned)std::max(1, cus * std::min(per_cu, 4))), dim3(256), lds, s, q,
+                     stage);
   return hipGetLastError();
 }
 
