@@ -1897,15 +1897,64 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
 // World#high_lights for one listed ray, now with lit_area_raises for every
 // light that fires (in light order, after that light's own cos raise, as
 // rt_map meets them), and rewrites the raise byte of the ray's record.  The
-// walk reads the hierarchy from LDS when the launcher staged it (`stage`:
-// small hierarchies, C2) or from global memory (L2-resident), its stack in
-// LDS (bvh_stack words per thread).  Grid-stride over the device-side count;
-// workgroups with no entry leave before staging.
+// walk reads the hierarchy from LDS when the launcher staged it (`stage` 1:
+// small hierarchies) or from global memory (L2-resident), its stack in LDS
+// (bvh_stack words per thread).  `stage` 2 (scenes of at most 256 spheres,
+// C2): one wave per listed ray instead, its lanes testing the spheres side by
+// side (lit_area raises iff some sphere's cover_area does, whatever the
+// order), which replaces a lane's walk over the whole cone by a few ballots.
+// Grid-stride over the device-side counts; workgroups with no entry leave.
+__device__ __forceinline__ bool lit_area_raises_wave(const SceneDev& S, V3 T, V3 L, double radius) {
+  if (!(radius > 0.0) || S.n_sphere == 0) return false;   // as lit_area_raises
+  const V3 lt = vsub(L, T);
+  for (int b = 0; b < S.n_sphere; b += 64) {
+    const int i = b + (int)__lane_id();
+    bool r = false;
+    if (i < S.n_sphere) {
+      const Sphere64 sp = S.sph64[i];
+      r = penumbra_raises(v3p(sp.c), sp.r, T, lt, radius);
+    }
+    if (__ballot(r)) return true;
+  }
+  return false;
+}
+
 __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
   extern __shared__ int lds_hl[];
   const SceneDev& S = p.scene;
   const uint32_t n = p.lv_ctl->hl_n < p.lv_hlq_cap ? p.lv_ctl->hl_n : p.lv_hlq_cap;
   const uint32_t nx = p.lv_ctl->xr_n < p.lv_xrq_cap ? p.lv_ctl->xr_n : p.lv_xrq_cap;
+  if (stage == 2) {                           // one wave per entry (every lane loads it: uniform flow)
+    const uint32_t w0 = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
+    for (uint32_t e = w0; e < n; e += nw) {
+      const double2* q = reinterpret_cast<const double2*>(p.lv_hlq + (size_t)e * HLQ_DOUBLES);
+      const double2 a = q[0], b = q[1], c = q[2], d = q[3];
+      Ray r;
+      r.o = v3(a.x, a.y, b.x);
+      r.d = v3(b.y, c.x, c.y);
+      const uint32_t rec = (uint32_t)__builtin_bit_cast(uint64_t, d.x);
+      uint32_t err = 0;
+      highlight_leaves_att(S, r, [] { return v3(0.0, 0.0, 0.0); }, [](V3) {}, err,
+                           [&](V3 T, V3 L, double rad) { return lit_area_raises_wave(S, T, L, rad); });
+      if (__lane_id() == 0) {
+        uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)rec * p.lv_rec_bytes);
+        *h = (*h & ~0xffu) | (err & 0xffu);
+      }
+    }
+    for (uint32_t e = w0; e < nx; e += nw) {
+      const double2* q = reinterpret_cast<const double2*>(p.lv_xrq + (size_t)e * 4);
+      const double2 a = q[0], b = q[1];
+      const V3 T = v3(a.x, a.y, b.x);
+      bool raised = false;
+      for (int l = 0; l < S.n_light && !raised; l++)
+        raised = lit_area_raises_wave(S, T, v3p(S.light[l].pos), S.light[l].radius);
+      if (raised && __lane_id() == 0) {
+        uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)__builtin_bit_cast(uint64_t, b.y));
+        *h = (*h & ~0xffu) | (uint32_t)ERR_DOMAIN;
+      }
+    }
+    return;
+  }
   if (blockIdx.x * 256u >= (n > nx ? n : nx)) return;   // uniform per workgroup
   const Bvh4Node* nodes = S.bvh_root != BVH_NONE ? S.bvh : nullptr;
   const float4* leaf4 = reinterpret_cast<const float4*>(S.bvh_sph32);
@@ -1954,10 +2003,11 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
 
 static hipError_t launch_hl_raise(const KParams& q, hipStream_t s) {
   if (q.scene.n_light == 0 || !q.lv_hlq) return hipSuccess;
-  // the hierarchy staged in LDS when small (C2: 2.3 KB; every workgroup with entries copies it)
+  // up to 256 spheres: a wave per entry over the spheres (C2); else the walk, the
+  // hierarchy staged in LDS when small (every workgroup with entries copies it)
   const size_t hier = (size_t)q.scene.n_nodes * sizeof(Bvh4Node) + (size_t)q.scene.n_slots * 16;
-  const int stage = q.scene.bvh_root != BVH_NONE && hier <= 16 * 1024 ? 1 : 0;
-  const size_t lds = (stage ? hier : 0) + (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
+  const int stage = q.scene.n_sphere <= 256 ? 2 : q.scene.bvh_root != BVH_NONE && hier <= 16 * 1024 ? 1 : 0;
+  const size_t lds = stage == 2 ? 0 : (stage ? hier : 0) + (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
   int cus = 0, per_cu = 0;
   hipError_t e = launch_fit(reinterpret_cast<const void*>(k_hl_raise), 256, lds, cus, per_cu);
   if (e != hipSuccess) return e;
