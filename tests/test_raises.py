@@ -232,10 +232,11 @@ def _renderer(sd, cd, engine, **opts):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fillers", [0, 40])
+@pytest.mark.parametrize("fillers", [0, 40, 300])
 def test_gpu_highlight_lit_area_raise_matches_oracle(gpu, tmp_path, fillers):
     """Same raise code and first pixel from the oracle and every engine / walk
-    (40 filler spheres: the hierarchy walk of lit_area_raises)."""
+    (40 filler spheres: the hierarchy walk of lit_area_raises; 300: k_hl_raise's
+    wave-split walk over the depth-3 subtrees instead of its wave over the spheres)."""
     from oracle.c_oracle import Oracle
     from raytracing_rb_amd.runtime import RtxError
     sd, cd = _highlight_scene(tmp_path, fillers=fillers)
@@ -277,7 +278,7 @@ def test_gpu_highlight_raise_through_trace_and_path_trace(gpu, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["shadow_A", "shadow_B"])
-@pytest.mark.parametrize("fillers", [0, 40])
+@pytest.mark.parametrize("fillers", [0, 40, 300])
 def test_gpu_local_lights_factor0_raise_with_exact_raises(gpu, tmp_path, case, fillers):
     from oracle.c_oracle import Oracle
     from raytracing_rb_amd.runtime import RtxError
