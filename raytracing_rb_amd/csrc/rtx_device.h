@@ -836,14 +836,10 @@ __device__ __forceinline__ bool raise_sphere(const RaiseAxis& a, float cx, float
 // Does World#lit_area(T, L, radius) raise?  `nodes`/`leaf4`/`x64` are the
 // hierarchy (LDS or global; nullptr: every sphere in record order), `stk`
 // this lane's traversal stack (stride BS entries, free while this runs).
-// (stk: int or, SPH_BVH_QLDS, int16_t entries.)  split = lane l of a wave that
-// checks one lit_area together (k_hl_raise): the lane walks only the subtree
-// at depth 3 whose child digits are l (base 4), or its share of the spheres;
-// lit_area raises iff some lane's part does.
+// (stk: int or, SPH_BVH_QLDS, int16_t entries.)
 template <typename SP>
 __device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Node* nodes, const float4* leaf4,
-                                                const Sphere64* x64, SP stk, int bs, V3 T, V3 L, double radius,
-                                                int split = -1) {
+                                                const Sphere64* x64, SP stk, int bs, V3 T, V3 L, double radius) {
   if (!(radius > 0.0) || S.n_sphere == 0) return false;   // r1 <= 0: no d with |R - r1| < d < r1 + R
   const V3 lt = vsub(L, T);
   RaiseAxis a;
@@ -859,7 +855,7 @@ __device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Nod
                    __builtin_isfinite(a.k) && __builtin_isfinite(a.mg) && ln > 0.0f && sl.fin;
   if (nodes == nullptr || S.bvh_root == BVH_NONE || !fin) {
     // every sphere in record order (the float32 filter only where it is valid)
-    for (int i = split >= 0 ? split : 0; i < S.n_sphere; i += split >= 0 ? 64 : 1) {
+    for (int i = 0; i < S.n_sphere; i++) {
       if (fin && !raise_sphere(a, S.sph32[4 * i], S.sph32[4 * i + 1], S.sph32[4 * i + 2], S.sph32[4 * i + 3]))
         continue;
       const Sphere64 sp = S.sph64[i];
@@ -869,22 +865,6 @@ __device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Nod
   }
   int sp = 0;
   int ref = S.bvh_root;
-  if (split >= 0) {                              // down to this lane's subtree, by the same child tests
-    int dd = 0;
-    while (dd < 3 && ref >= 0 && ref != BVH_NONE) {
-      const int k = (split >> (2 * (2 - dd))) & 3;
-      const Bvh4Node& nd = nodes[ref];
-      const int ch = nd.child[k];
-      ref = ch != BVH_NONE && (slab_line(nd, k, sl) || raise_box(a, nd.lh[0][k][0], nd.lh[0][k][1], nd.lh[1][k][0],
-                                                                 nd.lh[1][k][1], nd.lh[2][k][0], nd.lh[2][k][1]))
-                ? ch
-                : BVH_NONE;
-      dd++;
-    }
-    // a leaf above depth 3 is reached by several lanes: the one whose remaining digits are 0 takes it
-    if (ref != BVH_NONE && (split & ((1 << (2 * (3 - dd))) - 1)) != 0) ref = BVH_NONE;
-    if (ref == BVH_NONE) return false;
-  }
   while (true) {
     if (ref >= 0 && ref != BVH_NONE) {           // inner node: every child that may hold a raising sphere
       const Bvh4Node& nd = nodes[ref];

@@ -1899,12 +1899,11 @@ __global__ __launch_bounds__(256) void k_tree_finalize_extra(KParams p, int nlev
 // rt_map meets them), and rewrites the raise byte of the ray's record.  The
 // walk reads the hierarchy from LDS when the launcher staged it (`stage` 1:
 // small hierarchies) or from global memory (L2-resident), its stack in LDS
-// (bvh_stack words per thread).  One wave per listed ray instead: `stage` 2
-// (scenes of at most 256 spheres, C2) its lanes test the spheres side by side,
-// `stage` 3 (larger hierarchies, C4) each lane walks one depth-3 subtree
-// (lit_area raises iff some sphere's cover_area does, whatever the order), so
-// a lane's walk over the whole line and cone becomes 64 short ones and a
-// ballot.  Grid-stride over the device-side counts; workgroups with no entry leave.
+// (bvh_stack words per thread).  `stage` 2 (scenes of at most 256 spheres,
+// C2): one wave per listed ray instead, its lanes testing the spheres side by
+// side (lit_area raises iff some sphere's cover_area does, whatever the
+// order), which replaces a lane's walk over the whole cone by a few ballots.
+// Grid-stride over the device-side counts; workgroups with no entry leave.
 __device__ __forceinline__ bool lit_area_raises_wave(const SceneDev& S, V3 T, V3 L, double radius) {
   if (!(radius > 0.0) || S.n_sphere == 0) return false;   // as lit_area_raises
   const V3 lt = vsub(L, T);
@@ -1925,15 +1924,8 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
   const SceneDev& S = p.scene;
   const uint32_t n = p.lv_ctl->hl_n < p.lv_hlq_cap ? p.lv_ctl->hl_n : p.lv_hlq_cap;
   const uint32_t nx = p.lv_ctl->xr_n < p.lv_xrq_cap ? p.lv_ctl->xr_n : p.lv_xrq_cap;
-  if (stage >= 2) {                           // one wave per entry (every lane loads it: uniform flow)
+  if (stage == 2) {                           // one wave per entry (every lane loads it: uniform flow)
     const uint32_t w0 = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
-    int* stk = lds_hl + threadIdx.x;
-    auto raises = [&](V3 T, V3 L, double rad) {
-      if (stage == 2) return lit_area_raises_wave(S, T, L, rad);
-      const bool r = lit_area_raises(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, stk, 256,
-                                     T, L, rad, (int)__lane_id());
-      return __ballot(r) != 0;
-    };
     for (uint32_t e = w0; e < n; e += nw) {
       const double2* q = reinterpret_cast<const double2*>(p.lv_hlq + (size_t)e * HLQ_DOUBLES);
       const double2 a = q[0], b = q[1], c = q[2], d = q[3];
@@ -1942,7 +1934,8 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
       r.d = v3(b.y, c.x, c.y);
       const uint32_t rec = (uint32_t)__builtin_bit_cast(uint64_t, d.x);
       uint32_t err = 0;
-      highlight_leaves_att(S, r, [] { return v3(0.0, 0.0, 0.0); }, [](V3) {}, err, raises);
+      highlight_leaves_att(S, r, [] { return v3(0.0, 0.0, 0.0); }, [](V3) {}, err,
+                           [&](V3 T, V3 L, double rad) { return lit_area_raises_wave(S, T, L, rad); });
       if (__lane_id() == 0) {
         uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)rec * p.lv_rec_bytes);
         *h = (*h & ~0xffu) | (err & 0xffu);
@@ -1954,7 +1947,7 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
       const V3 T = v3(a.x, a.y, b.x);
       bool raised = false;
       for (int l = 0; l < S.n_light && !raised; l++)
-        raised = raises(T, v3p(S.light[l].pos), S.light[l].radius);
+        raised = lit_area_raises_wave(S, T, v3p(S.light[l].pos), S.light[l].radius);
       if (raised && __lane_id() == 0) {
         uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)__builtin_bit_cast(uint64_t, b.y));
         *h = (*h & ~0xffu) | (uint32_t)ERR_DOMAIN;
@@ -2010,12 +2003,11 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
 
 static hipError_t launch_hl_raise(const KParams& q, hipStream_t s) {
   if (q.scene.n_light == 0 || !q.lv_hlq) return hipSuccess;
-  // up to 256 spheres: a wave per entry over the spheres (C2); larger hierarchies: a wave
-  // per entry over the depth-3 subtrees (C4).  (Stage 1, a lane's walk over the hierarchy
-  // staged in LDS, and 0, a lane's walk over global memory, stay for diagnostic builds.)
+  // up to 256 spheres: a wave per entry over the spheres (C2); else the walk, the
+  // hierarchy staged in LDS when small (every workgroup with entries copies it)
   const size_t hier = (size_t)q.scene.n_nodes * sizeof(Bvh4Node) + (size_t)q.scene.n_slots * 16;
-  const int stage = q.scene.n_sphere <= 256 ? 2 : q.scene.bvh_root != BVH_NONE ? 3 : 0;
-  const size_t lds = stage == 2 ? 0 : (stage == 1 ? hier : 0) + (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
+  const int stage = q.scene.n_sphere <= 256 ? 2 : q.scene.bvh_root != BVH_NONE && hier <= 16 * 1024 ? 1 : 0;
+  const size_t lds = stage == 2 ? 0 : (stage ? hier : 0) + (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
   int cus = 0, per_cu = 0;
   hipError_t e = launch_fit(reinterpret_cast<const void*>(k_hl_raise), 256, lds, cus, per_cu);
   if (e != hipSuccess) return e;
