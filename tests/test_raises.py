@@ -236,7 +236,7 @@ def _renderer(sd, cd, engine, **opts):
 def test_gpu_highlight_lit_area_raise_matches_oracle(gpu, tmp_path, fillers):
     """Same raise code and first pixel from the oracle and every engine / walk
     (40 filler spheres: the hierarchy walk of lit_area_raises; 300: k_hl_raise's
-    wave-split walk over the depth-3 subtrees instead of its wave over the spheres)."""
+    per-lane walk instead of its wave over the spheres, used up to 256 spheres)."""
     from oracle.c_oracle import Oracle
     from raytracing_rb_amd.runtime import RtxError
     sd, cd = _highlight_scene(tmp_path, fillers=fillers)
