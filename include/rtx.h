@@ -314,7 +314,7 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          changes no bit), "kernel_events" (1: time the ray-tree launches, rtx_kernel_time),
          "engine" (0 persistent lanes: one camera sample's ray tree per lane; 1 [default] bounce levels: one launch
          per tree level, one ray per lane; same bits), "lv_batch" (bounce levels: camera samples per batch,
-         2^23), "lv_stage_pct" / "lv_rec_pct" (bounce-level buffer capacities in % of a batch's samples,
+         2^24), "lv_stage_pct" / "lv_rec_pct" (bounce-level buffer capacities in % of a batch's samples,
          300 / 1600, and at least "lv_floor" staging / 4 x "lv_floor" tree records, 2^20; samples that
          overflow them are re-rendered by the lanes engine, same bits), "lv_split" (bounce levels: 0 one fused
          launch per level, 1 three launches per level over dense queues: trace, shadow, shade; same bits; used up
