@@ -10,7 +10,11 @@
 * GPU: the default engine, whole frames on the device, median of 5 (C4: 3).
 * RMS vs oracle: per channel over the pixels the CPU run rendered.
 * Multi-GPU: every rank's share of an N-rank tiled frame timed alone on this
-  GPU (rtx_render_tiles_device); projected frame = max over ranks.
+  GPU, one frame at a time: every share warmed up once, then 5 rounds with
+  the rank order rotated by one per round (drift spreads over all ranks),
+  per-rank median; projected frame = max over ranks.  Round-robin 8-row
+  tiles (rtx_render_tiles_device) and LPT tile lists by the whole frame's
+  measured rays (tiles.lpt_plan, rtx_render_tile_list_device).
 """
 import json
 import os
@@ -58,7 +62,7 @@ def main():
         print(name, "cpu", res["configs"][name], flush=True)
     import torch
     from raytracing_rb_amd.runtime import Renderer
-    from raytracing_rb_amd.tiles import rows_per_rank
+    from raytracing_rb_amd.tiles import rows_per_rank, lpt_plan, row_tile_costs
     dev = torch.device("cuda", 0)
     for name, w, c, stride, _, greps in CONFIGS:
         sd, cd = config.load_scene(os.path.join(ROOT, "scenes", w), os.path.join(ROOT, "scenes", c))
@@ -88,13 +92,30 @@ def main():
                  exact_px=float(np.mean(np.all(d == 0, axis=2))))
         proj = {}
         if name in ("C2", "C4"):
+            rays = r.tile_rays()                     # of the whole-frame renders above
+            rounds = 5
             for n in (2, 4, 8):
-                R = rows_per_rank(H, 8, n)
-                packed = torch.empty((R, W, 3), dtype=torch.float64, device=dev)
-                shares = [timed(lambda k=k: r.render_tiles_device(packed.data_ptr(), 8, k, n), max(1, greps - 2))
-                          for k in range(n)]
-                proj[str(n)] = {"max_rank_ms": max(shares) * 1e3, "projected_speedup": t1 / max(shares),
-                                "projected_mpix_s": W * H / max(shares) / 1e6}
+                plan = lpt_plan(row_tile_costs(rays, 8), n)
+                rows = max(rows_per_rank(H, 8, n), len(plan[0]) * 8)
+                packed = torch.empty((rows, W, 3), dtype=torch.float64, device=dev)
+                for kind in ("rr", "lpt"):
+                    def share(k):
+                        if kind == "rr":
+                            r.render_tiles_device(packed.data_ptr(), 8, k, n)
+                        else:
+                            r.render_tile_list_device(packed.data_ptr(), plan[k], 8)
+                    for k in range(n):
+                        timed(lambda k=k: share(k), 1)      # warm-up
+                    per = [[] for _ in range(n)]
+                    for rnd in range(rounds):
+                        for j in range(n):
+                            k = (j + rnd) % n
+                            per[k].append(timed(lambda k=k: share(k), 1))
+                    ms = [float(np.median(v)) for v in per]
+                    proj.setdefault(str(n), {})[kind] = {
+                        "rank_ms": [round(v * 1e3, 4) for v in ms], "max_rank_ms": max(ms) * 1e3,
+                        "rank_spread": (max(ms) - min(ms)) / max(ms), "projected_speedup": t1 / max(ms),
+                        "projected_mpix_s": W * H / max(ms) / 1e6}
             e["projection"] = proj
         print(name, "gpu", {k: v for k, v in e.items() if not k.startswith("cpu")}, flush=True)
         r.close()
