@@ -186,6 +186,23 @@ def test_bvh_edge_scenes_bit_identical(gpu, tmp_path):
             assert _same_bits(_render(sd, cd, BVH_ALWAYS, src), lin), (name, src)
 
 
+def test_quantized_leaves_refused_fall_back(gpu, tmp_path):
+    """Spheres a million units apart: the 16-bit grid is too coarse for the
+    pre-test's margin (the host's q_ok check, tests/test_qleaf.py), so
+    sphere_src 4 runs the nodes in LDS with float32 leaves from global memory
+    (sph_mode_effective 4); the same bits as the ordered linear walk."""
+    from raytracing_rb_amd.runtime import Renderer
+    spheres = [([5 + k, -1.5 + 0.7 * k, -0.3 + 0.2 * k], 0.45, k % 3) for k in range(6)]
+    spheres += [([1e6, 0.0, 0.0], 1.0, 0), ([-1e6, 3.0, 0.0], 1.0, 1), ([0.0, 1e6, 2.0], 1.0, 2)]
+    world = _write(tmp_path, "far.yml", spheres)
+    sd, cd = _scene(world, "c2_camera.yml", width=96, height=54, pre_sample_times=2, max_sample_times=2)
+    r = Renderer(sd, cd, device=0)
+    r.set_option("bvh", BVH_ALWAYS)
+    r.set_option("sphere_src", 4)
+    assert r.get_option("sph_mode_effective") == 4
+    assert _same_bits(_render(sd, cd, BVH_ALWAYS, 4), _render(sd, cd, BVH_OFF))
+
+
 def test_bvh_edge_scenes_match_oracle(gpu, tmp_path):
     from oracle.c_oracle import Oracle
     from test_gpu_parity import _check
