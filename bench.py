@@ -109,6 +109,39 @@ def cpu_baseline(col_stride=4):
                       % (col_stride, WORKLOAD.split(":")[0], r["px"], nprocs, r["dt"], model)}
 
 
+FIXTURES = {"c2": ("c2_full_columns64.npz", "c2_world.yml"), "c4": ("c4_full_columns256.npz", "c4_world.yml")}
+
+
+def fixture_parity(frame, workload):
+    """Per-channel RMS, max |delta|, bit-exact fraction and max u8 difference of a
+    rendered full-size frame (torch, device) against the committed C-oracle
+    fixture columns (tests/golden/make_golden.py; the test tolerance of
+    DESIGN.md §6: RMS <= 1e-4).  Bytes as array_to_color (camera.rb:153-156):
+    trunc(min(256 c, 255))."""
+    import hashlib
+    import numpy as np
+    name, world = FIXTURES[workload]
+    path = os.path.join(ROOT, "tests", "golden", name)
+    z = np.load(path)
+    with open(os.path.join(ROOT, "scenes", world), "rb") as f:
+        if str(z["scene_sha"]) != hashlib.sha256(f.read()).hexdigest():
+            return {"fixture": "tests/golden/" + name, "error": "scene differs from the fixture's"}
+    cols = z["columns"]
+    got = frame[:, cols.tolist(), :].cpu().numpy()
+    ref = z["frame"]
+    if got.shape != ref.shape:
+        return {"fixture": "tests/golden/" + name, "error": "shape %s vs %s" % (got.shape, ref.shape)}
+    d = got - ref
+    u8 = lambda a: np.trunc(np.minimum(a * 256.0, 255.0)).astype(np.int64)
+    rms = np.sqrt((d ** 2).mean(axis=(0, 1)))
+    return {"fixture": "tests/golden/" + name, "columns": int(len(cols)), "pixels": int(ref.shape[0] * len(cols)),
+            "frame": "the last timed frame", "rms": [float("%.3g" % v) for v in rms],
+            "max_abs": float("%.3g" % np.abs(d).max()),
+            "bit_exact_frac": round(float(np.all(d == 0, axis=2).mean()), 6),
+            "u8_max": int(np.abs(u8(got) - u8(ref)).max()), "tolerance_rms": 1e-4,
+            "pass": bool((rms <= 1e-4).all())}
+
+
 def launch_ranks(args):
     """--gpus N > 1 without torch.distributed.run: start the N ranks as a child
     torch.distributed.run (this process never touches the GPU) and return its status."""
@@ -205,8 +238,10 @@ def main():
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # CPU test of the rank plumbing
     args = ap.parse_args()
     globals()["TILE_ROWS"] = args.tile_rows      # every share / gather of this run
-    if args.balance == "auto":
-        args.balance = "lpt" if args.gpus >= 8 else "rr"
+    if args.balance == "lpt" and args.tile_rows % 8:
+        ap.error("--balance lpt needs --tile-rows a multiple of 8 (its costs are the 8x8 tiles' ray counts)")
+    if args.balance == "auto":               # (lpt's costs come in 8x8 tiles: rr for other tile heights)
+        args.balance = "lpt" if args.gpus >= 8 and args.tile_rows % 8 == 0 else "rr"
 
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
@@ -340,13 +375,21 @@ def main():
         # are rendered AND gathered inside it.
         plan = None
         if args.balance == "lpt":
-            # every rank renders the whole frame once (outside the timed region)
-            # and derives the same plan from the same ray counts
-            full0 = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
-            rs[0].render_device(full0.data_ptr(), seed=1, stream=streams[0].cuda_stream)
-            torch.cuda.synchronize(dev)
-            plan = lpt_plan(row_tile_costs(rs[0].tile_rays(), TILE_ROWS), world)
-            del full0
+            # rank 0 renders the whole frame once (outside the timed region),
+            # derives the plan from its tiles' ray counts and broadcasts it: one
+            # plan for every rank even if ray counts differed between ranks (a
+            # re-rendered overflow sample's rays are not counted)
+            if rank == 0:
+                full0 = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+                rs[0].render_device(full0.data_ptr(), seed=1, stream=streams[0].cuda_stream)
+                torch.cuda.synchronize(dev)
+                plan = lpt_plan(row_tile_costs(rs[0].tile_rays(), TILE_ROWS), world)
+                del full0
+            box = [plan]
+            if world > 1:
+                dist.broadcast_object_list(box, src=0, device=dev)
+            plan = box[0]
+            assert len({len(l) for l in plan}) == 1, "LPT plan lists must be equally long (one gather size)"
         pipe = PipelinedTiles(rs, streams, W, H, TILE_ROWS, rank, world, dev, seed=1,
                               force_collective=args.force_collective, plan=plan)
         df = pipe.df
@@ -385,6 +428,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     check_raises()
+
+    # ---- the last timed frame against the committed oracle fixture (data, not
+    # the oracle): every 64th (C2) / 256th (C4) column of the full-size frame
+    parity = None
+    if rank == 0 and emulate is None:
+        last = df.frame if dist_step else frames[(counter[0] - 1) % F]
+        parity = fixture_parity(last, args.workload)
 
     # ---- the gathered frame equals one whole-frame render, bit for bit (rank 0)
     gather_check = None
@@ -560,6 +610,8 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "frames_in_flight": F,
             "frame_latency_ms": round(latency_ms, 4) if latency_ms is not None else None,
+            # SURVEY.md §8(d)'s one-frame-at-a-time rate: W*H / frame_latency_ms
+            "value_single_frame": round(W * H / latency_ms / 1e3, 3) if latency_ms else None,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -611,6 +663,8 @@ def main():
             "cpu_baseline": cpu,
             "work_counts": counts,
         }
+        if parity is not None:
+            line["parity"] = parity
         if gather_check is not None:
             line["gather_check"] = gather_check
         if rank_breakdown is not None:

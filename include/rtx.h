@@ -339,12 +339,7 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          only the covers the walk evaluates; World#high_lights' lit_area is checked either way; same colours),
          "lv_hl_cap" (bounce levels: entries of the batch's list of highlight rays whose lit_area raise is checked
          after the levels (k_hl_raise); 0 [default] = 1/256 of the tree-record capacity, at least 4096; a ray that
-         finds it full has its sample re-rendered by the lanes engine; same bits), "lv_refill" (0 [default]: each
-         wave of the bounce-level kernel walks one chunk of 64 rays at a time; k in 1..64: a lane whose nearest-hit
-         walk ended takes the next ray while the others' walks continue until fewer than k lanes still walk; once a
-         wave has 64 hits parked its running walks finish before it shades them; hierarchy-in-LDS sphere modes 5
-         and 6 with a hit ring; same bits), "lv_refill_save" (1: with lv_refill, walks still running when 64 hits
-         are parked are suspended across the shading half, saved to a device buffer; 0 [default]). */
+         finds it full has its sample re-rendered by the lanes engine; same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

@@ -85,15 +85,12 @@ struct rtx_context {
   int64_t opt_lv_static = -1;        // bounce levels: % of a launch's chunks scheduled statically (-1 auto)
   int64_t opt_lv_compact = -1;       // bounce levels: 1 = park hits in an LDS ring and shade full waves, -1 auto (when it fits)
   int64_t opt_lv_grid_div = 1;       // bounce levels: persistent level grids = resident workgroups / this
-  int64_t opt_lv_fin_cap = 0;        // bounce levels: tree records per tile gathered into LDS by the reduction (0: off; measured slower)
   int64_t opt_lv_fin_grid = 0;       // bounce levels: tree reduction blocks per CU (grid-stride over tiles), 0 = one block per tile
   int64_t opt_lv_redo_blocks = 8;    // bounce levels: workgroups of the overflow re-render launch (0: all resident)
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   int64_t opt_lv_ray_bytes = 0;      // bounce levels: staged ray record, 0 auto (80 B when every path fits 32 bits), 80, 96
   int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
   int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also run the raise walk of the covers they skip
-  int64_t opt_lv_refill = 0;         // k_level_c: refill lanes whose walk ended while fewer than this many walk (0 off)
-  int64_t opt_lv_refill_save = 0;    // 1: refill walks suspended across the shading half (saved); 0: finished first
   int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
@@ -451,10 +448,9 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_stage_pct", c->opt_lv_stage_pct}, {"lv_rec_pct", c->opt_lv_rec_pct}, {"lv_floor", c->opt_lv_floor},
       {"lv_split", c->opt_lv_split}, {"lv_static", c->opt_lv_static}, {"lv_compact", c->opt_lv_compact},
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
-      {"lv_redo_blocks", c->opt_lv_redo_blocks}, {"lv_fin_cap", c->opt_lv_fin_cap},
+      {"lv_redo_blocks", c->opt_lv_redo_blocks},
       {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
-      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_refill", c->opt_lv_refill},
-      {"lv_refill_save", c->opt_lv_refill_save}};
+      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -538,24 +534,9 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
     c->opt_lv_fin_grid = value;
     return RTX_OK;
   }
-  if (!strcmp(key, "lv_fin_cap")) {        // bounce levels: LDS tree records per tile in the reduction, 0 = off
-    if (value < 0 || value > 4096) return fail(c, RTX_EINVAL, "lv_fin_cap must be in [0, 4096]");
-    c->opt_lv_fin_cap = value;
-    return RTX_OK;
-  }
   if (!strcmp(key, "lv_hl_cap")) {         // bounce levels: deferred highlight-check list entries, 0 auto
     if (value < 0 || value > (1 << 26)) return fail(c, RTX_EINVAL, "lv_hl_cap must be in [0, 2^26]");
     c->opt_lv_hl_cap = value;
-    return RTX_OK;
-  }
-  if (!strcmp(key, "lv_refill")) {         // k_level_c: lanes take new rays while fewer than this many walk (0 off)
-    if (value < 0 || value > 64) return fail(c, RTX_EINVAL, "lv_refill must be in [0, 64]");
-    c->opt_lv_refill = value;
-    return RTX_OK;
-  }
-  if (!strcmp(key, "lv_refill_save")) {    // refill: suspend walks across the shading half (1) or finish them (0)
-    if (value != 0 && value != 1) return fail(c, RTX_EINVAL, "lv_refill_save must be 0 or 1");
-    c->opt_lv_refill_save = value;
     return RTX_OK;
   }
   if (!strcmp(key, "exact_raises")) {      // every shadow walk also checks the skipped covers' acos raises
@@ -1064,13 +1045,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // others' levels).  The extra-sample list and the statistics are shared
   // (appended / added atomically); each part has its own level buffers, its
   // own lanes-engine work counter and ray stacks for its overflow re-render.
-  // lv_refill: one save area per resident wave of k_level_c (2 per SIMD, 4 SIMDs per CU) for the walks
-  // suspended across a shading half
-  if (!c->n_cus) HIPCHK(c, hipDeviceGetAttribute(&c->n_cus, hipDeviceAttributeMultiprocessorCount, c->device));
-  const size_t save_waves = c->opt_lv_refill > 0 && c->opt_lv_refill_save ? (size_t)c->n_cus * 8 : 0;
-  const size_t sz_save =
-      al256(save_waves * ((size_t)LV_SAVE_DBL * 64 * 8 + (size_t)std::max(1, c->scene.bvh_stack) * 64 * 4));
-  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_xrq + sz_save;
+  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_xrq;
   const size_t total = parts * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
@@ -1089,17 +1064,12 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_hlq_cap = (uint32_t)hlcap;
     k.lv_xrq = xrcap ? (double*)q : nullptr;  q += sz_xrq;
     k.lv_xrq_cap = (uint32_t)xrcap;
-    k.lv_save = save_waves ? (double*)q : nullptr;
-    k.lv_save_waves = (int32_t)save_waves;
-    k.lv_refill = (int32_t)c->opt_lv_refill;
-    k.lv_refill_save = (int32_t)c->opt_lv_refill_save;
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;
   p.lv_compact = (int32_t)c->opt_lv_compact;
   p.lv_grid_div = (int32_t)c->opt_lv_grid_div;
   p.lv_redo_blocks = (int32_t)c->opt_lv_redo_blocks;
-  p.lv_fin_cap = (int32_t)c->opt_lv_fin_cap;   // the launcher turns it off when the rings do not fit LDS
   p.lv_fin_tiles = (int32_t)c->opt_lv_fin_grid;   // (blocks per CU here; the launcher sets the tile count)
   // Static chunks cost no atomics; dynamic claims balance rays of very
   // different cost.  Auto: all static while the sphere records fit one walk
@@ -1257,13 +1227,19 @@ rtx_status rtx_render_tile_list_device(rtx_context* c, const int32_t* tiles, int
   if (s) return s;
   if (n == 0) return RTX_OK;
   const int ntiles = (c->cam.height + tile_rows - 1) / tile_rows;
-  for (int k = 0; k < n; k++)
-    if (tiles[k] < 0) return fail(c, RTX_EINVAL, "tile %d: negative index %d", k, tiles[k]);
+  if ((int64_t)n * tile_rows > INT32_MAX) return fail(c, RTX_EINVAL, "%d tiles of %d rows exceed 2^31 rows", n, tile_rows);
+  // an index past the bottom is padding: clamped to ntiles (rows y >= height render nothing), so no
+  // tile * tile_rows product can overflow on the device (row_to_y)
+  std::vector<int32_t> list(tiles, tiles + n);
+  for (int k = 0; k < n; k++) {
+    if (list[k] < 0) return fail(c, RTX_EINVAL, "tile %d: negative index %d", k, list[k]);
+    if (list[k] > ntiles) list[k] = ntiles;
+  }
   const int maxs = required_stack(c);
   if (maxs < 0) return fail(c, RTX_EINVAL, "trace_depth x monte_carlo_diffusion_times too large");
   if ((s = ensure_stack(c, p, maxs))) return s;
   hipSetDevice(c->device);
-  if (c->rowtiles.size() != (size_t)n || !std::equal(c->rowtiles.begin(), c->rowtiles.end(), tiles)) {
+  if (c->rowtiles != list) {
     if ((size_t)n > c->rowtiles_cap) {
       hipFree(c->d_rowtiles);
       c->d_rowtiles = nullptr;
@@ -1271,13 +1247,12 @@ rtx_status rtx_render_tile_list_device(rtx_context* c, const int32_t* tiles, int
       HIPCHK(c, hipMalloc(&c->d_rowtiles, (size_t)n * sizeof(int32_t)));
       c->rowtiles_cap = (size_t)n;
     }
-    c->rowtiles.assign(tiles, tiles + n);
+    c->rowtiles = list;
     // ordered before this call's launches on `stream` (a caller that changes
     // the list while another stream's render still reads it must sync first)
     HIPCHK(c, hipMemcpyAsync(c->d_rowtiles, c->rowtiles.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice,
                              (hipStream_t)stream));
   }
-  (void)ntiles;
   p.x0 = 0;
   p.nx = c->cam.width;
   p.nrows = n * tile_rows;

@@ -1017,9 +1017,9 @@ RTX_SHADE_FN void hit_info(const SceneDev& S, int obj, const Ray& ray, V3& hit, 
 // where a private-array entry, swizzled across the wave, touched 21).
 constexpr int ITEM_WORDS = 11;
 constexpr int GITEM_DOUBLES = 12;
-template <int MAXS>
 struct Stack {
   int n;
+  int maxs;        // entries a lane may hold (its global region's size; sized on the host)
   double* lds;     // this lane's word 0 of entry 0; word w of entry e at lds[(e * ITEM_WORDS + w) * bs]
   double* g;       // this lane's global region: entry e at g[e * GITEM_DOUBLES]
   int bs;
@@ -1080,12 +1080,11 @@ __device__ __forceinline__ void add_leaf(V3& sum, V3 c, uint32_t& err) {   // ra
 // one is held in `pend` (it is what Array#pop returns next) and only older
 // siblings are written to the stack.  A child rt_map would discard on pop
 // (ray_tracer.rb:52) is dropped here: no leaf, no RNG draw, no effect.
-template <int MAXS>
-__device__ __forceinline__ void emit(Stack<MAXS>& st, Item& pend, bool& has, uint32_t& err, const Ray& r,
+__device__ __forceinline__ void emit(Stack& st, Item& pend, bool& has, uint32_t& err, const Ray& r,
                                      V3 att, uint64_t path, int depth) {
   if (depth <= 0 || vr(att) < 0.0001) return;
   if (has) {
-    if (st.n < MAXS) st.push(pend);
+    if (st.n < st.maxs) st.push(pend);
     else seterr(err, ERR_DOMAIN);                // cannot happen: stack sized on the host
   }
   pend.ray = r;
@@ -1098,18 +1097,17 @@ __device__ __forceinline__ void emit(Stack<MAXS>& st, Item& pend, bool& has, uin
 // The rest of rt_map once every light's lit area is known (ray_tracer.rb:80-158):
 // reflection / refraction children, then path-tracing children (no lit light)
 // or the local-lighting leaf.  Returns true with the next ray in `cur`.
-template <int MAXS>
 RTX_SHADE_FN bool shade_finish(const SceneDev& S, const CameraDev& cam, uint64_t seed, int x, int y,
                                           int sample, int obj, bool in, V3 hit, V3 delta, V3 n, V3 nn, V3 lc,
                                           int nl,
-                                          Item& cur, Stack<MAXS>& st, V3& sum, uint32_t& err) {
+                                          Item& cur, Stack& st, V3& sum, uint32_t& err) {
   const Material& m = S.mat[obj];
   Item pend;
   bool has = false;
   const uint64_t R = (uint64_t)cam.pt + 3;
   const double c = vcos(cur.ray.d, n, err);
   const Ray refl = reflection(cur.ray, nn, c, hit, delta, err);
-  emit<MAXS>(st, pend, has, err, refl, vmul(cur.att, v3p(m.refl_att)), cur.path * R + 1, cur.depth - 1);
+  emit(st, pend, has, err, refl, vmul(cur.att, v3p(m.refl_att)), cur.path * R + 1, cur.depth - 1);
   Ray refr;
   bool has_refr = false;
   if (m.type == OBJ_SPHERE)                                  // sphere.rb:92-94: rate inverted leaving
@@ -1117,7 +1115,7 @@ RTX_SHADE_FN bool shade_finish(const SceneDev& S, const CameraDev& cam, uint64_t
   else if (m.has_rr)                                         // plane.rb:57-61: same rate both ways
     has_refr = refraction(cur.ray, nn, c, hit, refl.d, m.rr, refr, err);
   if (has_refr)
-    emit<MAXS>(st, pend, has, err, refr, vmul(cur.att, v3p(m.refr_att)), cur.path * R + 2, cur.depth - 1);
+    emit(st, pend, has, err, refr, vmul(cur.att, v3p(m.refr_att)), cur.path * R + 2, cur.depth - 1);
   if (nl == 0) {
     // WorldObject#path_tracing (world_object.rb:76-90) from hit + delta
     const int pt = cam.pt;
@@ -1134,7 +1132,7 @@ RTX_SHADE_FN bool shade_finish(const SceneDev& S, const CameraDev& cam, uint64_t
       RTX_SINCOS(theta, &sth, &cth);
       RTX_SINCOS(phi, &sph, &cph);
       r.d = vadd(vsc(front, sth), vsc(vadd(vsc(left, cph), vsc(up, sph)), cth));
-      emit<MAXS>(st, pend, has, err, r, att, cur.path * R + 3 + (uint64_t)k, cur.depth - 1);
+      emit(st, pend, has, err, r, att, cur.path * R + 3 + (uint64_t)k, cur.depth - 1);
     }
   } else {
     lc = vdiv(lc, (double)nl);

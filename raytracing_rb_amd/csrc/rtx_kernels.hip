@@ -45,7 +45,7 @@ namespace rtx {
 // pixels k_finalize listed.  SRC_RAYS: one lane per explicit ray running
 // RayTracer#trace_sync (rtx_trace).  SPH: where the sphere walk reads its
 // records (SphMode, rtx_launch.h).  BS: threads per workgroup.
-template <bool COUNT, int MAXS, int WPS, int SPH, int SRC, int BS, bool PP>
+template <bool COUNT, int WPS, int SPH, int SRC, int BS, bool PP>
 __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   const double* __restrict__ rays = p.rays;
   const int32_t* __restrict__ keys = p.keys;
@@ -96,12 +96,13 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
   if (COUNT)
     for (int k = 0; k < C_N; k++) cnt[k] = 0;
 
-  Stack<MAXS> st;
+  Stack st;
   st.n = 0;
+  st.maxs = p.lanes_maxs;
   st.bs = BS;
   st.slots = p.stk_slots;
   st.lds = reinterpret_cast<double*>(lds + p.lds_items) + threadIdx.x;
-  st.g = p.stk_glb + ((size_t)blockIdx.x * BS + threadIdx.x) * (MAXS * GITEM_DOUBLES);
+  st.g = p.stk_glb + ((size_t)blockIdx.x * BS + threadIdx.x) * ((size_t)p.lanes_maxs * GITEM_DOUBLES);
   uint32_t err = 0;
   V3 sum = v3(0.0, 0.0, 0.0), avg = sum;
   bool started = false;              // the current item's tree has begun
@@ -353,7 +354,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
       tC += t1 - t0;
       t0 = t1;
     }
-    have = shade_finish<MAXS>(S, cam, p.seed, x, y, sample, besti, hin, hit, delta, n, nn, lc, nl, cur, st, sum,
+    have = shade_finish(S, cam, p.seed, x, y, sample, besti, hin, hit, delta, n, nn, lc, nl, cur, st, sum,
                               err);
     mode = M_NEED;
     if (RTX_STAMPS) tD += stamp() - t0;
@@ -756,11 +757,12 @@ hipError_t launch_fit(const void* kern, int bs, size_t lds, int& cus, int& per_c
 // Persistent launch: as many workgroups as can be resident at once (the
 // occupancy API; an over-estimate only leaves blocks that start after the
 // pool is empty and exit at once), never more than the work needs.
-template <bool COUNT, int MAXS, int SPH, int SRC, bool PP = false>
-static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
+template <bool COUNT, int SPH, int SRC, bool PP = false>
+static hipError_t launch_one(KParams p, int maxs, int nwork, hipStream_t s) {
   constexpr int BS = (SPH == SPH_BVH_LDS || SPH == SPH_BVH_GLOBAL) ? BS_BVH : BS_LIN;
   const size_t lds = lds_layout(p, SPH, BS);
-  auto kern = k_render<COUNT, MAXS, RTX_WPS, SPH, SRC, BS, PP>;
+  p.lanes_maxs = maxs;
+  auto kern = k_render<COUNT, RTX_WPS, SPH, SRC, BS, PP>;
   int cus = 0, per_cu = 0;
   hipError_t e = launch_fit(reinterpret_cast<const void*>(kern), BS, lds, cus, per_cu);
   if (e != hipSuccess) return e;
@@ -787,31 +789,29 @@ static hipError_t launch_one(KParams p, int nwork, hipStream_t s) {
   return e;
 }
 
-template <bool COUNT, int MAXS, int SRC>
-static hipError_t launch_mode(const KParams& p, int mode, int nwork, hipStream_t s) {
+template <bool COUNT, int SRC>
+static hipError_t launch_mode(const KParams& p, int mode, int maxs, int nwork, hipStream_t s) {
   switch (mode) {
-    case SPH_LIN_LDS: return launch_one<COUNT, MAXS, SPH_LIN_LDS, SRC>(p, nwork, s);
-    case SPH_LIN_SCALAR: return launch_one<COUNT, MAXS, SPH_LIN_SCALAR, SRC>(p, nwork, s);
+    case SPH_LIN_LDS: return launch_one<COUNT, SPH_LIN_LDS, SRC>(p, maxs, nwork, s);
+    case SPH_LIN_SCALAR: return launch_one<COUNT, SPH_LIN_SCALAR, SRC>(p, maxs, nwork, s);
     case SPH_BVH_LDS:
-      if (!COUNT && p.postpone > 0) return launch_one<false, MAXS, SPH_BVH_LDS, SRC, true>(p, nwork, s);
-      if (!COUNT) return launch_one<false, MAXS, SPH_BVH_LDS, SRC>(p, nwork, s);
+      if (!COUNT && p.postpone > 0) return launch_one<false, SPH_BVH_LDS, SRC, true>(p, maxs, nwork, s);
+      if (!COUNT) return launch_one<false, SPH_BVH_LDS, SRC>(p, maxs, nwork, s);
       break;
     case SPH_BVH_GLOBAL:
-      if (!COUNT && p.postpone > 0) return launch_one<false, MAXS, SPH_BVH_GLOBAL, SRC, true>(p, nwork, s);
-      if (!COUNT) return launch_one<false, MAXS, SPH_BVH_GLOBAL, SRC>(p, nwork, s);
+      if (!COUNT && p.postpone > 0) return launch_one<false, SPH_BVH_GLOBAL, SRC, true>(p, maxs, nwork, s);
+      if (!COUNT) return launch_one<false, SPH_BVH_GLOBAL, SRC>(p, maxs, nwork, s);
       break;
   }
   return hipErrorInvalidValue;
 }
 
+// The lane's ray-stack depth (maxs: 8, 16, 32 or 64 entries, sized on the host
+// from the camera's tree depth) is a launch parameter, not a template axis.
 template <int SRC>
 static hipError_t launch_src(const KParams& p, int mode, bool count, int maxs, int nwork, hipStream_t s) {
-#define RTX_L(M)                                                                                     \
-  if (maxs == M)                                                                                     \
-    return count ? launch_mode<true, M, SRC>(p, mode, nwork, s) : launch_mode<false, M, SRC>(p, mode, nwork, s);
-  RTX_L(8) RTX_L(16) RTX_L(32) RTX_L(64)
-#undef RTX_L
-  return hipErrorInvalidValue;
+  if (maxs != 8 && maxs != 16 && maxs != 32 && maxs != 64) return hipErrorInvalidValue;
+  return count ? launch_mode<true, SRC>(p, mode, maxs, nwork, s) : launch_mode<false, SRC>(p, mode, maxs, nwork, s);
 }
 
 // Camera#render_at over a region: the pre samples of every pixel, the
@@ -869,13 +869,7 @@ hipError_t launch_trace(KParams p, int mode, int maxs, hipStream_t s) {
   if (p.nrays == 0) return hipSuccess;
   if (mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX || mode == SPH_BVH_QLDS) mode = SPH_BVH_LDS;   // (see launch_render)
   mode = resolve_mode(p.scene, mode);
-  switch (maxs) {
-    case 8: return launch_mode<false, 8, SRC_RAYS>(p, mode, p.nrays, s);
-    case 16: return launch_mode<false, 16, SRC_RAYS>(p, mode, p.nrays, s);
-    case 32: return launch_mode<false, 32, SRC_RAYS>(p, mode, p.nrays, s);
-    case 64: return launch_mode<false, 64, SRC_RAYS>(p, mode, p.nrays, s);
-  }
-  return hipErrorInvalidValue;
+  return launch_src<SRC_RAYS>(p, mode, false, maxs, p.nrays, s);
 }
 
 hipError_t launch_path_trace(KParams p, hipStream_t s) {

@@ -65,7 +65,8 @@ struct KParams {
   int32_t lds_mat, lds_sphr;       // SPH_BVH_LDSX: staged materials (per object) / Sphere64 records (per sphere)
   int32_t stk_slots;               // ray-stack entries per lane kept in LDS (set by the launcher)
   int32_t stk_slots_max;           // cap (option "lds_stack"; the stack bucket by default)
-  double* stk_glb;                 // per-lane regions: MAXS * 12 doubles of ray stack
+  double* stk_glb;                 // per-lane regions: lanes_maxs * 12 doubles of ray stack
+  int32_t lanes_maxs;              // lanes engine: ray-stack entries per lane (8, 16, 32 or 64; set by the launcher)
   int32_t stk_glb_lanes;           // lanes the buffer holds (the launcher caps the grid to it)
   // Camera#render_at in two steps (launch_render): per (pixel, sample) records
   // of 4 doubles {r, g, b, first raise} at samples[(pixel * max(pre, max) + j) * 4]
@@ -106,19 +107,12 @@ struct KParams {
   int32_t lv_last_level;           // trace_depth - 1 (-1 if trace_depth < 1): the level whose children are all
                                    // cut off, run by a k_level_c compiled for it
   int32_t lv_grid_div;             // level launches: persistent grid = resident workgroups / this (option lv_grid_div)
-  int32_t lv_fin_cap;              // tree reduction: records of a tile gathered into LDS (0: walk from global memory)
   int32_t lv_fin_tiles;            // tree reduction pass 0: tiles of the batch (grid-stride loop when the grid is smaller)
   int32_t lv_redo_blocks;          // the lanes-engine re-render of overflowed samples: at most this many workgroups (0: all resident)
   int32_t lv_ray_dbl;              // staged ray record, doubles: 10 (80 B: path < 2^32, RNG key decoded from the root) or 12
   int32_t exact_raises;            // 1: every shadow walk (local_lights) also runs lit_area_raises (option exact_raises)
   uint32_t lv_hlq_cap;             // entries of lv_hlq
   double* lv_hlq;                  // highlight rays of the batch whose lit_area raise k_hl_raise checks (8 doubles each)
-  int32_t lv_refill;               // k_level_c: lanes whose nearest-hit walk ended take new rays while fewer than
-                                   // this many still walk (0: one chunk of 64 rays per wave at a time; option lv_refill)
-  int32_t lv_refill_save;          // 1: walks suspended across a shading half (saved to lv_save); 0: they finish first
-  int32_t lv_save_waves;           // waves the walk save area holds (the launcher caps a refill grid to it)
-  double* lv_save;                 // per wave: suspended walks saved across a shading half (LV_SAVE_DBL * 64 doubles
-                                   // + bvh_stack * 64 ints)
   uint32_t lv_xrq_cap;             // entries of lv_xrq (0 without exact_raises)
   double* lv_xrq;                  // exact_raises: shading hits whose local_lights raises k_hl_raise checks (4 doubles each)
 };
@@ -140,9 +134,6 @@ enum SphMode : int {
                          // SPH_BVH_LDS next to a hit ring, e.g. C4; the lanes engine walks it as SPH_BVH_LDS)
 };
 
-// Suspended nearest-hit walk of k_level_c (option lv_refill): doubles per lane
-// before its traversal stack (LV_SAVE_DBL * 64 doubles, then bvh_stack * 64 ints per wave).
-constexpr int LV_SAVE_DBL = 13;
 
 // Sphere modes that walk the ball hierarchy.
 constexpr bool sph_is_bvh(int m) {

@@ -192,7 +192,7 @@ struct LvQueue {
   __device__ __forceinline__ bool item(uint32_t c, uint32_t& s, uint32_t& off, uint32_t& dense_i) const {
     return item_k(c, __lane_id(), s, off, dense_i);
   }
-  // the same for ray k (< 64) of chunk c instead of the lane's own (lv_refill)
+  // the same for ray k (< 64) of chunk c instead of the lane's own
   __device__ __forceinline__ bool item_k(uint32_t c, uint32_t k, uint32_t& s, uint32_t& off,
                                          uint32_t& dense_i) const {
     s = (uint32_t)__popcll(__ballot(cin <= c));
@@ -393,50 +393,6 @@ __device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V
                            cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf,
                            false, 0);
   }
-}
-
-// The nearest-hit walk, resumable (k_level_c with option lv_refill): returns
-// false when fewer than `postpone` lanes of the wave still walk, the walk
-// kept in ref / sp (+ the lane's LDS stack) and best / besti / hit / hin;
-// resume = true continues it (query_bvh's postponing: every lane visits the
-// same nodes and leaves in the same order, so the result is unchanged).
-template <int SPH, int BS>
-__device__ __forceinline__ bool lv_walk_ext_pp(const KParams& p, char* lds, V3 o, V3 d, double& best, int& besti,
-                                               V3& hit, bool& hin, uint32_t& err, int& ref, int& sp, bool resume,
-                                               int postpone) {
-  const SceneDev& S = p.scene;
-  int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
-  double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
-  int ncov = 0;
-  bool ovf = false;
-  double total = 0.0;
-  const Bvh4Node* nodes = reinterpret_cast<const Bvh4Node*>(lds);
-  if (SPH == SPH_BVH_QLDS) {
-    const QLeaf ql = {reinterpret_cast<const uint4*>(lds + p.lds_leaf), S.q_org[0], S.q_org[1], S.q_org[2],
-                      S.q_step[0], S.q_step[1], S.q_step[2], S.q_rstep};
-    return query_bvh<BS, true>(S, nodes, ql, S.bvh_sph64, S.bvh_obj, qstack(lds, p), cov_i, cov_v, true, o, d, hit,
-                               0.0, best, besti, hit, hin, total, err, ref, sp, ncov, ovf, resume, postpone);
-  }
-  int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
-  const float4* leaf4 = reinterpret_cast<const float4*>(lds + p.lds_leaf);
-  if (SPH == SPH_BVH_LDSX)
-    return query_bvh<BS, true>(S, nodes, leaf4, reinterpret_cast<const Sphere64*>(lds + p.lds_x64),
-                               reinterpret_cast<const int32_t*>(lds + p.lds_xobj), stk, cov_i, cov_v, true, o, d, hit,
-                               0.0, best, besti, hit, hin, total, err, ref, sp, ncov, ovf, resume, postpone);
-  return query_bvh<BS, true>(S, nodes, leaf4, S.bvh_sph64, S.bvh_obj, stk, cov_i, cov_v, true, o, d, hit, 0.0, best,
-                             besti, hit, hin, total, err, ref, sp, ncov, ovf, resume, postpone);   // SPH_BVH_LDS
-}
-
-// Stack entry e of this lane's nearest-hit walk in LDS (lv_refill's save / restore).
-template <int SPH, int BS>
-__device__ __forceinline__ int lv_stack_get(const KParams& p, char* lds, int e) {
-  if (SPH == SPH_BVH_QLDS) return qstack(lds, p)[e * BS];
-  return (reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x)[e * BS];
-}
-template <int SPH, int BS>
-__device__ __forceinline__ void lv_stack_set(const KParams& p, char* lds, int e, int v) {
-  if (SPH == SPH_BVH_QLDS) qstack(lds, p)[e * BS] = (int16_t)v;
-  else (reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x)[e * BS] = v;
 }
 
 // The ray of a level's queue entry: a camera sample (level 0: `idx` = its
@@ -823,7 +779,7 @@ constexpr int LV_RING_FIELDS_SMALL = 5;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
 constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMALL * 8;
 
-template <int SPH, int BS, int RF, bool LAST, bool REFILL>
+template <int SPH, int BS, int RF, bool LAST>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
   constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
@@ -842,20 +798,6 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * ((size_t)LV_RING * RF * 8));
   uint32_t head = 0, pend = 0;                // wave-uniform: first parked slot, parked hits
   bool got = true;
-  // lv_refill: the wave's pool (rays rf_next.. of chunk rf_chunk) and the
-  // lane's nearest-hit walk (rf_has: one is running or suspended)
-  uint32_t rf_chunk = 0, rf_next = 64;
-  bool rf_has = false, rf_started = false;
-  V3 rf_o = v3(0.0, 0.0, 0.0), rf_d = rf_o, rf_hit = rf_o;
-  double rf_best = 0.0;
-  int rf_besti = -1, rf_ref = BVH_NONE, rf_sp = 0;
-  bool rf_hin = true;
-  uint32_t rf_i = 0, rf_slot = 0, rf_errA = 0, rf_errL = 0;
-  // (wave-uniform values kept in scalar registers: the shading half runs at the VGPR limit)
-  double* const rf_sv =
-      REFILL ? p.lv_save + (size_t)(blockIdx.x * (BS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) *
-                               ((size_t)LV_SAVE_DBL * 64 + (size_t)S.bvh_stack * 32)
-             : nullptr;
 
   unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
   unsigned long long nA = 0, nE = 0, nS = 0;
@@ -866,8 +808,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     t0 = t1;             \
   }
   while (true) {
-    bool rf_saved = false;                    // lv_refill: suspended walks saved below
-    if constexpr (!REFILL) {
+    {                                         // first half, chunk by chunk, until 64 hits are parked
       uint32_t chunk = 0;
       if (got) got = sched.claim(in.chunks, chunk);   // (never again once exhausted)
       if (RTX_STAMPS) t0 = stamp();
@@ -963,150 +904,6 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       if (pend < 64 && (got || pend == 0)) {
         if (!got) break;                        // no chunk left and nothing parked
         continue;                               // not a full wave of hits yet
-      }
-    } else {
-      // ---- first half with refill (option lv_refill): a
-      // lane whose walk ended (or whose ray needs none) takes the next ray of
-      // the wave's pool, the current chunk, claiming the next chunk when it
-      // runs out; the walks run until fewer than lv_refill lanes still walk.
-      // Once 64 hits are parked the running walks finish first (no refill,
-      // no postponing), so the shading half starts with no walk suspended
-      // (lv_refill_save = 1: walks suspended across it, saved to lv_save).
-      const bool drain = !p.lv_refill_save && pend >= 64u;
-      while (!drain) {
-        const uint64_t needm = __ballot(!rf_has);
-        if (needm == 0) break;
-        if (rf_next >= 64u) {                 // pool empty: the next chunk
-          if (!got) break;
-          got = sched.claim(in.chunks, rf_chunk);
-          if (!got) break;
-          rf_chunk = __builtin_amdgcn_readfirstlane(rf_chunk);
-          rf_next = 0;
-        }
-        const uint32_t k = rf_next + (uint32_t)__popcll(needm & ((1ull << lane) - 1ull));
-        const bool take = !rf_has && k < 64u;
-        rf_next = __builtin_amdgcn_readfirstlane(min(64u, rf_next + (uint32_t)__popcll(needm)));
-        uint32_t s, off, i;
-        bool active = in.item_k(rf_chunk, take ? k : 0u, s, off, i) && take;
-        const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
-        const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
-        Item cur;
-        int root = 0, x = 0, y = 0, sample = 0;
-        bool alive = false;
-        if (active) {
-          bool valid = true;
-          if (level == 0) {
-            lv_ray(p, level, slot, cur, root, x, y, sample, valid);
-            p.lv_redo_of[i] = -1;
-          } else {
-            const double2 a = qs[0], b = qs[1], c = qs[2];
-            cur.ray.o = v3(a.x, a.y, b.x);
-            cur.ray.d = v3(b.y, c.x, c.y);
-          }
-          active = valid;
-          alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // ray_tracer.rb:52
-          if (active && base + i >= p.lv_lcap) {
-            lv_redo(p, level == 0 ? root : lv_ray_root(p, qs));
-            active = alive = false;
-          }
-        }
-        char* rec = p.lv_rec + (size_t)(base + i) * p.lv_rec_bytes;
-        double* leafp = reinterpret_cast<double*>(rec + 8);
-        uint32_t errA = 0;
-        int nleaf = 0;
-        bool fired = false, hl_defer = false;
-        if (alive)
-          fired = highlight_leaves_att(S, cur.ray, [&] {
-            if (level == 0) return cur.att;
-            const double2 d = qs[3], e = qs[4];
-            return v3(d.x, d.y, e.x);
-          }, [&](V3 c) {
-            leafp[3 * nleaf] = c.x;
-            leafp[3 * nleaf + 1] = c.y;
-            leafp[3 * nleaf + 2] = c.z;
-            nleaf++;
-          }, errA, [&](V3, V3, double) { hl_defer = true; return false; });   // lit_area's raise: k_hl_raise
-        lv_hl_defer(p, hl_defer, cur.ray, base + i, [&] { return level == 0 ? root : lv_ray_root(p, qs); });
-        const bool ext = alive && !fired;
-        if (active && !ext)                   // the ray ends here without a walk: its record
-          *reinterpret_cast<uint2*>(rec) = make_uint2((errA & 0xffu) | ((uint32_t)nleaf << 8), 0u);
-        if (ext) {
-          rf_has = true;
-          rf_started = false;
-          rf_o = cur.ray.o;
-          rf_d = cur.ray.d;
-          rf_i = i;
-          rf_slot = slot;
-          rf_errA = errA;
-          rf_errL = 0;
-          rf_best = S.max_distance;
-          rf_besti = -1;
-          rf_hit = v3(0.0, 0.0, 0.0);
-          rf_hin = true;
-        }
-      }
-      const bool exhausted = !got && rf_next >= 64u;   // wave-uniform: no ray left to take
-      bool done = false;
-      if (rf_has) {
-        done = lv_walk_ext_pp<SPH, BS>(p, lds, rf_o, rf_d, rf_best, rf_besti, rf_hit, rf_hin, rf_errL, rf_ref, rf_sp,
-                                       rf_started, exhausted || drain ? 0 : p.lv_refill);
-        rf_started = true;
-      }
-      const bool fin = rf_has && done;
-      const bool shade = fin && rf_besti >= 0;
-      if (fin && !shade) {                    // the ray ends here: its record
-        const uint32_t err = rf_errA ? rf_errA : rf_errL;
-        *reinterpret_cast<uint2*>(p.lv_rec + (size_t)(base + rf_i) * p.lv_rec_bytes) = make_uint2(err & 0xffu, 0u);
-      }
-      const uint64_t hm = __ballot(shade);
-      if (shade) {
-        const uint32_t k = (head + pend + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))) & (LV_RING - 1);
-        double* r = ring + k;
-        r[0 * LV_RING] = rf_hit.x;
-        r[1 * LV_RING] = rf_hit.y;
-        r[2 * LV_RING] = rf_hit.z;
-        if (RF == LV_RING_FIELDS) {
-          r[3 * LV_RING] = rf_o.x;
-          r[4 * LV_RING] = rf_o.y;
-          r[5 * LV_RING] = rf_o.z;
-          r[6 * LV_RING] = rf_d.x;
-          r[7 * LV_RING] = rf_d.y;
-          r[8 * LV_RING] = rf_d.z;
-        }
-        r[FI * LV_RING] = __builtin_bit_cast(double, (uint64_t)rf_i | (uint64_t)rf_slot << 32);
-        r[(FI + 1) * LV_RING] = __builtin_bit_cast(
-            double, (uint64_t)((uint32_t)rf_besti | (rf_hin ? 0x80000000u : 0u)) |
-                        (uint64_t)((rf_errA & 0xffu) | (rf_errL & 0xffu) << 8) << 32);
-      }
-      pend += (uint32_t)__popcll(hm);
-      rf_has = rf_has && !done;
-      const bool flush = exhausted && __ballot(rf_has) == 0;
-      if (pend >= 64 && !p.lv_refill_save && __ballot(rf_has) != 0) continue;   // finish the walks first
-      if (pend < 64 && !(flush && pend > 0)) {
-        if (flush) break;                     // no ray left, no walk running, nothing parked
-        continue;                             // not a full wave of hits yet
-      }
-      // the shading half below walks with this lane's LDS stack: save the suspended walks
-      rf_saved = __ballot(rf_has) != 0;
-      if (rf_saved && rf_has) {
-        double* v = rf_sv + lane;
-        v[0 * 64] = rf_o.x;
-        v[1 * 64] = rf_o.y;
-        v[2 * 64] = rf_o.z;
-        v[3 * 64] = rf_d.x;
-        v[4 * 64] = rf_d.y;
-        v[5 * 64] = rf_d.z;
-        v[6 * 64] = rf_best;
-        v[7 * 64] = rf_hit.x;
-        v[8 * 64] = rf_hit.y;
-        v[9 * 64] = rf_hit.z;
-        v[10 * 64] = __builtin_bit_cast(double, (uint64_t)rf_i | (uint64_t)rf_slot << 32);
-        v[11 * 64] = __builtin_bit_cast(double, (uint64_t)(uint32_t)rf_besti |
-                                                    (uint64_t)((rf_errA & 0xffu) | (rf_errL & 0xffu) << 8 |
-                                                               (rf_hin ? 0x10000u : 0u)) << 32);
-        v[12 * 64] = __builtin_bit_cast(double, (uint64_t)(uint32_t)rf_ref | (uint64_t)(uint32_t)rf_sp << 32);
-        int* st = reinterpret_cast<int*>(rf_sv + LV_SAVE_DBL * 64) + lane;
-        for (int e = 0; e < rf_sp; e++) st[e * 64] = lv_stack_get<SPH, BS>(p, lds, e);
       }
     }
     // ---- second half on up to 64 parked hits (64, except the final flush)
@@ -1204,35 +1001,6 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec, 0,
               errA, errS, errL, errP, m, LAST);
     RTX_LV_STAMP(5)
-    if constexpr (REFILL) {                   // the suspended walks back (every path assigns them)
-      if (rf_saved && rf_has) {
-        const double* v = rf_sv + lane;
-        rf_o = v3(v[0 * 64], v[1 * 64], v[2 * 64]);
-        rf_d = v3(v[3 * 64], v[4 * 64], v[5 * 64]);
-        rf_best = v[6 * 64];
-        rf_hit = v3(v[7 * 64], v[8 * 64], v[9 * 64]);
-        const uint64_t w10 = __builtin_bit_cast(uint64_t, v[10 * 64]), w11 = __builtin_bit_cast(uint64_t, v[11 * 64]),
-                       w12 = __builtin_bit_cast(uint64_t, v[12 * 64]);
-        rf_i = (uint32_t)w10;
-        rf_slot = (uint32_t)(w10 >> 32);
-        rf_besti = (int)(uint32_t)w11;
-        rf_errA = (uint32_t)(w11 >> 32) & 0xffu;
-        rf_errL = (uint32_t)(w11 >> 40) & 0xffu;
-        rf_hin = ((w11 >> 48) & 1u) != 0;
-        rf_ref = (int)(uint32_t)w12;
-        rf_sp = (int)(uint32_t)(w12 >> 32);
-        const int* st = reinterpret_cast<const int*>(rf_sv + LV_SAVE_DBL * 64) + lane;
-        for (int e = 0; e < rf_sp; e++) lv_stack_set<SPH, BS>(p, lds, e, st[e * 64]);
-      } else {
-        rf_o = rf_d = rf_hit = v3(0.0, 0.0, 0.0);
-        rf_best = 0.0;
-        rf_i = rf_slot = rf_errA = rf_errL = 0;
-        rf_besti = -1;
-        rf_hin = true;
-        rf_ref = BVH_NONE;
-        rf_sp = 0;
-      }
-    }
   }
 #undef RTX_LV_STAMP
   if (RTX_STAMPS && __lane_id() == 0) {
@@ -1249,9 +1017,9 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS, int RF, bool LAST, bool REFILL>
+template <int SPH, int BS, int RF, bool LAST>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
-  k_level_c_body<SPH, BS, RF, LAST, REFILL>(p, level);
+  k_level_c_body<SPH, BS, RF, LAST>(p, level);
   lv_level_done(p, level + 1);
 }
 
@@ -1668,191 +1436,6 @@ __global__ __launch_bounds__(256) void k_tree_finalize(KParams p, int nlev) {
   }
 }
 
-// The same reduction with the tile's trees gathered into LDS first (option
-// lv_fin_cap > 0).  k_tree_finalize's walks are chains of dependent global
-// loads, one per visited record (the next record is known only once the
-// current one has arrived), and a wave runs as many steps as its largest
-// tree: the kernel spent ~80 % of its wave time waiting (r03k).  Here the
-// block copies its 64 x pre trees into LDS level by level: level 0 is the
-// tile's items, and level d + 1 is the children of level d, placed by a block
-// prefix count over the parents in LDS order (so a parent's children stay
-// contiguous and in slot order, as in the level queues) and loaded by the
-// parent's thread; every load of a level is in flight at once, so the
-// block waits nlev round trips in all.  Then each thread walks its trees in
-// LDS exactly as lv_tree_sum does (pre-order, children in reverse slot order,
-// the same additions in the same order: the same bits).  A tile whose trees
-// do not fit `cap` records falls back to the global walk (lv_tree_sum).
-//
-// Dynamic LDS: nlev * 64 slice offsets | 64 * pre colours (24 B) + raises
-// (4 B) | SD * 256 walk-stack words | cap first-child indices (u16) | cap
-// records (lv_rec_bytes each; the fallback's walk stacks alias them).
-__host__ __device__ __forceinline__ size_t lv_fin_g_rec_off(int nlev, int pre, int sd, int cap) {
-  const size_t o = (size_t)nlev * 64 * 4;
-  return (((o + 7) & ~(size_t)7) + (size_t)64 * pre * 28 + (size_t)sd * 256 * 4 + (size_t)cap * 2 + 15) &
-         ~(size_t)15;
-}
-
-// lv_tree_sum over the tree copied into LDS (record `root` of level 0).  The
-// pending child ranges (lo | hi << 16) are LDS words stk[k * 256], k < SD
-// (a register array indexed by the stack depth would live in scratch).
-template <int SD>
-__device__ __forceinline__ V3 lv_tree_sum_lds(const char* recs, const uint16_t* kid, uint32_t* stk, int rb, int root,
-                                              int nlev, uint32_t& err_out) {
-  int sp = 0;
-  V3 sum = v3(0.0, 0.0, 0.0);
-  uint32_t err = 0;
-  bool gt1 = false;
-  int lev = 0;
-  uint32_t q = (uint32_t)root;
-  while (true) {
-    const char* rec = recs + (size_t)q * rb;
-    const uint32_t hx = *reinterpret_cast<const uint32_t*>(rec);
-    const double* lf = reinterpret_cast<const double*>(rec + 8);
-    if (!err) err = hx & 0xffu;
-    const int nleaf = (int)(hx >> 8 & 0xffu);
-    for (int k = 0; k < nleaf; k++) {         // rt_reduce (ray_tracer.rb:292-298), in emission order
-      sum = vadd(sum, v3(lf[3 * k], lf[3 * k + 1], lf[3 * k + 2]));
-      if (!(sum.x <= 1 && sum.y <= 1 && sum.z <= 1)) gt1 = true;
-    }
-    const uint32_t nch = (uint32_t)__popc(hx >> 16);
-    if (nch && lev + 1 < nlev && sp < SD) {
-      const uint32_t c0 = kid[q];
-      stk[sp * 256] = c0 | (c0 + nch) << 16;
-      sp++;
-    }
-    // next: the last unvisited child of the deepest pending range (LIFO pop)
-    uint32_t e = 0;
-    while (sp > 0) {
-      e = stk[(sp - 1) * 256];
-      if ((e & 0xffffu) != e >> 16) break;
-      sp--;
-    }
-    if (sp == 0) break;
-    e -= 1u << 16;
-    stk[(sp - 1) * 256] = e;
-    q = e >> 16;
-    lev = sp;
-  }
-  err_out = err ? err : (gt1 ? (uint32_t)ERR_COLOR_GT1 : 0u);
-  return sum;
-}
-
-template <int SD>
-__global__ __launch_bounds__(256) void k_tree_finalize_g(KParams p, int nlev) {
-  __shared__ uint32_t base[LV_MAXL + 1];
-  __shared__ uint32_t wpart[4];
-  extern __shared__ uint32_t lds_fin[];
-  uint32_t* pex = lds_fin;
-  const unsigned long long ts0 = RTX_STAMPS ? stamp() : 0ull;   // RTX_STAMPS diagnostic build only
-  lv_layout(p, nlev, base, pex);
-  const unsigned long long ts1 = RTX_STAMPS ? stamp() : 0ull;
-  const int pre = p.pre, cap = p.lv_fin_cap, rb = p.lv_rec_bytes;
-  const int n_items = 64 * pre;
-  const int item0 = blockIdx.x * n_items;
-  const int tid = (int)threadIdx.x, wave = tid >> 6, lane = (int)__lane_id();
-  char* lb = reinterpret_cast<char*>(lds_fin);
-  double* scol = reinterpret_cast<double*>(lb + (((size_t)nlev * 64 * 4 + 7) & ~(size_t)7));
-  uint32_t* serr = reinterpret_cast<uint32_t*>(scol + 64 * pre * 3);
-  uint32_t* stk = serr + n_items + tid;
-  uint16_t* kid = reinterpret_cast<uint16_t*>(serr + n_items + SD * 256);
-  char* recs = lb + lv_fin_g_rec_off(nlev, pre, SD, cap);
-  const int nq = rb >> 4;                      // 16-B words per record
-  const uint32_t log2cap = (uint32_t)p.lv_slice_log2, smask = (1u << log2cap) - 1u;
-  bool fits = n_items <= cap;
-  // ---- level 0: the tile's items (padding and re-rendered samples: no tree)
-  if (fits) {
-    for (int it = tid; it < n_items; it += 256) {
-      const int item = item0 + it;
-      uint4* dst = reinterpret_cast<uint4*>(recs + (size_t)it * rb);
-      if (decode_item(p, item).valid && p.lv_redo_of[item] < 0) {
-        const uint4* src = reinterpret_cast<const uint4*>(p.lv_rec + (size_t)(base[0] + item) * rb);
-        for (int w = 0; w < nq; w++) dst[w] = src[w];
-      } else {
-        dst[0] = make_uint4(0u, 0u, 0u, 0u);   // no leaves, no children
-      }
-    }
-  }
-  __syncthreads();
-  // ---- level d + 1: the children of level d's records [lo, hi)
-  int lo = 0, hi = n_items;
-  for (int d = 0; fits && d + 1 < nlev; d++) {
-    const int n = hi - lo;
-    const int m = (n + 255) >> 8;              // parents per thread, a contiguous run
-    const int a = lo + tid * m, b = min(a + m, hi);
-    uint32_t cnt = 0;
-    for (int k = a; k < b; k++) cnt += (uint32_t)__popc(*reinterpret_cast<const uint32_t*>(recs + (size_t)k * rb) >> 16);
-    const uint32_t incl = wave_scan_incl(cnt);
-    if (lane == 63) wpart[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      const uint32_t v = wpart[w];
-      before += w < wave ? v : 0u;
-      total += v;
-    }
-    __syncthreads();                           // wpart is reused by the next level
-    if (total == 0) break;
-    if (hi + (int)total > cap) {               // uniform: the tile's trees do not fit
-      fits = false;
-      break;
-    }
-    uint32_t pos = (uint32_t)hi + before + incl - cnt;
-    for (int k = a; k < b; k++) {
-      const uint2 hdr = *reinterpret_cast<const uint2*>(recs + (size_t)k * rb);
-      const uint32_t nch = (uint32_t)__popc(hdr.x >> 16);
-      kid[k] = (uint16_t)pos;
-      if (!nch) continue;
-      // the children's slot -> their dense index at level d + 1 (as lv_tree_sum)
-      const uint32_t c0 = pex[(d + 1) * 64 + (hdr.y >> log2cap)] + (hdr.y & smask);
-      const uint4* src = reinterpret_cast<const uint4*>(p.lv_rec + (size_t)(base[d + 1] + c0) * rb);
-      uint4* dst = reinterpret_cast<uint4*>(recs + (size_t)pos * rb);
-      for (uint32_t w = 0; w < nch * (uint32_t)nq; w++) dst[w] = src[w];
-      pos += nch;
-    }
-    __syncthreads();
-    lo = hi;
-    hi += (int)total;
-  }
-  const unsigned long long tsg = RTX_STAMPS ? stamp() : 0ull;
-  // ---- the sums, in trace_sync's order
-  uint32_t* slo = reinterpret_cast<uint32_t*>(recs) + tid;   // fallback walk stacks (alias the records)
-  uint32_t* shi = slo + SD * 256;
-  if (!fits) __syncthreads();                  // every thread is past its last read of the records
-  for (int it = tid; it < n_items; it += 256) {
-    const int item = item0 + it;
-    if (!decode_item(p, item).valid) continue;
-    uint32_t e = 0;
-    V3 c;
-    const int r = p.lv_redo_of[item];
-    if (r >= 0) {
-      const double* q = p.lv_redo_smp + (size_t)r * 4;
-      e = (uint32_t)__builtin_bit_cast(uint64_t, q[3]);
-      c = v3(q[0], q[1], q[2]);
-    } else if (fits) {
-      c = lv_tree_sum_lds<SD>(recs, kid, stk, rb, it, nlev, e);
-    } else {
-      uint32_t nv = 0;
-      c = lv_tree_sum(p, base, pex, item, nlev, slo, shi, 256, SD, e, nv);
-    }
-    scol[3 * it] = c.x;
-    scol[3 * it + 1] = c.y;
-    scol[3 * it + 2] = c.z;
-    serr[it] = e;
-  }
-  if (RTX_STAMPS) {                           // layout / gather + walks, waves; gather part in [14]
-    const unsigned long long ts2 = stamp();
-    if (__lane_id() == 0) {
-      atomicAdd(&rtx_stamps[11], ts1 - ts0);
-      atomicAdd(&rtx_stamps[12], ts2 - ts1);
-      atomicAdd(&rtx_stamps[13], 1ull);
-      atomicAdd(&rtx_stamps[14], tsg - ts1);
-    }
-  }
-  __syncthreads();
-  lv_tile_pixels(p, scol, serr, blockIdx.x);
-}
-
 // Pass 1: one thread per extra-list entry of the batch: (pre mean * pre +
 // the extra samples in order) / max_sample_times.
 template <int SD>
@@ -2126,15 +1709,17 @@ static hipError_t launch_timed(K kern, long blocks, int bs, size_t lds, hipStrea
   return e;
 }
 
-// k_level_c for a level: the batch's last level compiled apart; with refill
-// (option lv_refill) for the sphere modes it is compiled for (C2's and C4's).
+// k_level_c for a level: the batch's last level compiled apart.
 template <int SPH, int BS, int RF>
-static void (*level_c_kernel(bool last, bool refill))(KParams, int) {
-  if constexpr (SPH == SPH_BVH_LDSX || SPH == SPH_BVH_QLDS) {
-    if (refill) return last ? k_level_c<SPH, BS, RF, true, true> : k_level_c<SPH, BS, RF, false, true>;
-  }
-  return last ? k_level_c<SPH, BS, RF, true, false> : k_level_c<SPH, BS, RF, false, false>;
+static void (*level_c_kernel(bool last))(KParams, int) {
+  return last ? k_level_c<SPH, BS, RF, true> : k_level_c<SPH, BS, RF, false>;
 }
+
+#ifndef RTX_LV_FUSED_BS
+#define RTX_LV_FUSED_BS 0                  // k_level's block size (0: BS_LIN / BS_BVH)
+#endif
+template <int SPH>
+constexpr int fused_bs() { return RTX_LV_FUSED_BS ? RTX_LV_FUSED_BS : (sph_is_bvh(SPH) ? BS_BVH : BS_LIN); }
 
 // kind: 0 k_level (fused), 1 k_lv_trace, 2 k_lv_shadow.  Persistent: as many
 // workgroups as fit at once, never more than cap_items need.
@@ -2145,9 +1730,9 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   q.stk_slots_max = 0;                         // no ray stack in this engine
   size_t lds = lds_layout(q, SPH, BS);
   auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
-  bool refill = (SPH == SPH_BVH_LDSX || SPH == SPH_BVH_QLDS) && kind == 0 && q.lv_compact != 0 && q.lv_refill > 0 &&
-                (!q.lv_refill_save || (q.lv_save && q.lv_save_waves >= BS / 64));
-  if (kind == 0 && q.lv_compact != 0) {        // hit compaction when the rings fit next to the walk's LDS
+  // hit compaction when the rings fit next to the walk's LDS (k_level_c is
+  // instantiated for the fused kernel's block size only)
+  if constexpr (BS == fused_bs<SPH>()) if (kind == 0 && q.lv_compact != 0) {
     constexpr bool BVH = sph_is_bvh(SPH);
     const size_t ring = (lds + 15) & ~(size_t)15, budget = BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
     const size_t need = ring + (size_t)(BS / 64) * LV_RING_WAVE_BYTES;
@@ -2155,35 +1740,28 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
     if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level, refill);
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level);
     } else if (BVH && need_small <= budget) {  // the compact ring (C4-sized hierarchies)
       q.lds_ring = (int32_t)ring;
       lds = need_small;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, refill);
-    } else {
-      refill = false;
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level);
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)
   const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(kern), BS, lds, cus, per_cu);
   if (e != hipSuccess) return e;
-  long grid = std::max<long>(1, (long)cus * per_cu / std::max(1, q.lv_grid_div));
-  if (refill && q.lv_refill_save)                // one save area per wave
-    grid = std::min<long>(grid, std::max(1, q.lv_save_waves / (BS / 64)));
+  const long grid = std::max<long>(1, (long)cus * per_cu / std::max(1, q.lv_grid_div));
   return launch_timed(kern, std::min<long>((cap_items + BS - 1) / BS, grid), BS, lds, s, kev, q, level);
 }
 
 // The fused kernel runs the engine's block sizes (BS_LIN / BS_BVH, 2 waves per
 // SIMD).  The split walk kernels (3 waves per SIMD) take 256-thread blocks
 // when three of them fit a CU's LDS, else the hierarchy's 512.
-#ifndef RTX_LV_FUSED_BS
-#define RTX_LV_FUSED_BS 0                  // k_level's block size (0: BS_LIN / BS_BVH)
-#endif
 template <int SPH>
 static hipError_t launch_level(const KParams& p, int kind, int level, long cap_items, hipStream_t s,
                                KernelEvents* kev) {
   constexpr bool BVH = sph_is_bvh(SPH);
-  constexpr int FBS = RTX_LV_FUSED_BS ? RTX_LV_FUSED_BS : (BVH ? BS_BVH : BS_LIN);
+  constexpr int FBS = fused_bs<SPH>();
   if (kind == 0) return launch_level_bs<SPH, FBS>(p, kind, level, cap_items, s, kev);
   if (BVH) {
     KParams q = p;
@@ -2237,34 +1815,7 @@ static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStrea
   return hipGetLastError();
 }
 
-// Pass 0 with the trees gathered into LDS (lv_fin_cap > 0; register walk
-// stacks of SD entries, nlev - 1 <= SD).
-template <int SD>
-static hipError_t launch_finalize_g(KParams q, int nlev, int n, hipStream_t s) {
-  // at most as many records as fit a CU's LDS next to the rest
-  // (the kernel's static LDS, and 16 B for the alignment of the record area)
-  hipFuncAttributes fa{};
-  size_t stat = 16 * 1024;
-  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_tree_finalize_g<SD>)) == hipSuccess)
-    stat = fa.sharedSizeBytes;
-  const size_t fixed = lv_fin_g_rec_off(nlev, q.pre, SD, 0) + stat + 16;
-  const long fit = fixed < LDS_TOTAL_BYTES ? (long)((LDS_TOTAL_BYTES - fixed) / (q.lv_rec_bytes + 2)) : 0;
-  q.lv_fin_cap = (int32_t)std::min<long>(q.lv_fin_cap, fit);
-  const size_t recs = (size_t)q.lv_fin_cap * q.lv_rec_bytes;
-  const size_t lds = lv_fin_g_rec_off(nlev, q.pre, SD, q.lv_fin_cap) + std::max(recs, (size_t)SD * 2 * 256 * 4);
-  if (lds + stat > LDS_TOTAL_BYTES) return launch_finalize_sd<16>(q, nlev, n, s);   // (pre too large: the walk)
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tree_finalize_g<SD>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_tree_finalize_g<SD>, dim3((unsigned)n), dim3(256), lds, s, q, nlev);
-  return hipGetLastError();
-}
-
 static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t s) {
-  if (q.lv_pass == 0 && q.lv_fin_cap > 0) {
-    if (nlev <= 5) return launch_finalize_g<4>(q, nlev, n, s);
-    if (nlev <= 9) return launch_finalize_g<8>(q, nlev, n, s);
-  }
   // a walk keeps one pending child range per level below the root: nlev - 1
   // entries; the smaller stack lets 8 blocks share a CU (C2, depth 5) instead of 6
   if (nlev <= 5) return launch_finalize_sd<4>(q, nlev, n, s);

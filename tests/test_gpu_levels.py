@@ -277,38 +277,6 @@ def test_compaction_batches_overflow_schedule(gpu, opts):
             assert r.level_stats()["redo"] > 0
 
 
-# ---- refill (option lv_refill: lanes whose nearest-hit walk ended take new rays, walks saved across shading)
-@pytest.mark.parametrize("world,camera,ov", SCENES_SMALL)
-def test_refill_bit_identical(gpu, world, camera, ov):
-    sd, cd = _scene(world, camera, **ov)
-    lanes = _renderer(sd, cd, 0).render(seed=6)
-    for refill, save in ((1, 0), (16, 0), (40, 0), (64, 0), (16, 1), (64, 1)):
-        for compact in (1, 2):
-            r = _renderer(sd, cd, 1, lv_compact=compact, lv_refill=refill, lv_refill_save=save)
-            assert _same(r.render(seed=6), lanes), (refill, save, compact)
-            st = r.level_stats()
-            assert st["redo"] == 0 and st["dropped"] == 0
-
-
-def test_refill_c4_and_overflow(gpu):
-    """C4 (16-bit leaf records, compact ring) and C2 with the record arena and
-    queue slices overflowing into the re-render, under refill; same bits."""
-    import sys
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    import make_scenes
-    make_scenes.ensure_c4()
-    sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=64, height=36)
-    lanes = _renderer(sd, cd, 0).render(seed=2)
-    for refill, save in ((8, 0), (32, 0), (32, 1)):
-        assert _same(_renderer(sd, cd, 1, lv_refill=refill, lv_refill_save=save).render(seed=2), lanes), refill
-    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
-    lanes = _renderer(sd, cd, 0).render(seed=5)
-    for opts in (dict(lv_stage_pct=5, lv_floor=0), dict(lv_rec_pct=101, lv_floor=0), dict(lv_batch=512)):
-        for save in (0, 1):
-            r = _renderer(sd, cd, 1, lv_refill=24, lv_refill_save=save, **opts)
-            assert _same(r.render(seed=5), lanes), (opts, save)
-
-
 def test_compaction_errors_and_c4_fallback(gpu, tmp_path):
     """Raise sites keep their order through the ring (full and compact); C4's
     staged hierarchy leaves no LDS for a ring: with sphere_src 0 the option
@@ -459,34 +427,31 @@ def test_two_streams_c2_full_frame_and_kernel_time(gpu):
     assert launches == 10 and 0.5 < ms < 50.0, (ms, launches)   # union of the two halves' level launches
 
 
-# ---- tree reduction with the tile's trees gathered into LDS (option lv_fin_cap)
+# ---- tree reduction (k_tree_finalize): deep trees, path tracing, extra samples, overflow
 @pytest.mark.parametrize("world,camera,ov", [
     ("c2_world.yml", "c2_camera.yml", dict(width=120, height=70)),
     ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, monte_carlo_diffusion_times=3, trace_depth=6)),
     ("mix_world.yml", "mix_camera.yml", dict(width=40, height=22, pre_sample_times=2, max_sample_times=5,
                                              variant_threshold=0.0)),
 ])
-def test_gathered_reduction_changes_no_bit(gpu, world, camera, ov):
-    """lv_fin_cap: LDS gather (default), a cap that makes some tiles fall back
-    to the global walk, one below a tile's level 0 (every tile falls back), and
-    the global walk alone (0) render the same bits as the lanes engine."""
+def test_reduction_changes_no_bit(gpu, world, camera, ov):
+    """The tree reduction renders the lanes engine's bits (one and two parts)."""
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=4)
-    for cap in (1024, 4096, 300, 100, 0):
-        r = _renderer(sd, cd, 1, lv_fin_cap=cap)
-        assert _same(r.render(seed=4), lanes), cap
+    for parts in (1, 2):
+        r = _renderer(sd, cd, 1, lv_streams=parts)
+        assert _same(r.render(seed=4), lanes), parts
         r.close()
 
 
-def test_gathered_reduction_with_overflow(gpu):
-    """Re-rendered samples (their trees are not followed) inside gathered tiles."""
+def test_reduction_with_overflow(gpu):
+    """Re-rendered samples (their trees are not followed) inside reduced tiles."""
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
     lanes = _renderer(sd, cd, 0).render(seed=6)
-    for cap in (1024, 300):
-        r = _renderer(sd, cd, 1, lv_fin_cap=cap, lv_stage_pct=5, lv_floor=0)
-        assert _same(r.render(seed=6), lanes), cap
-        assert r.level_stats()["redo"] > 0
-        r.close()
+    r = _renderer(sd, cd, 1, lv_stage_pct=5, lv_floor=0)
+    assert _same(r.render(seed=6), lanes)
+    assert r.level_stats()["redo"] > 0
+    r.close()
 
 
 # ---- raises of children the cutoff drops (lv_finish builds only their normalize tests)
@@ -721,7 +686,7 @@ def test_grid_stride_reduction_changes_no_bit(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=4)
     for k in (1, 4):
-        for opts in (dict(), dict(lv_fin_cap=0), dict(lv_stage_pct=5, lv_floor=0)):
+        for opts in (dict(), dict(lv_stage_pct=5, lv_floor=0)):
             r = _renderer(sd, cd, 1, lv_fin_grid=k, lv_streams=1, **opts)
             assert _same(r.render(seed=4), lanes), (k, opts)
             r.close()

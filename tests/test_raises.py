@@ -218,8 +218,7 @@ def test_oracle_raises_on_local_lights_factor0_cover(oracle_lib, tmp_path, case)
 ENGINES = [(0, {}), (1, {}), (1, dict(lv_split=1)), (1, dict(lv_compact=0)), (1, dict(lv_compact=2)),
            (0, dict(bvh=2)), (1, dict(bvh=2)), (1, dict(bvh=2, sphere_src=2)), (1, dict(bvh=2, sphere_src=4)),
            (1, dict(bvh=0)), (1, dict(bvh=2, sphere_src=4, lv_split=1)),
-           (1, dict(lv_hl_cap=1)), (1, dict(lv_hl_cap=1, lv_split=1)), (1, dict(lv_refill=32)),
-           (1, dict(bvh=2, sphere_src=4, lv_refill=16))]   # deferred-check list overflow: re-render
+           (1, dict(lv_hl_cap=1)), (1, dict(lv_hl_cap=1, lv_split=1))]   # deferred-check list overflow: re-render
 
 
 def _renderer(sd, cd, engine, **opts):
