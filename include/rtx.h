@@ -335,8 +335,10 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          = 80 whenever (monte_carlo_diffusion_times + 3)^trace_depth <= 2^32, else 96; 80 for a camera whose paths
          do not fit fails the render with RTX_EINVAL; same bits), "exact_raises" (1: every shadow walk of
          local_lights also checks the Math.acos raise of the covers it skips, spheres whose binary cover factor is 0
-         (sphere.rb:45-46), so the reference's raise is reported wherever it happens; 0 [default]:
-         only the covers the walk evaluates; World#high_lights' lit_area is checked either way; same colours),
+         (sphere.rb:45-46), so the reference's raise is reported wherever it happens: the check
+         is part of the shadow walk (a kernel variant), which then also visits the boxes the light's cone meets;
+         0 [default]: only the covers the walk evaluates; World#high_lights' lit_area is checked either way; same
+         colours),
          "lv_hl_cap" (bounce levels: entries of the batch's list of highlight rays whose lit_area raise is checked
          after the levels (k_hl_raise); 0 [default] = 1/256 of the tree-record capacity, at least 4096; a ray that
          finds it full has its sample re-rendered by the lanes engine; same bits). */

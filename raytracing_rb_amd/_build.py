@@ -12,7 +12,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "librtx.so")
 SOURCES = [os.path.join(CSRC, f) for f in ("rtx_kernels.hip", "rtx_levels.hip", "rtx_capi.cpp")]
-HEADERS = [os.path.join(CSRC, f) for f in ("rtx_scene.h", "rtx_vec3.h", "rtx_launch.h", "rtx_device.h")] + [
+HEADERS = [os.path.join(CSRC, f) for f in ("rtx_scene.h", "rtx_vec3.h", "rtx_launch.h", "rtx_device.h", "rtx_bvh_build.h")] + [
     os.path.join(ROOT, "include", "rtx.h")]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -90,7 +90,8 @@ struct rtx_context {
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   int64_t opt_lv_ray_bytes = 0;      // bounce levels: staged ray record, 0 auto (80 B when every path fits 32 bits), 80, 96
   int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
-  int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also run the raise walk of the covers they skip
+  int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also check the acos raises of the covers they skip
+                                     // (C2 +10 %, C4 +108 %, r09c; so not the default)
   int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
@@ -138,197 +139,7 @@ static void free_scene(rtx_context* c) {
   c->have_scene = false;
 }
 
-// ------------------------------------------------------------------ BVH build
-// Four-wide hierarchy: each node splits its spheres in two (binned SAH near
-// the root, median of the longest centroid axis below), then splits each half
-// again (up to four children);
-// groups of <= BVH_LEAF spheres become leaves.  Child boxes are float32 and
-// contain every member sphere exactly (bounds rounded outwards); see
-// DESIGN.md §2.1 and rtx_scene.h.
-namespace {
-struct BSph {
-  double c[3];
-  double r;
-  int rec;
-};
-
-static float f32_down(double x) {           // largest float <= x
-  float f = (float)x;
-  if ((double)f > x) f = nextafterf(f, -INFINITY);
-  return f;
-}
-static float f32_up(double x) {             // smallest float >= x
-  float f = (float)x;
-  if ((double)f < x) f = nextafterf(f, INFINITY);
-  return f;
-}
-
-struct Bvh4Builder {
-  std::vector<BSph>& sp;
-  const std::vector<Sphere64>& sph64;
-  const std::vector<float>& sph32;
-  const std::vector<int32_t>& sph_obj;
-  std::vector<Bvh4Node> nodes;
-  std::vector<float> slot32;
-  std::vector<Sphere64> slot64;
-  std::vector<int32_t> slot_obj;
-  int stack = 0;                              // worst-case traversal stack (3 pushes per internal level)
-
-  // float32 box containing every sphere of sp[lo, hi); the double bounds are
-  // widened by a relative 1e-12 to cover their own rounding.
-  void box(int lo, int hi, float blo[3], float bhi[3]) {
-    for (int a = 0; a < 3; a++) {
-      double mn = INFINITY, mx = -INFINITY;
-      for (int i = lo; i < hi; i++) {
-        const double r = fabs(sp[i].r);
-        mn = fmin(mn, sp[i].c[a] - r);
-        mx = fmax(mx, sp[i].c[a] + r);
-      }
-      blo[a] = f32_down(mn - 1e-12 * fabs(mn) - 1e-300);
-      bhi[a] = f32_up(mx + 1e-12 * fabs(mx) + 1e-300);
-    }
-  }
-
-  // Split sp[lo, hi) in two.  Binned surface-area heuristic (16 centroid bins
-  // per axis, cost = area(left) * n_left + area(right) * n_right over the
-  // spheres' boxes) while the traversal stack above stays shallow; otherwise,
-  // or when no bin boundary separates the centroids, the median of the longest
-  // centroid axis.  Deterministic: stable partitions, first-best bin wins.
-  bool sah = true;
-  int split(int lo, int hi, int pushes = 0) {
-    double cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = lo; i < hi; i++)
-      for (int a = 0; a < 3; a++) {
-        cmn[a] = fmin(cmn[a], sp[i].c[a]);
-        cmx[a] = fmax(cmx[a], sp[i].c[a]);
-      }
-    if (sah && pushes <= RTX_SAH_PUSHES) {
-      constexpr int NB = 16;
-      auto bin_of = [&](double x, int a) {
-        int b = (int)((x - cmn[a]) / (cmx[a] - cmn[a]) * NB);
-        return b < 0 ? 0 : (b >= NB ? NB - 1 : b);
-      };
-      auto area = [](const double* mn, const double* mx) {
-        const double dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
-        return dx * dy + dy * dz + dz * dx;
-      };
-      double best = INFINITY;
-      int best_axis = -1, best_bin = -1;
-      for (int a = 0; a < 3; a++) {
-        if (!(cmx[a] - cmn[a] > 0)) continue;
-        double bmn[NB][3], bmx[NB][3];
-        int cnt[NB] = {0};
-        for (int b = 0; b < NB; b++)
-          for (int k = 0; k < 3; k++) {
-            bmn[b][k] = INFINITY;
-            bmx[b][k] = -INFINITY;
-          }
-        for (int i = lo; i < hi; i++) {
-          const int b = bin_of(sp[i].c[a], a);
-          const double r = fabs(sp[i].r);
-          cnt[b]++;
-          for (int k = 0; k < 3; k++) {
-            bmn[b][k] = fmin(bmn[b][k], sp[i].c[k] - r);
-            bmx[b][k] = fmax(bmx[b][k], sp[i].c[k] + r);
-          }
-        }
-        double rmn[NB][3], rmx[NB][3];                  // suffix boxes over bins b..NB-1
-        int rcnt[NB];
-        double amn[3] = {INFINITY, INFINITY, INFINITY}, amx[3] = {-INFINITY, -INFINITY, -INFINITY};
-        int acc = 0;
-        for (int b = NB - 1; b >= 0; b--) {
-          for (int k = 0; k < 3; k++) {
-            rmn[b][k] = amn[k] = fmin(amn[k], bmn[b][k]);
-            rmx[b][k] = amx[k] = fmax(amx[k], bmx[b][k]);
-          }
-          rcnt[b] = acc += cnt[b];
-        }
-        double lmn[3] = {INFINITY, INFINITY, INFINITY}, lmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-        int lc = 0;
-        for (int b = 0; b + 1 < NB; b++) {              // left = bins 0..b, right = bins b+1..
-          for (int k = 0; k < 3; k++) {
-            lmn[k] = fmin(lmn[k], bmn[b][k]);
-            lmx[k] = fmax(lmx[k], bmx[b][k]);
-          }
-          lc += cnt[b];
-          if (lc == 0 || rcnt[b + 1] == 0) continue;
-          const double cost = area(lmn, lmx) * lc + area(rmn[b + 1], rmx[b + 1]) * rcnt[b + 1];
-          if (cost < best) {
-            best = cost;
-            best_axis = a;
-            best_bin = b;
-          }
-        }
-      }
-      if (best_axis >= 0) {
-        const int a = best_axis;
-        auto it = std::stable_partition(sp.begin() + lo, sp.begin() + hi,
-                                        [&](const BSph& q) { return bin_of(q.c[a], a) <= best_bin; });
-        const int mid = (int)(it - sp.begin());
-        if (mid > lo && mid < hi) return mid;
-      }
-    }
-    int axis = 0;
-    for (int a = 1; a < 3; a++)
-      if (cmx[a] - cmn[a] > cmx[axis] - cmn[axis]) axis = a;
-    const int mid = (lo + hi) / 2;
-    std::nth_element(sp.begin() + lo, sp.begin() + mid, sp.begin() + hi, [axis](const BSph& a, const BSph& b) {
-      return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.rec < b.rec);
-    });
-    return mid;
-  }
-
-  int32_t leaf(int lo, int hi) {
-    const int id = (int)(slot_obj.size() / BVH_LEAF);
-    float soa[4][BVH_LEAF];                      // a leaf's float32 records component-major:
-    for (int u = 0; u < BVH_LEAF; u++) {         // {x0..x3}, {y0..y3}, {z0..z3}, {R^2 0..3}
-      const int rec = lo + u < hi ? sp[lo + u].rec : -1;
-      slot_obj.push_back(rec >= 0 ? sph_obj[rec] : -1);
-      slot64.push_back(rec >= 0 ? sph64[rec] : Sphere64{{0.0, 0.0, 0.0}, -1.0});
-      for (int k = 0; k < 4; k++) soa[k][u] = rec >= 0 ? sph32[4 * rec + k] : 0.0f;
-    }
-    for (int k = 0; k < 4; k++)
-      for (int u = 0; u < BVH_LEAF; u++) slot32.push_back(soa[k][u]);
-    return ~(int32_t)((id << 2) | (hi - lo - 1));
-  }
-
-  // Reference to the subtree over sp[lo, hi); `pushes` = stack entries above it.
-  int32_t build(int lo, int hi, int pushes) {
-    if (hi - lo <= BVH_LEAF) return leaf(lo, hi);
-    const int me = (int)nodes.size();
-    nodes.push_back(Bvh4Node{});
-    int g[5], ng = 0;
-    const int mid = split(lo, hi, pushes);
-    for (int h = 0; h < 2; h++) {
-      const int a = h ? mid : lo, b = h ? hi : mid;
-      g[ng++] = a;
-      if (b - a > BVH_LEAF) g[ng++] = split(a, b, pushes);
-    }
-    g[ng] = hi;
-    Bvh4Node n;
-    for (int k = 0; k < 4; k++) {               // empty slot: a point far outside every scene,
-      n.child[k] = BVH_NONE;                     // which no finite ray's slab test accepts
-      for (int a = 0; a < 3; a++) {
-        n.lh[a][k][0] = 3e38f;
-        n.lh[a][k][1] = 3e38f;
-      }
-    }
-    const int below = pushes + ng - 1;          // visiting one child leaves <= ng-1 siblings pushed
-    if (below > stack) stack = below;
-    for (int k = 0; k < ng; k++) {
-      float blo[3], bhi[3];
-      box(g[k], g[k + 1], blo, bhi);
-      for (int a = 0; a < 3; a++) {
-        n.lh[a][k][0] = blo[a];
-        n.lh[a][k][1] = bhi[a];
-      }
-      n.child[k] = build(g[k], g[k + 1], below);
-    }
-    nodes[me] = n;
-    return me;
-  }
-};
-}  // namespace
+#include "rtx_bvh_build.h"
 
 extern "C" {
 
@@ -600,70 +411,6 @@ static void put_plane(std::vector<double>& g, V3 P, V3 F, V3 U, double uu, doubl
   g.push_back(vu);
 }
 
-// 16-bit pre-test records of the hierarchy's leaves (SPH_BVH_QLDS, DESIGN.md
-// §3.15): per leaf 8 words, {x 0..3}, {y 0..3}, {z 0..3}, {r 0..3} as 16-bit
-// pairs (slot u in the low half of word 2k for u = 0, 2).  The device decodes
-// center axis a as fmaf(q, step[a], org[a]) and the radius as q * rstep, in
-// float32, the operations repeated here: a decoded center lies e from the true
-// one (exact, in binary64) and the decoded radius is at least R + e, so the
-// decoded ball holds the true one and the §2.1 pre-test stays conservative;
-// its "wholly behind" half also needs e below half its margin (m S).
-struct QuantLeaves {
-  std::vector<uint32_t> rec;
-  float org[3] = {0.0f, 0.0f, 0.0f}, step[3] = {1.0f, 1.0f, 1.0f}, rstep = 1.0f;
-  bool ok = false;
-  double max_err = 0.0;
-};
-
-static QuantLeaves quantize_leaves(const Bvh4Builder& bb, float sph_scale) {
-  QuantLeaves ql;
-  const size_t n_slots = bb.slot64.size();
-  ql.rec.assign(n_slots * 2, 0u);
-  double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-  for (const Sphere64& s : bb.slot64) {
-    if (!(s.r >= 0.0)) continue;                  // padding slot
-    for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], s.c[a]), hi[a] = std::max(hi[a], s.c[a]);
-  }
-  if (!(lo[0] <= hi[0])) return ql;               // no spheres
-  for (int a = 0; a < 3; a++) {
-    ql.org[a] = (float)lo[a];
-    const float st = (float)((hi[a] - lo[a]) / 65535.0 * (1.0 + 1e-6));
-    ql.step[a] = st > 0.0f ? st : 1.0f;
-  }
-  std::vector<double> grown(n_slots, 0.0);        // R + e per slot
-  double max_r = 0.0;
-  for (size_t k = 0; k < n_slots; k++) {
-    const Sphere64& s = bb.slot64[k];
-    if (!(s.r >= 0.0)) continue;
-    double e2 = 0.0;
-    for (int a = 0; a < 3; a++) {
-      double qd = std::nearbyint((s.c[a] - (double)ql.org[a]) / (double)ql.step[a]);
-      qd = std::min(65535.0, std::max(0.0, qd));
-      const uint32_t qv = (uint32_t)qd;
-      const double dec = (double)std::fmaf((float)qv, ql.step[a], ql.org[a]);
-      e2 += (dec - s.c[a]) * (dec - s.c[a]);
-      const size_t w = (k / BVH_LEAF) * 8 + (size_t)a * 2 + (k % BVH_LEAF) / 2;
-      ql.rec[w] |= qv << (16 * (k % 2));
-    }
-    const double e = std::sqrt(e2) * (1.0 + 1e-9);
-    ql.max_err = std::max(ql.max_err, e);
-    grown[k] = (s.r + e) * (1.0 + 1e-12);
-    max_r = std::max(max_r, grown[k]);
-  }
-  if (!std::isfinite(max_r)) return ql;
-  ql.rstep = max_r > 0.0 ? (float)(max_r / 65535.0 * (1.0 + 1e-6)) : 1.0f;
-  for (size_t k = 0; k < n_slots; k++) {
-    if (!(bb.slot64[k].r >= 0.0)) continue;
-    double qd = std::ceil(grown[k] / (double)ql.rstep);
-    while (qd <= 65535.0 && (double)((float)qd * ql.rstep) < grown[k]) qd += 1.0;
-    if (qd > 65535.0) return ql;
-    const size_t w = (k / BVH_LEAF) * 8 + 6 + (k % BVH_LEAF) / 2;
-    ql.rec[w] |= (uint32_t)qd << (16 * (k % 2));
-  }
-  ql.ok = ql.max_err <= 0.5 * CULL_M * (double)sph_scale;
-  return ql;
-}
-
 rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   if (!c || !sd) return fail(c, RTX_EINVAL, "null argument");
   if (sd->n_objects < 0 || sd->n_lights < 0 || sd->n_textures < 0)
@@ -855,6 +602,28 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   for (int a = 0; a < 3; a++) S.q_org[a] = ql.org[a], S.q_step[a] = ql.step[a];
   S.q_rstep = ql.rstep;
   S.q_ok = ql.ok && S.n_nodes <= 32767 && (int64_t)S.n_slots <= 32767;   // references fit int16 stack entries
+  // a decoded center lies within max_err of the true one; a decoded radius within max_err + 2 rstep of R
+  // (ceil to the step, at most one more step: quantize_leaves)
+  S.q_err = (float)((ql.max_err + 2.0 * (double)ql.rstep) * 1.01 + 1e-9 * ql.max_r);
+  {                                                  // the spheres' box, float32, rounded outwards
+    double mn[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, mx[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    for (const Sphere64& sp : sph64)
+      for (int a = 0; a < 3; a++) {
+        mn[a] = std::min(mn[a], sp.c[a] - fabs(sp.r));
+        mx[a] = std::max(mx[a], sp.c[a] + fabs(sp.r));
+      }
+    for (int a = 0; a < 3; a++) {
+      if (!(mn[a] <= mx[a])) {                       // no spheres: an empty box far away
+        S.root_c[a] = 3e38f;
+        S.root_h[a] = 0.0f;
+        continue;
+      }
+      const float cf = (float)(0.5 * (mn[a] + mx[a]));
+      const double h = std::max(mx[a] - (double)cf, (double)cf - mn[a]);
+      S.root_c[a] = cf;
+      S.root_h[a] = f32_up(h * (1.0 + 1e-9) + 1e-30);
+    }
+  }
   HIPCHK(c, hipMemcpy(c->d_scene, &S, sizeof S, hipMemcpyHostToDevice));
   c->have_scene = true;
   return RTX_OK;
@@ -1025,10 +794,6 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // has its sample re-rendered by the lanes engine (option lv_hl_cap: the size)
   const size_t hlcap = c->opt_lv_hl_cap > 0 ? (size_t)c->opt_lv_hl_cap : std::max<size_t>(4096, lcap / 256);
   const size_t sz_hlq = al256(hlcap * 64);
-  // exact_raises: the shading hits whose covers' raises k_hl_raise checks, at most one per record (with
-  // 1/4 of the records C4's deep levels overflowed: 15 M samples re-rendered, 49 s per frame, r07g)
-  const size_t xrcap = c->opt_exact_raises ? std::max<size_t>(4096, lcap) : 0;
-  const size_t sz_xrq = al256(xrcap * 32);
   const size_t sz_ctl = al256(sizeof(LevelCtl)), sz_redo = al256(n0 * 4), sz_smp = al256(n0 * 32),
                sz_stage = al256(scap * RAY_BYTES), sz_rec = al256(lcap * (size_t)rec_bytes),
                sz_extra = al256((npx + 64) * 4);
@@ -1045,7 +810,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // others' levels).  The extra-sample list and the statistics are shared
   // (appended / added atomically); each part has its own level buffers, its
   // own lanes-engine work counter and ray stacks for its overflow re-render.
-  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_xrq;
+  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq;
   const size_t total = parts * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
@@ -1062,8 +827,6 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_area = split ? (double*)q : nullptr; q += sz_area;
     k.lv_hlq = (double*)q;                    q += sz_hlq;
     k.lv_hlq_cap = (uint32_t)hlcap;
-    k.lv_xrq = xrcap ? (double*)q : nullptr;  q += sz_xrq;
-    k.lv_xrq_cap = (uint32_t)xrcap;
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "rtx_launch.h"
 #include "rtx_scene.h"
@@ -240,6 +241,86 @@ RTX_SHADE_FN double penumbra(V3 C, double R, V3 T, V3 lt, double radius, uint32_
   return 1.0;
 }
 
+// ----------------------------------------------------------------- World#lit_area's raises
+// Sphere#cover_area (sphere.rb:28-57) runs its penumbra arithmetic for every
+// sphere, whatever its binary factor, and Math.acos raises Math::DomainError
+// for a cos_theta below -1 (only the upper clamp exists, :43-44).  Inside the
+// branch d > |R - r1| neither can be below -1 in exact arithmetic:
+//   cos_theta1 + 1 = (r1 + d - R)(r1 + d + R) / (2 r1 d),
+//   cos_theta2 + 1 = (R + d - r1)(R + d + r1) / (2 R d);
+// rounded, either can when d is within a few ulps of |R - r1| (DESIGN.md §2.4;
+// tools/raise_search.py finds such configurations).  The shading walks skip
+// the penumbra of spheres whose factor is 0, so these raises need their own
+// check: World#high_lights' lit_area (world.rb:92-93) by its own walk
+// (lit_area_raises), World#local_lights' (world.rb:76) inside the shadow walk
+// (option exact_raises, the default: xr_setup / xr_band below).
+//
+// penumbra_raises: the reference's own operations up to the two acos
+// arguments (the bits of penumbra() and of rt_oracle.c's cover_area).
+__device__ __forceinline__ bool penumbra_raises(V3 C, double R, V3 T, V3 lt, double radius) {
+  const double t = vdot(vsub(C, T), lt) / vr2(lt);
+  const V3 x1 = vadd(T, vsc(lt, t));
+  const double r1 = radius * (vr(vsub(x1, T)) / vr(lt));
+  const double d = vr(vsub(x1, C));
+  if (d >= r1 + R) return false;                 // :38-39 (a NaN goes on, as in Ruby, and never raises)
+  if (!(d > fabs(R - r1))) return false;         // :42
+  const double c1 = (r1 * r1 + d * d - R * R) / (2.0 * r1 * d);
+  const double c2 = (R * R + d * d - r1 * r1) / (2.0 * R * d);
+  return c1 < -1.0 || c2 < -1.0;                 // ([x, 1.0].min < -1 iff x < -1)
+}
+
+// Option exact_raises inside the shadow walk of World#lit_area(T, L, radius)
+// (DESIGN.md §2.4).  A sphere whose cover_area raises although its binary
+// factor is 0 touches the surface of the double cone rho = radius |t| around
+// the line Q(t) = T + t (L - T) (t = 1 at the light) in the cross-section
+// through its own center: the cone's circle there (r1 = radius |t|) and the
+// sphere's are internally tangent, d = |R - r1| (sphere.rb:42), up to a few
+// binary64 ulps.  So
+//   * at a leaf, a sphere can raise only if its distance rho from the line
+//     lies within mg of |R - r1| (xr_band, on the pre-test's own float32
+//     quantities: l = rho^2 |d|^2 up to 14 ulps of |oc|^2 |d|^2, q = (C - T).d,
+//     r1 = radius |q| / |d|^2); those go to the binary64 test (penumbra_raises);
+//   * a box that holds one meets the cone: a point P of the spheres' box within
+//     radius |t| (+ mg) of Q(t) has, on each axis, |t| (|d_a| - radius) <=
+//     |c_a - T_a| + h_a + mg, which bounds |t| by tm (xr_setup), so the walk
+//     slab-tests the child boxes dilated by radius tm + mg over t in [-tm, tm];
+//     the segment's own boxes (t in [0, 1], dilated by m S <= mg) are among
+//     them, so the covers' walk is unchanged.
+// The box dilation mg = 2e-5 S (1 + radius / |d|) is ten times the float32
+// error of T, d and the box bounds (as the covers' m S, §2.2).  The band's own
+// half-width is 32 float32 ulps of S (1 + radius / |d|): the float32 geometry
+// (T, d, the centers and radii rounded, S >= |T|_1, |C|_1 + R) moves rho, R and
+// r1 by less than 10 ulps of S (1 + radius / |d|) from the binary64 values whose
+// tangency raises (to within a few binary64 ulps), and the rounding of l and of
+// the squared bounds is covered separately (4e-6 (sq + hi^2) |d|^2 >= 14 ulps of
+// sq |d|^2); 16-bit leaf records add their decoding error (q_err) to both.
+// A ray for which these bounds are not finite walks every sphere in order and
+// tests each one in binary64.
+struct XrRay {
+  float k;       // radius / |d|^2: r1 = k |q|
+  float mb;      // the band's half-width (with the 16-bit records' decoding error)
+  bool all;      // no valid float32 bound: every sphere goes to the binary64 test
+};
+
+__device__ __forceinline__ XrRay xr_ray(float Sx, float dd, double radius, float qerr) {
+  XrRay x;
+  // hardware reciprocal / rsqrt (1 ulp): the bounds carry far more margin
+  const float rad = (float)radius, kn = rad * __builtin_amdgcn_rsqf(dd);
+  x.k = rad * __builtin_amdgcn_rcpf(dd);
+  x.mb = 32.0f * 5.9604645e-8f * Sx * (1.0f + kn) + (2.0f + kn) * qerr;
+  x.all = !(__builtin_isfinite(x.k) && __builtin_isfinite(x.mb) && dd > 0.0f);
+  return x;
+}
+
+// rho = |R - r1| within mb, for one sphere: l = |oc|^2 |d|^2 - (oc.d)^2 and sq =
+// |oc|^2 as the pre-test computed them, R its radius.
+__device__ __forceinline__ bool xr_band(const XrRay& x, float dd, float l, float q, float sq, float R) {
+  const float t = fabsf(R - x.k * fabsf(q));
+  const float lo = fmaxf(t - x.mb, 0.0f), hi = t + x.mb;
+  const float e = 4e-6f * (sq + hi * hi) * dd;   // l's rounding (<= 14 ulps of sq dd) and the bounds'
+  return x.all || (l >= lo * lo * dd - e && l <= hi * hi * dd + e);
+}
+
 // ----------------------------------------------------------------- the query
 // One ordered walk over every object with ray (o, d), for every active lane.
 //   EXTEND: World#intersect — nearest hit (strict <, YAML order) -> best/besti.
@@ -248,7 +329,7 @@ RTX_SHADE_FN double penumbra(V3 C, double R, V3 T, V3 lt, double radius, uint32_
 template <bool COUNT, typename SPH>
 __device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o, V3 d,
                                       V3 L, double radius, double& best, int& besti, V3& bhit, bool& bin,
-                                      double& total, uint32_t& err, unsigned long long* cnt) {
+                                      double& total, uint32_t& err, unsigned long long* cnt, bool xr = false) {
   const double r = vr(d);
   const double r2 = r * r;                        // front.r2
   // front.normalize is needed only by a sphere that passes the pre-test:
@@ -270,6 +351,9 @@ __device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o
   const float ms2 = CULL_M * Sx * Sx;
   const float kline = dd * ms2;
   const float qneg = -CULL_M * Sx * sqrtf(dd);
+  xr = xr && !ext;                                // exact_raises: the shadow walk's band check
+  const XrRay xrr = xr_ray(Sx, dd, radius, 0.0f);
+  const bool xall = xrr.all || !(__builtin_isfinite(Sx) && __builtin_isfinite(kline));
   if (COUNT) {
     if (ext) {
       cnt[C_SPHERE_TESTS] += S.n_sphere;
@@ -305,17 +389,30 @@ __device__ __forceinline__ void query(const SceneDev& S, SPH sph, bool ext, V3 o
           c[u].z = sph[b + 2];
           c[u].w = sph[b + 3];
         }
-        uint32_t keep = 0;
+        uint32_t keep = 0, xkeep = 0;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           const float ocx = c[u].x - ox, ocy = c[u].y - oy, ocz = c[u].z - oz;
           const float s = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
           const float q = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
-          const bool miss_line = __builtin_fmaf(s, dd, -q * q) > __builtin_fmaf(dd, c[u].w, kline);
+          const float l = __builtin_fmaf(s, dd, -q * q);
+          const bool miss_line = l > __builtin_fmaf(dd, c[u].w, kline);
           const bool behind = q < qneg && s > c[u].w + ms2;
           keep |= (miss_line || behind) ? 0u : (1u << u);
+          if (xr && (xall || xr_band(xrr, dd, l, q, s, __builtin_amdgcn_sqrtf(c[u].w)))) xkeep |= 1u << u;
         }
-        if (k0 + 4 > run.count) keep &= (1u << (run.count - k0)) - 1u;
+        if (k0 + 4 > run.count) {
+          keep &= (1u << (run.count - k0)) - 1u;
+          xkeep &= (1u << (run.count - k0)) - 1u;
+        }
+        // exact_raises: the binary64 test of every sphere the band keeps (its cover_area's
+        // acos arguments, whatever its factor; a factor-1 cover checks again below)
+        while (xkeep && !(err & 0xffu)) {
+          const int u = __builtin_ctz(xkeep);
+          xkeep &= xkeep - 1;
+          const RTX_CONST Sphere64& sp = sph64[run.rec0 + k0 + u];
+          if (penumbra_raises(v3(sp.c[0], sp.c[1], sp.c[2]), sp.r, o, d, radius)) seterr(err, ERR_DOMAIN);
+        }
 #if RTX_STAMPS == 2
         if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
           for (int u = 0; u < 4; u++) atomicAdd(&rtx_stamps[6], __ballot(keep >> u & 1) ? 1ull : 0ull);
@@ -474,7 +571,7 @@ __device__ __forceinline__ SlabRay slab_setup(const SceneDev& S, V3 o, V3 d) {
 // Entry distance of child box k of `node` if the ray may want it (the slab test
 // of the box dilated by m*S, §2.2, against the far bound thi), else +inf.
 template <typename NR>
-__device__ __forceinline__ float slab_key(const NR& node, int k, const SlabRay& s, float thi) {
+__device__ __forceinline__ float slab_key(const NR& node, int k, const SlabRay& s, float tlo, float thi) {
   // {t0, t1} per axis in one v_pk_fma_f32 each: the same fused FP32 operations as
   // fmaf(lo, i, -a), fmaf(hi, i, -b)
   const F2 tx = __builtin_elementwise_fma(*reinterpret_cast<const F2*>(&node.lh[0][k][0]), s.pix, s.pax);
@@ -484,7 +581,44 @@ __device__ __forceinline__ float slab_key(const NR& node, int k, const SlabRay& 
   const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
   const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
   // empty slots hold a box at (3e38, 3e38, 3e38): never wanted by a finite ray
-  return (tn <= tf && tf >= 0.0f && tn <= thi) ? tn : __builtin_inff();
+  return (tn <= tf && tf >= tlo && tn <= thi) ? tn : __builtin_inff();
+}
+
+// exact_raises (above): the cone's extent in t over the spheres' box, for each
+// nappe.  A point Q(t) = T + t d within radius |t| + mg of the box on axis a has
+// |t| (|d_a| - radius) <= (the box's far side from T along the nappe's
+// direction on a) + mg, so for every axis with |d_a| > radius: t <= tf going
+// towards the light, -t <= tb going away from it.  The child boxes are then
+// slab-tested dilated by radius max(tb, tf) + mg over t in [-tb, tf], which
+// holds the segment's own boxes (t in [0, 1], dilated by m S <= mg).  False
+// when no finite bound exists (the caller walks every sphere).
+__device__ __forceinline__ bool xr_setup(const SceneDev& S, SlabRay& s, double radius, float& tlo, float& thi) {
+  if (!s.fin) return false;
+  const float rad = (float)radius;
+  const float mg = CULL_M * s.Sx * (1.0f + rad * __builtin_amdgcn_rsqf(s.dd));   // (node boxes are exact: no decoding error)
+  float tf = __builtin_inff(), tb = __builtin_inff();
+  const float o[3] = {s.ox, s.oy, s.oz}, dv[3] = {s.dx, s.dy, s.dz};
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    const float ad = fabsf(dv[a]), den = ad - rad;
+    if (!(den > 1e-5f * (ad + rad))) continue;
+    const float iden = __builtin_amdgcn_rcpf(den);                     // (1 ulp; the bounds are widened below)
+    const float up = (S.root_c[a] + S.root_h[a] + mg - o[a]) * iden;   // to the box's high side
+    const float dn = (o[a] - (S.root_c[a] - S.root_h[a]) + mg) * iden; // to its low side
+    tf = fminf(tf, dv[a] > 0.0f ? up : dn);
+    tb = fminf(tb, dv[a] > 0.0f ? dn : up);
+  }
+  tf = fmaxf(tf, 0.0f) * (1.0f + 1e-5f);
+  tb = fmaxf(tb, 0.0f) * (1.0f + 1e-5f);
+  if (!(tf < 1e30f && tb < 1e30f)) return false;
+  const float r = __builtin_fmaf(rad, fmaxf(tf, tb), mg) * (1.0f + 1e-5f);   // >= m S: the covers' dilation too
+  const float ix = s.pix.x, iy = s.piy.x, iz = s.piz.x;
+  s.pax = F2{-((s.ox + r) * ix), -((s.ox - r) * ix)};
+  s.pay = F2{-((s.oy + r) * iy), -((s.oy - r) * iy)};
+  s.paz = F2{-((s.oz + r) * iz), -((s.oz - r) * iz)};
+  tlo = -tb;
+  thi = tf;
+  return __builtin_isfinite(r);
 }
 
 // Planes and boxes first, in run order (their order does not matter either).
@@ -566,7 +700,7 @@ template <int BS, typename LP, typename XP, typename OP>
 __device__ __forceinline__ void walk_leaf(int lf, LP leaf4, XP x64, OP xobj, const SlabRay& s, bool ext, V3 o, V3 d,
                                           V3 dn, double r, double r2, V3 L, double radius, double& best, int& besti,
                                           V3& bhit, bool& bin, float& thi, uint32_t& err, int* ci, double* cv,
-                                          int& ncov, bool& ovf) {
+                                          int& ncov, bool& ovf, bool xr, float qerr) {
   const int v = ~lf;
   const int slot0 = (v >> 2) * BVH_LEAF;
   const int cnt = (v & 3) + 1;
@@ -574,7 +708,8 @@ __device__ __forceinline__ void walk_leaf(int lf, LP leaf4, XP x64, OP xobj, con
   // operations as the per-sphere form in query())
   float4 cx, cy, cz, cw;
   leaf_records(leaf4, v, cx, cy, cz, cw);
-  uint32_t keep = 0;
+  uint32_t keep = 0, xkeep = 0;
+  const XrRay xrr = xr ? xr_ray(s.Sx, s.dd, radius, qerr) : XrRay{};
   const F2 po = {s.ox, s.ox}, poy = {s.oy, s.oy}, poz = {s.oz, s.oz};
   const F2 pdx = {s.dx, s.dx}, pdy = {s.dy, s.dy}, pdz = {s.dz, s.dz}, pdd = {s.dd, s.dd};
   const F2 pkl = {s.kline, s.kline}, pms = {s.ms2, s.ms2};
@@ -591,8 +726,18 @@ __device__ __forceinline__ void walk_leaf(int lf, LP leaf4, XP x64, OP xobj, con
     const bool m0 = l.x > rr.x || (q.x < s.qneg && sq.x > wm.x);   // misses the line, or wholly behind
     const bool m1 = l.y > rr.y || (q.y < s.qneg && sq.y > wm.y);
     keep |= (m0 ? 0u : 1u << (2 * h)) | (m1 ? 0u : 2u << (2 * h));
+    if (xr)                                         // exact_raises: rho within mg of |R - r1|
+      xkeep |= (xr_band(xrr, s.dd, l.x, q.x, sq.x, __builtin_amdgcn_sqrtf(Wr.x)) ? 1u << (2 * h) : 0u) |
+               (xr_band(xrr, s.dd, l.y, q.y, sq.y, __builtin_amdgcn_sqrtf(Wr.y)) ? 2u << (2 * h) : 0u);
   }
   keep &= (1u << cnt) - 1u;
+  xkeep &= (1u << cnt) - 1u;
+  while (xkeep && !(err & 0xffu)) {                 // their cover_area's acos arguments in binary64
+    const int u = __builtin_ctz(xkeep);
+    xkeep &= xkeep - 1;
+    const Sphere64 sp64 = x64[slot0 + u];
+    if (penumbra_raises(v3(sp64.c[0], sp64.c[1], sp64.c[2]), sp64.r, o, d, radius)) seterr(err, ERR_DOMAIN);
+  }
   while (keep) {
     const int u = __builtin_ctz(keep);
     keep &= keep - 1;
@@ -622,11 +767,11 @@ __device__ __forceinline__ void walk_leaf(int lf, LP leaf4, XP x64, OP xobj, con
 template <int BS>
 __device__ __forceinline__ void walk_covers(const SceneDev& S, V3 o, V3 d, V3 L, double radius, double& best,
                                             int& besti, V3& bhit, bool& bin, double& total, uint32_t& err,
-                                            const double* cv, int ncov, bool ovf) {
+                                            const double* cv, int ncov, bool ovf, bool xr) {
   total = 1.0;
   if (ovf) {
     // more than COVER_K non-zero covers: the ordered linear walk (rare)
-    query<false>(S, cptr(S.sph32), false, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
+    query<false>(S, cptr(S.sph32), false, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr, xr);
   } else {
     for (int k = 0; k < ncov; k++) total -= cv[k * BS];
   }
@@ -644,22 +789,26 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
                                           double* cv,
                                           bool ext, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
                                           V3& bhit, bool& bin, double& total, uint32_t& err, int& ref, int& sp,
-                                          int& ncov, bool& ovf, bool resume, int postpone) {
+                                          int& ncov, bool& ovf, bool resume, int postpone, bool xr = false) {
   const double r = vr(d);
   const double r2 = r * r;                        // front.r2
   V3 dn = d;
   if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r); // front.normalize (same bits as the walk)
-  const SlabRay s = slab_setup(S, o, d);
+  SlabRay s = slab_setup(S, o, d);
+  xr = xr && !ext;                                // exact_raises: the shadow walk also checks the raises
+  constexpr bool Q16 = std::is_same<LP, QLeaf>::value;   // 16-bit leaf records: their decoding error
+  const float rf = (float)r;
+  // ray parameter range: EXTEND [0, the current best hit], SHADOW [0, the light]; with
+  // exact_raises the cone bound [-tm, tm] (xr_setup), the child boxes dilated to its radius
+  float tlo = 0.0f;
+  float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + s.mS / rf;
   // A non-finite or zero ray makes no cull (comparisons would be unordered).
-  if (!s.fin) {
+  if (!s.fin || (xr && !xr_setup(S, s, radius, tlo, thi))) {
     // no float32 cull is valid for this ray: the ordered linear walk (same result)
     if (!ext) total = 1.0;
-    query<false>(S, cptr(S.sph32), ext, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr);
+    query<false>(S, cptr(S.sph32), ext, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr, xr);
     return true;
   }
-  const float rf = (float)r;
-  // far bound on the ray parameter: EXTEND the current best hit, SHADOW the light
-  float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + s.mS / rf;
   if (!resume) {
     ncov = 0;
     ovf = false;
@@ -696,7 +845,7 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         ch[k] = nodes[ref].child[k];
-        key[k] = slab_key(nodes[ref], k, s, thi);
+        key[k] = slab_key(nodes[ref], k, s, tlo, thi);
       }
 #define RTX_CS(a, b)         \
   if (key[b] < key[a]) {     \
@@ -735,7 +884,7 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
     }
     if (lf != BVH_NONE)
       walk_leaf<BS>(lf, leaf4, x64, xobj, s, ext, o, d, dn, r, r2, L, radius, best, besti, bhit, bin, thi, err, ci, cv,
-                    ncov, ovf);
+                    ncov, ovf, xr, Q16 ? S.q_err : 0.0f);
     if (!SPEC) {
       ref = sp > 0 ? stk[(--sp) * BS] : BVH_NONE;
       if (PP && __popcll(__ballot(ref != BVH_NONE)) < postpone && ref != BVH_NONE) return false;
@@ -748,35 +897,8 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
     atomicAdd(&w[2], ws_li);
     atomicAdd(&w[3], ws_ll);
   }
-  if (!ext) walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf);
+  if (!ext) walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, xr);
   return true;
-}
-
-// ----------------------------------------------------------------- World#lit_area's raises
-// Sphere#cover_area (sphere.rb:28-57) runs its penumbra arithmetic for every
-// sphere, whatever its binary factor, and Math.acos raises Math::DomainError
-// for a cos_theta below -1 (only the upper clamp exists, :43-44).  Inside the
-// branch d > |R - r1| neither can be below -1 in exact arithmetic:
-//   cos_theta1 + 1 = (r1 + d - R)(r1 + d + R) / (2 r1 d),
-//   cos_theta2 + 1 = (R + d - r1)(R + d + r1) / (2 R d);
-// rounded, either can when d is within a few ulps of |R - r1| (DESIGN.md §2.4;
-// tools/raise_search.py finds such configurations).  The shading walks skip
-// the penumbra of spheres whose factor is 0, so these raises need their own
-// walk: World#high_lights' lit_area (world.rb:92-93) always, World#local_lights'
-// (world.rb:76) with option exact_raises.
-//
-// penumbra_raises: the reference's own operations up to the two acos
-// arguments (the bits of penumbra() and of rt_oracle.c's cover_area).
-__device__ __forceinline__ bool penumbra_raises(V3 C, double R, V3 T, V3 lt, double radius) {
-  const double t = vdot(vsub(C, T), lt) / vr2(lt);
-  const V3 x1 = vadd(T, vsc(lt, t));
-  const double r1 = radius * (vr(vsub(x1, T)) / vr(lt));
-  const double d = vr(vsub(x1, C));
-  if (d >= r1 + R) return false;                 // :38-39 (a NaN goes on, as in Ruby, and never raises)
-  if (!(d > fabs(R - r1))) return false;         // :42
-  const double c1 = (r1 * r1 + d * d - R * R) / (2.0 * r1 * d);
-  const double c2 = (R * R + d * d - r1 * r1) / (2.0 * R * d);
-  return c1 < -1.0 || c2 < -1.0;                 // ([x, 1.0].min < -1 iff x < -1)
 }
 
 // Which spheres can raise, in float32 (s: signed distance of the center along
@@ -896,7 +1018,8 @@ __device__ __forceinline__ bool lit_area_raises(const SceneDev& S, const Bvh4Nod
   return false;
 }
 
-// lit_area_raises over a launch's sphere mode: the hierarchy from where the
+// lit_area_raises over a launch's sphere mode (the lanes engine's inline highlight
+// check): the hierarchy from where the
 // workgroup staged it (SphMode), the lane's LDS traversal stack.
 template <int SPH, int BS>
 __device__ __forceinline__ bool raises_walk(const KParams& p, char* lds, V3 T, V3 L, double radius) {
@@ -1197,9 +1320,6 @@ __device__ __forceinline__ Ray lens_ray(const CameraDev& c, V3 target, int x, in
 // (Math.acos, sphere.rb:45-46): `raises(T, L, radius)` answers whether it does
 // (lit_area_raises), asked only while the ray has no raise yet.
 // att_fn() gives the ray's attenuation, asked for only when a light fires.
-#ifndef RTX_EXACT_RAISES
-#define RTX_EXACT_RAISES 1   // 0: diagnostic builds only (option exact_raises compiled out of the walk kernels)
-#endif
 #ifndef RTX_HL_RAISES
 #define RTX_HL_RAISES 1      // 0: diagnostic builds only (timing without the highlight's lit_area raise walk)
 #endif

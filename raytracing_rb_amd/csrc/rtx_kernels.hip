@@ -280,22 +280,24 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
     }
     if (mode == M_DONE) break;
 
-    // ---- B: the object walk, shared by EXTEND and SHADOW lanes
+    // ---- B: the object walk, shared by EXTEND and SHADOW lanes (a SHADOW walk
+    // also checks its covers' acos raises, option exact_raises: rtx_device.h xr_band)
+    const bool xr = p.exact_raises != 0 && mode == M_SHADOW;
     if (SPH == SPH_LIN_LDS)
-      query<COUNT>(S, sph_lds, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, cnt);
+      query<COUNT>(S, sph_lds, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, cnt, xr);
     else if (SPH == SPH_LIN_SCALAR)
-      query<COUNT>(S, sph_k, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, cnt);
+      query<COUNT>(S, sph_k, mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, cnt, xr);
     else if (SPH == SPH_BVH_LDS)
       q_resume = !query_bvh<BS, PP>(S, reinterpret_cast<const Bvh4Node*>(lds),
                                 reinterpret_cast<const float4*>(lds + p.lds_leaf), S.bvh_sph64, S.bvh_obj, stk,
                                 cov_i, cov_v,
                                 mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, q_ref, q_sp,
-                                q_ncov, q_ovf, q_resume, p.postpone);
+                                q_ncov, q_ovf, q_resume, p.postpone, xr);
     else
       q_resume = !query_bvh<BS, PP>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, S.bvh_obj,
                                 stk, cov_i, cov_v,
                                 mode == M_EXTEND, qo, qd, qL, qrad, best, besti, hit, hin, total, err, q_ref, q_sp,
-                                q_ncov, q_ovf, q_resume, p.postpone);
+                                q_ncov, q_ovf, q_resume, p.postpone, xr);
     if (RTX_STAMPS) {
       t1 = stamp();
       tB += t1 - t0;
@@ -318,9 +320,6 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
     } else {
       // World#local_lights (world.rb:72-80) fused with the light loop of
       // WorldObject#local_lighting (world_object.rb:51-74): same order, same sums.
-      // option exact_raises: the raises of the covers the walk skipped (factor 0)
-      if (RTX_EXACT_RAISES && p.exact_raises && !(err & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, qrad))
-        seterr(err, ERR_DOMAIN);
       const double area = total > 0 ? total : 0.0;
       if (area > 0) {
         const LightDev& L = S.light[li];

@@ -29,7 +29,6 @@ struct LevelCtl {
   uint32_t redo_n;                              // level-0 items handed to the lanes engine (capacity overflow)
   uint32_t dropped;                             // child rays that found no room (diagnostic)
   uint32_t hl_n;                                // highlight rays whose lit_area raise check is deferred (k_hl_raise)
-  uint32_t xr_n;                                // shading hits whose covers' raise check is deferred (exact_raises)
   uint32_t pad[27];                             // (pad[0]: the lanes-engine work counter of parts 1..)
   uint32_t sc[LV_MAXL + 1][LV_SLICES * 32];     // rays allocated in slice s of level d: sc[d][32 s]
   uint32_t sh[LV_MAXL + 1][LV_SLICES * 32];     // split phases: hits of level d in slice s
@@ -110,11 +109,9 @@ struct KParams {
   int32_t lv_fin_tiles;            // tree reduction pass 0: tiles of the batch (grid-stride loop when the grid is smaller)
   int32_t lv_redo_blocks;          // the lanes-engine re-render of overflowed samples: at most this many workgroups (0: all resident)
   int32_t lv_ray_dbl;              // staged ray record, doubles: 10 (80 B: path < 2^32, RNG key decoded from the root) or 12
-  int32_t exact_raises;            // 1: every shadow walk (local_lights) also runs lit_area_raises (option exact_raises)
+  int32_t exact_raises;            // 1: every shadow walk (local_lights) also checks its covers' acos raises (option exact_raises)
   uint32_t lv_hlq_cap;             // entries of lv_hlq
   double* lv_hlq;                  // highlight rays of the batch whose lit_area raise k_hl_raise checks (8 doubles each)
-  uint32_t lv_xrq_cap;             // entries of lv_xrq (0 without exact_raises)
-  double* lv_xrq;                  // exact_raises: shading hits whose local_lights raises k_hl_raise checks (4 doubles each)
 };
 
 // Where the sphere walk reads its records:

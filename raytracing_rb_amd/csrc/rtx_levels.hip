@@ -354,15 +354,18 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
 }
 
 // One walk (EXTEND or SHADOW) through the launch's sphere mode.
+// xr: a SHADOW walk of local_lights also checks the covers' acos raises
+// (option exact_raises, rtx_device.h xr_band).
 template <int SPH, int BS>
 __device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V3 o, V3 d, V3 L, double rad,
-                                        double& best, int& besti, V3& hit, bool& hin, double& total, uint32_t& err) {
+                                        double& best, int& besti, V3& hit, bool& hin, double& total, uint32_t& err,
+                                        bool xr = false) {
   const SceneDev& S = p.scene;
   if (SPH == SPH_LIN_LDS) {
     query<false>(S, reinterpret_cast<const float*>(lds), ext, o, d, L, rad, best, besti, hit, hin, total, err,
-                 nullptr);
+                 nullptr, xr);
   } else if (SPH == SPH_LIN_SCALAR) {
-    query<false>(S, cptr(S.sph32), ext, o, d, L, rad, best, besti, hit, hin, total, err, nullptr);
+    query<false>(S, cptr(S.sph32), ext, o, d, L, rad, best, besti, hit, hin, total, err, nullptr, xr);
   } else {
     int* stk = reinterpret_cast<int*>(lds + p.lds_stack) + threadIdx.x;
     int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
@@ -374,24 +377,24 @@ __device__ __forceinline__ void lv_walk(const KParams& p, char* lds, bool ext, V
                         S.q_step[0], S.q_step[1], S.q_step[2], S.q_rstep};
       query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), ql, S.bvh_sph64, S.bvh_obj,
                            qstack(lds, p), cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref,
-                           q_sp, q_ncov, q_ovf, false, 0);
+                           q_sp, q_ncov, q_ovf, false, 0, xr);
     } else if (SPH == SPH_BVH_LDS)
       query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
                            S.bvh_sph64, S.bvh_obj, stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total,
-                           err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
+                           err, q_ref, q_sp, q_ncov, q_ovf, false, 0, xr);
     else if (SPH == SPH_BVH_LDSX)
       query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(lds + p.lds_leaf),
                            reinterpret_cast<const Sphere64*>(lds + p.lds_x64),
                            reinterpret_cast<const int32_t*>(lds + p.lds_xobj), stk, cov_i, cov_v, ext, o, d, L, rad,
-                           best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
+                           best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf, false, 0, xr);
     else if (SPH == SPH_BVH_MIX)
       query_bvh<BS, false>(S, reinterpret_cast<const Bvh4Node*>(lds), reinterpret_cast<const float4*>(S.bvh_sph32),
                            S.bvh_sph64, S.bvh_obj, stk, cov_i, cov_v, ext, o, d, L, rad, best, besti, hit, hin, total,
-                           err, q_ref, q_sp, q_ncov, q_ovf, false, 0);
+                           err, q_ref, q_sp, q_ncov, q_ovf, false, 0, xr);
     else
       query_bvh<BS, false>(S, S.bvh, reinterpret_cast<const float4*>(S.bvh_sph32), S.bvh_sph64, S.bvh_obj, stk, cov_i,
                            cov_v, ext, o, d, L, rad, best, besti, hit, hin, total, err, q_ref, q_sp, q_ncov, q_ovf,
-                           false, 0);
+                           false, 0, xr);
   }
 }
 
@@ -444,7 +447,7 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
                                           const Item& cur, int root, int x, int y, int sample, int besti, bool hin,
                                           V3 hit, V3 delta, V3 nrm, V3 nn, double c, V3 lc, int nl, char* rec,
                                           int nleaf, uint32_t errA, uint32_t errS, uint32_t errL, uint32_t errP,
-                                          const Material* m, bool last = false, bool xr = true) {
+                                          const Material* m, bool last = false) {
   const SceneDev& S = p.scene;
   const CameraDev& cam = *p.cam;
   const int depth = last ? 1 : cam.depth - level;   // last: the batch's last level (every child is cut off)
@@ -582,38 +585,11 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
     if (!err) err = errP;
     *reinterpret_cast<uint2*>(rec) = make_uint2((err & 0xffu) | ((uint32_t)nleaf << 8) | (mask << 16), child0);
   }
-  // Option exact_raises: local_lights' lit_area raises of the covers the
-  // shadow walks skipped (factor 0), checked after the levels
-  // by k_hl_raise (an inline walk here cost the kernel registers and spills
-  // even when off).  Only a hit with no raise before local_lights' (errA,
-  // errS, errL) is listed: a raise found there replaces the record's
-  // (local_lighting's, or none).
-  if (RTX_EXACT_RAISES && xr && p.exact_raises) {
-    const bool want = shade && active && !((errA | errS | errL) & 0xffu);
-    const uint64_t wm = __ballot(want);
-    if (wm) {
-      const int lane = (int)__lane_id(), first = __builtin_ctzll(wm);
-      uint32_t b = 0;
-      if (lane == first) b = atomicAdd(&p.lv_ctl->xr_n, (uint32_t)__popcll(wm));
-      b = (uint32_t)__builtin_amdgcn_readlane((int)b, first);
-      if (want) {
-        const uint32_t e = b + (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
-        if (e < p.lv_xrq_cap) {
-          const V3 qo = vadd(hit, delta);     // local_lights' target (world.rb:76)
-          double2* q = reinterpret_cast<double2*>(p.lv_xrq + (size_t)e * 4);
-          q[0] = make_double2(qo.x, qo.y);
-          q[1] = make_double2(qo.z, __builtin_bit_cast(double, (uint64_t)(size_t)(rec - p.lv_rec)));
-        } else {
-          lv_redo(p, root);
-        }
-      }
-    }
-  }
 }
 
 // Level `level` (0 .. trace_depth-1) of one batch in one launch (option
 // lv_split = 0).  Persistent, static chunk schedule.
-template <int SPH, int BS>
+template <int SPH, int BS, bool XR>
 __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
   const SceneDev& S = p.scene;
   extern __shared__ float4 lds_sph[];
@@ -710,7 +686,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
       int bi2 = -1;
       V3 h2 = qo;
       bool in2 = true;
-      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL);
+      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL, XR);
       const double area = tot > 0 ? tot : 0.0;
       if (area > 0) {
         nl++;
@@ -743,9 +719,9 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS>
+template <int SPH, int BS, bool XR>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level) {
-  k_level_body<SPH, BS>(p, level);
+  k_level_body<SPH, BS, XR>(p, level);
   lv_level_done(p, level + 1);
 }
 
@@ -779,7 +755,7 @@ constexpr int LV_RING_FIELDS_SMALL = 5;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
 constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMALL * 8;
 
-template <int SPH, int BS, int RF, bool LAST>
+template <int SPH, int BS, int RF, bool LAST, bool XR>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
   constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
@@ -984,7 +960,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       int bi2 = -1;
       V3 h2 = qo;
       bool in2 = true;
-      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL);
+      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL, XR);
       const double area = tot > 0 ? tot : 0.0;
       if (area > 0) {
         nl++;
@@ -1017,9 +993,9 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS, int RF, bool LAST>
+template <int SPH, int BS, int RF, bool LAST, bool XR>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
-  k_level_c_body<SPH, BS, RF, LAST>(p, level);
+  k_level_c_body<SPH, BS, RF, LAST, XR>(p, level);
   lv_level_done(p, level + 1);
 }
 
@@ -1151,9 +1127,8 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_shadow(KParams p, in
       V3 h2 = qo;
       bool in2 = true;
       uint32_t err = 0;
-      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, err);
-      if (RTX_EXACT_RAISES && p.exact_raises && !(err & 0xffu) && raises_walk<SPH, BS>(p, lds, qo, qL, L.radius))
-        seterr(err, ERR_DOMAIN);
+      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, err,
+                       p.exact_raises != 0);   // (split phases: the check's flag at run time)
       reinterpret_cast<double2*>(p.lv_area)[(size_t)hs * nL + li] =
           make_double2(tot, __builtin_bit_cast(double, (uint64_t)err));
     }
@@ -1224,7 +1199,7 @@ __device__ __forceinline__ void k_lv_shade_body(const KParams& p, int level) {
       }
     }
     lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec,
-              0, errA, errS, errL, errP, shade ? &S.mat[besti] : S.mat, false, false);   // (k_lv_shadow checks exact raises)
+              0, errA, errS, errL, errP, shade ? &S.mat[besti] : S.mat);
   }
 }
 
@@ -1506,7 +1481,6 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
   extern __shared__ int lds_hl[];
   const SceneDev& S = p.scene;
   const uint32_t n = p.lv_ctl->hl_n < p.lv_hlq_cap ? p.lv_ctl->hl_n : p.lv_hlq_cap;
-  const uint32_t nx = p.lv_ctl->xr_n < p.lv_xrq_cap ? p.lv_ctl->xr_n : p.lv_xrq_cap;
   if (stage == 2) {                           // one wave per entry (every lane loads it: uniform flow)
     const uint32_t w0 = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
     for (uint32_t e = w0; e < n; e += nw) {
@@ -1524,21 +1498,9 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
         *h = (*h & ~0xffu) | (err & 0xffu);
       }
     }
-    for (uint32_t e = w0; e < nx; e += nw) {
-      const double2* q = reinterpret_cast<const double2*>(p.lv_xrq + (size_t)e * 4);
-      const double2 a = q[0], b = q[1];
-      const V3 T = v3(a.x, a.y, b.x);
-      bool raised = false;
-      for (int l = 0; l < S.n_light && !raised; l++)
-        raised = lit_area_raises_wave(S, T, v3p(S.light[l].pos), S.light[l].radius);
-      if (raised && __lane_id() == 0) {
-        uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)__builtin_bit_cast(uint64_t, b.y));
-        *h = (*h & ~0xffu) | (uint32_t)ERR_DOMAIN;
-      }
-    }
     return;
   }
-  if (blockIdx.x * 256u >= (n > nx ? n : nx)) return;   // uniform per workgroup
+  if (blockIdx.x * 256u >= n) return;          // uniform per workgroup
   const Bvh4Node* nodes = S.bvh_root != BVH_NONE ? S.bvh : nullptr;
   const float4* leaf4 = reinterpret_cast<const float4*>(S.bvh_sph32);
   int* stk = lds_hl + threadIdx.x;
@@ -1565,22 +1527,6 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
     });
     uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)rec * p.lv_rec_bytes);
     *h = (*h & ~0xffu) | (err & 0xffu);
-  }
-  // exact_raises: every light's lit_area from a listed hit's target (world.rb:72-80)
-  for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < nx; e += gridDim.x * 256) {
-    const double2* q = reinterpret_cast<const double2*>(p.lv_xrq + (size_t)e * 4);
-    const double2 a = q[0], b = q[1];
-    const V3 T = v3(a.x, a.y, b.x);
-    const size_t off = (size_t)__builtin_bit_cast(uint64_t, b.y);
-    bool raised = false;
-    for (int l = 0; l < S.n_light && !raised; l++) {
-      const LightDev& L = S.light[l];
-      raised = lit_area_raises(S, nodes, leaf4, S.bvh_sph64, stk, 256, T, v3p(L.pos), L.radius);
-    }
-    if (raised) {
-      uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + off);
-      *h = (*h & ~0xffu) | (uint32_t)ERR_DOMAIN;
-    }
   }
 }
 
@@ -1621,7 +1567,6 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
     p.lv_ctl->redo_n = 0;
     p.lv_ctl->dropped = 0;
     p.lv_ctl->hl_n = 0;
-    p.lv_ctl->xr_n = 0;
     p.lv_ctl->lay_base[0] = 0;
     p.lv_ctl->lay_base[1] = v;
   }
@@ -1711,8 +1656,9 @@ static hipError_t launch_timed(K kern, long blocks, int bs, size_t lds, hipStrea
 
 // k_level_c for a level: the batch's last level compiled apart.
 template <int SPH, int BS, int RF>
-static void (*level_c_kernel(bool last))(KParams, int) {
-  return last ? k_level_c<SPH, BS, RF, true> : k_level_c<SPH, BS, RF, false>;
+static void (*level_c_kernel(bool last, bool xr))(KParams, int) {
+  if (xr) return last ? k_level_c<SPH, BS, RF, true, true> : k_level_c<SPH, BS, RF, false, true>;
+  return last ? k_level_c<SPH, BS, RF, true, false> : k_level_c<SPH, BS, RF, false, false>;
 }
 
 #ifndef RTX_LV_FUSED_BS
@@ -1729,7 +1675,10 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   KParams q = p;
   q.stk_slots_max = 0;                         // no ray stack in this engine
   size_t lds = lds_layout(q, SPH, BS);
-  auto kern = kind == 0 ? k_level<SPH, BS> : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
+  // exact_raises (the default) compiles the shadow walks' raise check in (k_level / k_level_c <..., XR>)
+  const bool xr = q.exact_raises != 0;
+  auto kern = kind == 0 ? (xr ? k_level<SPH, BS, true> : k_level<SPH, BS, false>)
+              : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
   // hit compaction when the rings fit next to the walk's LDS (k_level_c is
   // instantiated for the fused kernel's block size only)
   if constexpr (BS == fused_bs<SPH>()) if (kind == 0 && q.lv_compact != 0) {
@@ -1740,11 +1689,11 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
     if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level);
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level, xr);
     } else if (BVH && need_small <= budget) {  // the compact ring (C4-sized hierarchies)
       q.lds_ring = (int32_t)ring;
       lds = need_small;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level);
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, xr);
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)

@@ -127,6 +127,9 @@ struct SceneDev {
   // for the pre-test and every reference fits a 16-bit traversal stack
   float q_org[3], q_step[3], q_rstep;
   int32_t q_ok;
+  float q_err;            // bound on |decoded - true| of a 16-bit record's center and radius (exact_raises' band)
+  // box of every sphere (float32, rounded outwards): center and half extents (exact_raises' cone bound)
+  float root_c[3], root_h[3];
 };
 
 struct CameraDev {

@@ -6,9 +6,10 @@ calls of the reference:
   cone the ray is in, and its raise aborts the render.  Reproduced by both
   oracles and both engines.
 * World#local_lights' lit_area (world.rb:76) over spheres whose binary cover
-  factor is 0 (behind the target, or off the line): the shading walks skip
-  them, so the raise is reproduced with option exact_raises = 1; with the
-  default 0 the GPU does not report it (DESIGN.md §2.4 states the departure).
+  factor is 0 (behind the target, inside the cone off the line, beyond the
+  light): with option exact_raises = 1 the shadow walks check them (fused into
+  the walk); the default 0 reports only the covers they
+  evaluate (the departure DESIGN.md §2.3 states).
 
 The raising spheres are found by tools/raise_search.py (committed in
 tests/golden/raise_scenes.json): a sphere placed within a few ulps of the
@@ -26,6 +27,8 @@ import pytest
 from conftest import GOLDEN, ROOT
 
 sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import raise_cases  # noqa: E402
 import raise_search  # noqa: E402
 
 with open(os.path.join(GOLDEN, "raise_scenes.json")) as _f:
@@ -134,7 +137,7 @@ def _first_pixel(status, code):
 
 # ------------------------------------------------------------------ CPU: the search and the oracles
 def test_search_reproduces_committed_configurations():
-    got = raise_search.search_all()
+    got = raise_search.search_all(raise_cases.pixel_T())
     assert got == CASES
 
 
@@ -214,6 +217,45 @@ def test_oracle_raises_on_local_lights_factor0_cover(oracle_lib, tmp_path, case)
         assert out2[0].max() > 0
 
 
+PIXEL_CASES = ["pixel_A_back", "pixel_B_front", "pixel_A_far"]
+
+
+def _pixel_scene(tmp_path, case, fillers=0, sphere=True):
+    """The plane, the light and the raising sphere of a pixel case, seen by
+    raise_search.PIXEL_CAMERA: PIXEL's primary ray hits the plane at exactly
+    the case's T, so its local_lights raises (high-light angle 1 degree: no
+    camera or reflected ray is in the light's cone here)."""
+    c = CASES[case]
+    w = _world(tmp_path, case, 1.0, plane=True, fillers=fillers, sphere=sphere)
+    cc = raise_search.PIXEL_CAMERA
+    cam = tmp_path / "c.yml"
+    cam.write_text(raise_cases.camera_yaml(cc["position"], cc["front"], cc["width"], cc["height"]))
+    return _load(w, str(cam))
+
+
+@pytest.mark.parametrize("case", PIXEL_CASES)
+def test_oracles_raise_at_the_pixel_of_a_factor0_cover(oracle_lib, tmp_path, case):
+    """A whole render raises Math::DomainError first at PIXEL in both oracles;
+    without the sphere it renders."""
+    from oracle import rt_ref
+    from oracle.c_oracle import Oracle
+    c = CASES[case]
+    assert c["T"] == list(raise_cases.pixel_T())
+    sd, cd = _pixel_scene(tmp_path, case)
+    out, status, rc = Oracle(sd, cd).render()
+    assert rc == 3, rc
+    assert _first_pixel(status, 3) == tuple(raise_search.PIXEL)
+    _, cam = rt_ref.load_scene(str(tmp_path / "w.yml"), str(tmp_path / "c.yml"))
+    with pytest.raises(Exception) as e:
+        for xx in range(cd.width):
+            for yy in range(cd.height):
+                cam.render_at(xx, yy)
+    assert "DomainError" in str(e.value) and (xx, yy) == tuple(raise_search.PIXEL)
+    sd2, cd2 = _pixel_scene(tmp_path, case, sphere=False)
+    out2, status2, rc2 = Oracle(sd2, cd2).render()
+    assert rc2 == 0 and not status2.any()
+
+
 # ------------------------------------------------------------------ GPU
 ENGINES = [(0, {}), (1, {}), (1, dict(lv_split=1)), (1, dict(lv_compact=0)), (1, dict(lv_compact=2)),
            (0, dict(bvh=2)), (1, dict(bvh=2)), (1, dict(bvh=2, sphere_src=2)), (1, dict(bvh=2, sphere_src=4)),
@@ -278,16 +320,49 @@ def test_gpu_highlight_raise_through_trace_and_path_trace(gpu, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["shadow_A", "shadow_B"])
 @pytest.mark.parametrize("fillers", [0, 40, 300])
-def test_gpu_local_lights_factor0_raise_with_exact_raises(gpu, tmp_path, case, fillers):
+def test_gpu_local_lights_factor0_raise(gpu, tmp_path, case, fillers):
+    """rtx_trace (the lanes engine, every sphere walk): exact_raises = 1 reports
+    the raise of the factor-0 cover; the default returns the colour."""
     from oracle.c_oracle import Oracle
     from raytracing_rb_amd.runtime import RtxError
     sd, cd, rays, keys = _shadow_trace(tmp_path, case, fillers=fillers)
     ref, st, rc = Oracle(sd, cd).trace(rays, keys)
     assert rc == 3
     for engine, opts in ENGINES:
-        # default: the skipped cover is not checked: the colour, no raise
-        fb = _renderer(sd, cd, engine, **opts).trace(rays, keys)
-        assert np.isfinite(fb).all()
         with pytest.raises(RtxError) as e:
             _renderer(sd, cd, engine, exact_raises=1, **opts).trace(rays, keys)
         assert e.value.kind == "domain", (engine, opts)
+        fb = _renderer(sd, cd, engine, **opts).trace(rays, keys)
+        assert np.isfinite(fb).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PIXEL_CASES)
+@pytest.mark.parametrize("fillers", [0, 40, 300])
+def test_gpu_local_lights_factor0_raise_in_a_render(gpu, tmp_path, case, fillers):
+    """A whole render through every engine / walk / ring / split / sphere mode
+    with exact_raises = 1 (the level kernels' fused shadow-walk check,
+    DESIGN.md §2.4): the same Math::DomainError at the same first pixel as the
+    oracle; the default renders (no raise reported) and every other pixel
+    equals the oracle's frame without the raising sphere's raise."""
+    from oracle.c_oracle import Oracle
+    from raytracing_rb_amd.runtime import RtxError
+    sd, cd = _pixel_scene(tmp_path, case, fillers=fillers)
+    _, status, rc = Oracle(sd, cd).render()
+    assert rc == 3
+    x, y = _first_pixel(status, 3)
+    for engine, opts in ENGINES:
+        with pytest.raises(RtxError) as e:
+            _renderer(sd, cd, engine, exact_raises=1, **opts).render()
+        assert e.value.kind == "domain", (engine, opts, str(e.value))
+        m = re.search(r"at pixel \((\d+),(\d+)\)", str(e.value))
+        assert m and (int(m.group(1)), int(m.group(2))) == (x, y), (engine, opts, str(e.value), (x, y))
+        fb = _renderer(sd, cd, engine, **opts).render()
+        assert np.isfinite(fb).all(), (engine, opts)
+    # control: without the sphere the frame renders and equals the oracle's, with the check on
+    sd2, cd2 = _pixel_scene(tmp_path, case, fillers=fillers, sphere=False)
+    ref, st2, rc2 = Oracle(sd2, cd2).render()
+    assert rc2 == 0
+    for engine, opts in ENGINES:
+        fb = _renderer(sd2, cd2, engine, exact_raises=1, **opts).render()
+        assert np.abs(fb - ref).max() <= 1e-12, (engine, opts)

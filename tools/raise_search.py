@@ -76,9 +76,11 @@ def cover_raises(C, R, T, L, radius):
     return None
 
 
-def find_sphere(T, L, radius, regime="A", side=-1.0, seed=1, tries=200000, s_range=(0.5, 3.0)):
+def find_sphere(T, L, radius, regime="A", side=-1.0, seed=1, tries=200000, s_range=(0.5, 3.0), r_range=(0.05, 0.5)):
     """A sphere (C, R) whose cover_area from T towards L raises; `side` the
-    sign of its center's position along T -> L (A only; B uses side too)."""
+    sign of its center's position along T -> L (A only; B uses side too);
+    r_range: B's radius as a fraction of the cone's r1 there (below 0.5 the
+    line misses the sphere, so its binary cover factor is 0)."""
     rng = random.Random(seed)
     lt = _sub(L, T)
     n = _r(lt)
@@ -95,7 +97,7 @@ def find_sphere(T, L, radius, regime="A", side=-1.0, seed=1, tries=200000, s_ran
             R = r1 + rng.uniform(0.05, 1.0)
             rho = R - r1
         else:
-            R = rng.uniform(0.05, 0.5) * r1
+            R = rng.uniform(*r_range) * r1
             rho = r1 - R
         C = _add(T, _add(_sc(u, s), _sc(p, rho)))
         c = cover_raises(C, R, T, L, radius)
@@ -112,19 +114,38 @@ def find_sphere(T, L, radius, regime="A", side=-1.0, seed=1, tries=200000, s_ran
 #              on the plane z = 0 (hit (0,0,0), delta (0,0,1e-5)); the light
 #              off the reflection's cone; spheres below the plane (A) or
 #              beside the cone (B).
+#   pixel_*:   T = hit + delta of one camera pixel's primary ray on the plane
+#              z = 0 (PIXEL_CAMERA, pixel (9, 5); computed with the reference's
+#              operations by tests/golden/make_raise_scenes.py, which passes it
+#              in as `pixel_T`), so a whole render raises at that pixel: behind
+#              T (A), inside the cone between T and the light with the line
+#              missing the sphere (B), beyond the light (A).
 CASES = {
     "highlight": dict(T=(0.0, 0.0, 0.0), L=(6.0, 0.5, 0.25), radius=0.8, regime="A", side=-1.0, seed=11),
     "shadow_A": dict(T=(0.0, 0.0, 1e-05), L=(3.0, 0.0, 4.0), radius=0.8, regime="A", side=-1.0, seed=12),
     "shadow_B": dict(T=(0.0, 0.0, 1e-05), L=(3.0, 0.0, 4.0), radius=2.5, regime="B", side=-1.0, seed=13,
                      s_range=(2.0, 4.0)),
+    "pixel_A_back": dict(T=None, L=(3.0, 0.0, 4.0), radius=0.8, regime="A", side=-1.0, seed=21),
+    "pixel_B_front": dict(T=None, L=(3.0, 0.0, 4.0), radius=1.5, regime="B", side=1.0, seed=22,
+                          s_range=(1.5, 4.0), r_range=(0.05, 0.45)),
+    "pixel_A_far": dict(T=None, L=(3.0, 0.0, 4.0), radius=0.8, regime="A", side=1.0, seed=23,
+                        s_range=(7.5, 9.5)),
 }
+PIXEL = (9, 5)
+PIXEL_CAMERA = dict(position=(-1.0, -4.0, 3.0), front=(1.0, 4.0, -3.0), width=24, height=16)
 
 
-def search_all():
+def search_all(pixel_T=None):
+    """Every configuration; the pixel cases need their T (pixel_T: the
+    reference-arithmetic hit + delta of PIXEL, computed by the caller)."""
     out = {}
     for name, c in CASES.items():
         kw = dict(c)
         T, L, radius = kw.pop("T"), kw.pop("L"), kw.pop("radius")
+        if T is None:
+            if pixel_T is None:
+                continue
+            T = tuple(pixel_T)
         f = find_sphere(T, L, radius, **kw)
         if f is None:
             raise RuntimeError("no raising configuration found for %s" % name)

@@ -1,0 +1,467 @@
+// walk_sim.cpp — CPU simulator of librtx's hierarchy walks (analysis tool; not
+// product code, not the oracle).  It loads a scene with the native CLI's YAML
+// loader, builds the hierarchy with the library's own host builder
+// (csrc/rtx_bvh_build.h), traces a sample of the camera's ray trees in binary64
+// (approximate shading: the ray distribution, not the pixels, is what matters
+// here) and, for every shadow ray of World#local_lights, counts the work of the
+// shadow walk under several culling rules:
+//
+//   seg       the segment walk (child boxes dilated by m S, t in [0, 1]):
+//             the exact_raises = 0 walk;
+//   cyl_sym   exact_raises as first built (r09b): boxes dilated by radius tm + mg
+//             over t in [-tm, tm], one bound tm for both nappes of the cone;
+//   cyl_asym  the same with each nappe's own bound: t in [-tb, tf], dilation
+//             radius max(tb, tf) + mg;
+//   cone_box  per child box its own dilation radius max|t| + mg (t over the
+//             box's projection on the axis), t in [-tb, tf];
+//   cone      the exact L-infinity cone test per child box (both nappes).
+//
+// Counts per shadow walk: inner nodes visited, child boxes tested, leaves
+// visited, spheres pre-tested, spheres the raise band keeps.  The nearest-hit
+// walks are counted too (seg rule with the shrinking far bound).
+//
+//   g++ -O2 -std=c++17 -o tools/walk_sim tools/walk_sim.cpp -lz
+//   tools/walk_sim scenes/c2_world.yml scenes/c2_camera.yml [stride] [max_rays_per_level]
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../raytracing_rb_amd/cli/scene_load.hpp"
+#include "../raytracing_rb_amd/csrc/rtx_bvh_build.h"
+#include "../raytracing_rb_amd/csrc/rtx_vec3.h"
+
+using namespace rtx;
+
+namespace {
+
+size_t lds_bytes(int n_nodes, int n_slots, int stack) {   // rtx_kernels.hip bvh_lds_bytes
+  return (size_t)n_nodes * sizeof(Bvh4Node) + (size_t)n_slots * 16 + (size_t)stack * 512 * 4 + 4 * 512 * 12 + 64;
+}
+
+struct Sim {
+  std::vector<rtx_object_desc> obj;
+  std::vector<rtx_light_desc> lights;
+  std::vector<Sphere64> sph64;
+  std::vector<float> sph32;
+  std::vector<int32_t> sph_obj;
+  Bvh4Builder* bb = nullptr;
+  int root = BVH_NONE;
+  float sph_scale = 0.0f;
+  float root_c[3], root_h[3];
+  float q_err = 0.0f;
+  bool q16 = false;
+  double maxd = 1e4;
+
+  void build(bool sah) {
+    for (size_t i = 0; i < obj.size(); i++) {
+      const rtx_object_desc& o = obj[i];
+      if (o.type != RTX_SPHERE) continue;
+      Sphere64 s;
+      for (int a = 0; a < 3; a++) s.c[a] = o.center[a];
+      s.r = o.radius;
+      sph64.push_back(s);
+      sph_obj.push_back((int)i);
+      for (int a = 0; a < 3; a++) sph32.push_back((float)o.center[a]);
+      sph32.push_back((float)(o.radius * o.radius));
+      const float sc = (float)((fabs(o.center[0]) + fabs(o.center[1]) + fabs(o.center[2]) + fabs(o.radius)) * (1 + 1e-6));
+      sph_scale = std::max(sph_scale, sc);
+    }
+    std::vector<BSph>* bs = new std::vector<BSph>(sph64.size());
+    for (size_t k = 0; k < sph64.size(); k++) {
+      for (int a = 0; a < 3; a++) (*bs)[k].c[a] = sph64[k].c[a];
+      (*bs)[k].r = sph64[k].r;
+      (*bs)[k].rec = (int)k;
+    }
+    const std::vector<BSph> in = *bs;
+    bb = new Bvh4Builder{*bs, sph64, sph32, sph_obj};
+    bb->sah = sah;
+    root = bs->empty() ? BVH_NONE : bb->build(0, (int)bs->size(), 0);
+    if (sah && lds_bytes((int)bb->nodes.size(), (int)bb->slot_obj.size(), bb->stack + 1) > 160 * 1024) {
+      std::vector<BSph>* b2 = new std::vector<BSph>(in);
+      Bvh4Builder* med = new Bvh4Builder{*b2, sph64, sph32, sph_obj};
+      med->sah = false;
+      const int r = med->build(0, (int)b2->size(), 0);
+      if (lds_bytes((int)med->nodes.size(), (int)med->slot_obj.size(), med->stack + 1) <= 160 * 1024) {
+        bb = med;
+        root = r;
+      }
+    }
+    const QuantLeaves ql = quantize_leaves(*bb, sph_scale);
+    q16 = ql.ok && sph64.size() > 256;        // C4-sized scenes run SPH_BVH_QLDS
+    q_err = (float)((ql.max_err + 2.0 * (double)ql.rstep) * 1.01 + 1e-9 * ql.max_r);
+    double mn[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, mx[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    for (const Sphere64& s : sph64)
+      for (int a = 0; a < 3; a++) mn[a] = std::min(mn[a], s.c[a] - s.r), mx[a] = std::max(mx[a], s.c[a] + s.r);
+    for (int a = 0; a < 3; a++) {
+      root_c[a] = (float)(0.5 * (mn[a] + mx[a]));
+      root_h[a] = (float)(std::max(mx[a] - root_c[a], root_c[a] - mn[a]) * (1 + 1e-6));
+    }
+  }
+};
+
+// ------------------------------------------------------------------ exact geometry (binary64)
+bool sphere_hit(const Sphere64& s, V3 o, V3 d, double& t_out, bool& inside) {
+  const V3 C = v3p(s.c);
+  const V3 oc = vsub(C, o);
+  const double dd = vdot(d, d);
+  const double t = vdot(oc, d) / dd;
+  const V3 np = vadd(o, vsc(d, t));
+  const double nd = vr(vsub(np, C));
+  if (!(nd <= s.r)) return false;
+  const double h = sqrt(s.r * s.r - nd * nd) / sqrt(dd);
+  inside = vr(oc) <= s.r;
+  const double th = inside ? t + h : t - h;
+  if (!inside && t < 0) return false;
+  if (th < 0) return false;
+  t_out = th;
+  return true;
+}
+
+bool plane_hit(const rtx_object_desc& p, V3 o, V3 d, double& t) {
+  const V3 F = v3p(p.front);
+  const double den = vdot(F, d);
+  if (den == 0) return false;
+  t = vdot(vsub(v3p(p.point), o), F) / den;
+  return t >= 0;
+}
+
+// ------------------------------------------------------------------ walks
+struct Stats {
+  double walks = 0, nodes = 0, tests = 0, leaves = 0, spheres = 0, band = 0, band2 = 0, band3 = 0;
+  void add(const Stats& o) {
+    walks += o.walks, nodes += o.nodes, tests += o.tests, leaves += o.leaves, spheres += o.spheres, band += o.band;
+    band2 += o.band2, band3 += o.band3;
+  }
+};
+
+enum Rule { SEG = 0, CYL_SYM, CYL_ASYM, CONE_BOX, CONE, NRULE };
+const char* rule_name[NRULE] = {"seg", "cyl_sym", "cyl_asym", "cone_box", "cone"};
+
+struct RayF {
+  float o[3], d[3], i[3], dd, Sx, mS;
+};
+
+RayF rayf(const Sim& S, V3 o, V3 d) {
+  RayF r;
+  r.o[0] = (float)o.x, r.o[1] = (float)o.y, r.o[2] = (float)o.z;
+  r.d[0] = (float)d.x, r.d[1] = (float)d.y, r.d[2] = (float)d.z;
+  r.dd = r.d[0] * r.d[0] + r.d[1] * r.d[1] + r.d[2] * r.d[2];
+  r.Sx = fabsf(r.o[0]) + fabsf(r.o[1]) + fabsf(r.o[2]) + S.sph_scale;
+  r.mS = CULL_M * r.Sx;
+  const float l1 = fabsf(r.d[0]) + fabsf(r.d[1]) + fabsf(r.d[2]), tiny = 1e-20f * l1;
+  for (int a = 0; a < 3; a++) {
+    const float e = fabsf(r.d[a]) < tiny ? copysignf(tiny, r.d[a]) : r.d[a];
+    r.i[a] = 1.0f / e;
+  }
+  return r;
+}
+
+// slab test of box (lo, hi) dilated by dil over t in [tlo, thi]; entry t or inf
+float slab(const RayF& r, const float lo[3], const float hi[3], float dil, float tlo, float thi) {
+  float tn = -INFINITY, tf = INFINITY;
+  for (int a = 0; a < 3; a++) {
+    const float t0 = (lo[a] - dil - r.o[a]) * r.i[a], t1 = (hi[a] + dil - r.o[a]) * r.i[a];
+    tn = fmaxf(tn, fminf(t0, t1));
+    tf = fminf(tf, fmaxf(t0, t1));
+  }
+  return (tn <= tf && tf >= tlo && tn <= thi) ? tn : INFINITY;
+}
+
+// the exact L-infinity cone test: some t with Q(t) within rad |t| + mg of the box on every axis
+bool cone_box_exact(const RayF& r, const float lo[3], const float hi[3], float rad, float mg) {
+  for (int nap = 0; nap < 2; nap++) {          // nap 0: t >= 0, nap 1: t <= 0 (tau = -t >= 0)
+    float lower = 0.0f, upper = INFINITY;
+    bool ok = true;
+    for (int a = 0; a < 3 && ok; a++) {
+      const float da = nap ? -r.d[a] : r.d[a];
+      // lo - mg - rad tau <= o + tau da <= hi + mg + rad tau
+      const float L = lo[a] - mg - r.o[a], H = hi[a] + mg - r.o[a];
+      const float p = da + rad, m = da - rad;  // tau p >= L, tau m <= H
+      if (p > 0) lower = fmaxf(lower, L / p);
+      else if (p < 0) upper = fminf(upper, L / p);
+      else if (L > 0) ok = false;
+      if (m > 0) upper = fminf(upper, H / m);
+      else if (m < 0) lower = fmaxf(lower, H / m);
+      else if (H < 0) ok = false;
+    }
+    if (ok && lower <= upper * (1 + 1e-5f) + 1e-30f) return true;
+  }
+  return false;
+}
+
+// nappe bounds of the cone against the spheres' box (t in [-tb, tf])
+void nappe_bounds(const Sim& S, const RayF& r, float rad, float mg, float& tb, float& tf, float& tm) {
+  tb = tf = tm = INFINITY;
+  for (int a = 0; a < 3; a++) {
+    const float ad = fabsf(r.d[a]), den = ad - rad;
+    if (!(den > 1e-5f * (ad + rad))) continue;
+    const float lo = S.root_c[a] - S.root_h[a], hi = S.root_c[a] + S.root_h[a];
+    tm = fminf(tm, (S.root_h[a] + mg + fabsf(S.root_c[a] - r.o[a])) / den);
+    const float up = (hi + mg - r.o[a]) / den, dn = (r.o[a] - lo + mg) / den;   // toward +a / -a
+    if (r.d[a] > 0) tf = fminf(tf, up), tb = fminf(tb, dn);
+    else tf = fminf(tf, dn), tb = fminf(tb, up);
+  }
+  tb = fmaxf(tb, 0.0f) * (1 + 1e-5f);
+  tf = fmaxf(tf, 0.0f) * (1 + 1e-5f);
+  tm *= 1 + 1e-5f;
+}
+
+// One shadow walk (T = o, d = L - T) under `rule`; the exact covers are not needed here.
+Stats shadow_walk(const Sim& S, V3 o, V3 d, double radius, Rule rule) {
+  Stats st;
+  st.walks = 1;
+  const RayF r = rayf(S, o, d);
+  const float rad = (float)radius, D = sqrtf(r.dd);
+  const float mg = CULL_M * r.Sx * (1.0f + rad / D) + (S.q16 ? (2.0f + rad / D) * S.q_err : 0.0f);
+  float tb, tf, tm;
+  nappe_bounds(S, r, rad, mg, tb, tf, tm);
+  float tlo = 0.0f, thi = 1.0f + 1e-5f + r.mS / D, dil = r.mS;
+  if (rule == CYL_SYM) tlo = -tm, thi = tm, dil = rad * tm + mg;
+  if (rule == CYL_ASYM || rule == CONE_BOX) tlo = -tb, thi = tf, dil = rad * std::max(tb, tf) + mg;
+  if (rule != SEG && !(std::isfinite(tm) && std::isfinite(tb) && std::isfinite(tf))) {   // every sphere
+    st.spheres = (double)S.sph64.size();
+    st.band = st.spheres;
+    return st;
+  }
+  const float kq = rad / r.dd;
+  // the band's own tolerance: 32 float32 ulps of the scene scale (the float32
+  // geometry's error is below 10), + the 16-bit records' decoding error
+  const float mgb = 32.0f * 5.96e-8f * r.Sx * (1.0f + rad / D);
+  const float mgq = mgb + (S.q16 ? (2.0f + rad / D) * S.q_err : 0.0f);
+  std::vector<int> stk;
+  if (S.root == BVH_NONE) return st;
+  stk.push_back(S.root);
+  while (!stk.empty()) {
+    const int ref = stk.back();
+    stk.pop_back();
+    if (ref >= 0) {
+      st.nodes++;
+      const Bvh4Node& n = S.bb->nodes[ref];
+      for (int k = 0; k < 4; k++) {
+        if (n.child[k] == BVH_NONE) continue;
+        st.tests++;
+        const float lo[3] = {n.lh[0][k][0], n.lh[1][k][0], n.lh[2][k][0]};
+        const float hi[3] = {n.lh[0][k][1], n.lh[1][k][1], n.lh[2][k][1]};
+        bool want;
+        if (rule == CONE) {
+          want = cone_box_exact(r, lo, hi, rad, mg) || slab(r, lo, hi, r.mS, 0.0f, 1.0f + 1e-5f + r.mS / D) < INFINITY;
+        } else if (rule == CONE_BOX) {
+          float t0 = 0.0f, t1 = 0.0f;          // the box's projection on the axis (in t)
+          for (int a = 0; a < 3; a++) {
+            const float p = (lo[a] - r.o[a]) * r.d[a] / r.dd, q = (hi[a] - r.o[a]) * r.d[a] / r.dd;
+            t0 += fminf(p, q), t1 += fmaxf(p, q);
+          }
+          const float dl = rad * fmaxf(fabsf(t0), fabsf(t1)) + mg;
+          want = slab(r, lo, hi, dl, tlo, thi) < INFINITY;
+        } else {
+          want = slab(r, lo, hi, dil, tlo, thi) < INFINITY;
+        }
+        if (want) stk.push_back(n.child[k]);
+      }
+    } else {
+      st.leaves++;
+      const int v = ~ref, slot0 = (v >> 2) * BVH_LEAF, cnt = (v & 3) + 1;
+      for (int u = 0; u < cnt; u++) {
+        st.spheres++;
+        if (rule == SEG) continue;
+        const float* c = &S.bb->slot32[(size_t)(v >> 2) * 16];
+        const float ox = c[u] - r.o[0], oy = c[4 + u] - r.o[1], oz = c[8 + u] - r.o[2];
+        const float sq = ox * ox + oy * oy + oz * oz, q = ox * r.d[0] + oy * r.d[1] + oz * r.d[2];
+        const float l = sq * r.dd - q * q, R = sqrtf(c[12 + u]);
+        const float t = fabsf(R - kq * fabsf(q));
+        auto band = [&](float w) {
+          const float lo = fmaxf(t - w, 0.0f), hi = t + w;
+          const float e = 4e-6f * (sq + hi * hi) * r.dd;
+          return l >= lo * lo * r.dd - e && l <= hi * hi * r.dd + e;
+        };
+        if (band(mg)) st.band++;             // (r09b's band: the box dilation's mg)
+        if (band(mgq)) st.band2++;           // 32 ulps (+ the 16-bit decoding error)
+        if (band(mgb)) st.band3++;           // 32 ulps on float32 records
+      }
+      (void)slot0;
+    }
+  }
+  return st;
+}
+
+// nearest hit over every object (binary64; spheres through the hierarchy, counted)
+int nearest(const Sim& S, V3 o, V3 d, double& best_t, bool& inside, Stats& st) {
+  st.walks++;
+  int besti = -1;
+  best_t = INFINITY;
+  for (size_t i = 0; i < S.obj.size(); i++) {
+    if (S.obj[i].type != RTX_PLANE) continue;
+    double t;
+    if (plane_hit(S.obj[i], o, d, t) && t < best_t && vr(vsc(d, t)) < S.maxd) best_t = t, besti = (int)i, inside = false;
+  }
+  if (S.root == BVH_NONE) return besti;
+  const RayF r = rayf(S, o, d);
+  std::vector<int> stk{S.root};
+  while (!stk.empty()) {
+    const int ref = stk.back();
+    stk.pop_back();
+    const float thi = std::isfinite(best_t) ? (float)(best_t * (1 + 1e-6)) : INFINITY;
+    if (ref >= 0) {
+      st.nodes++;
+      const Bvh4Node& n = S.bb->nodes[ref];
+      for (int k = 0; k < 4; k++) {
+        if (n.child[k] == BVH_NONE) continue;
+        st.tests++;
+        const float lo[3] = {n.lh[0][k][0], n.lh[1][k][0], n.lh[2][k][0]};
+        const float hi[3] = {n.lh[0][k][1], n.lh[1][k][1], n.lh[2][k][1]};
+        if (slab(r, lo, hi, r.mS, 0.0f, thi) < INFINITY) stk.push_back(n.child[k]);
+      }
+    } else {
+      st.leaves++;
+      const int v = ~ref, slot0 = (v >> 2) * BVH_LEAF, cnt = (v & 3) + 1;
+      for (int u = 0; u < cnt; u++) {
+        st.spheres++;
+        double t;
+        bool in;
+        if (sphere_hit(S.bb->slot64[slot0 + u], o, d, t, in) && t < best_t) {
+          best_t = t, besti = S.bb->slot_obj[slot0 + u], inside = in;
+        }
+      }
+    }
+  }
+  return besti;
+}
+
+struct Ray {
+  V3 o, d, att;
+  int depth;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s world.yml camera.yml [stride] [max_rays_per_level]\n", argv[0]);
+    return 2;
+  }
+  const int stride = argc > 3 ? atoi(argv[3]) : 8;
+  const size_t cap = argc > 4 ? (size_t)atoll(argv[4]) : 200000;
+  rtxcli::Scene sc;
+  rtxcli::load_world(argv[1], sc);
+  const rtx_camera_desc cam = rtxcli::load_camera(argv[2]);
+  Sim S;
+  S.obj = sc.objects;
+  S.lights = sc.lights;
+  S.maxd = sc.desc.max_distance;
+  S.build(true);
+  printf("scene: %zu spheres, %zu nodes, %zu slots, stack %d, q16 %d, q_err %.3g, sph_scale %.3g\n", S.sph64.size(),
+         S.bb->nodes.size(), S.bb->slot_obj.size(), S.bb->stack + 1, (int)S.q16, S.q_err, S.sph_scale);
+  // camera rays (pinhole through the pixel centers of every stride-th pixel; lens jitter ignored)
+  const V3 pos = v3p(cam.position), front = v3p(cam.front), up = v3p(cam.up);
+  uint32_t e = 0;
+  const V3 left = vnorm(vcross(up, front), e), upn = vnorm(up, e), fn = vnorm(front, e);
+  std::vector<Ray> level;
+  for (int y = 0; y < cam.height; y += stride)
+    for (int x = 0; x < cam.width; x += stride) {
+      const double u = 2.0 * ((double)x / cam.width - 0.5) * cam.retina_width;
+      const double w = 2.0 * ((double)y / cam.height - 0.5) * cam.retina_height;
+      const V3 dir = vadd(vsc(fn, cam.image_distance), vadd(vsc(left, -u), vsc(upn, -w)));
+      level.push_back(Ray{pos, dir, v3(1, 1, 1), cam.trace_depth});
+    }
+  std::mt19937_64 rng(1);
+  Stats tot_sh[NRULE], tot_ext;
+  for (int lev = 0; lev < cam.trace_depth && !level.empty(); lev++) {
+    if (level.size() > cap) {                   // a uniform subsample of the level
+      std::vector<Ray> sub;
+      const double step = (double)level.size() / cap;
+      for (size_t k = 0; k < cap; k++) sub.push_back(level[(size_t)(k * step)]);
+      level.swap(sub);
+    }
+    Stats sh[NRULE], ext;
+    size_t hits = 0;
+    std::vector<Ray> next;
+    for (const Ray& ray : level) {
+      double t;
+      bool inside = false;
+      const int oi = nearest(S, ray.o, ray.d, t, inside, ext);
+      if (oi < 0) continue;
+      hits++;
+      const rtx_object_desc& ob = S.obj[oi];
+      const V3 hit = vadd(ray.o, vsc(ray.d, t));
+      V3 n, delta;
+      if (ob.type == RTX_SPHERE) {
+        const V3 C = v3p(ob.center);
+        n = inside ? vsub(C, hit) : vsub(hit, C);
+        delta = vsc(vsub(hit, C), 1e-5 * (inside ? -1.0 : 1.0));
+      } else {
+        n = v3p(ob.front);
+        if (vdot(n, ray.d) > 0) n = vneg(n);
+        delta = vsc(n, 1e-5);
+      }
+      const V3 T = vadd(hit, delta);
+      int nl = 0;
+      for (const rtx_light_desc& L : S.lights) {
+        const V3 lt = vsub(v3p(L.position), T);
+        for (int rr = 0; rr < NRULE; rr++) sh[rr].add(shadow_walk(S, T, lt, L.radius, (Rule)rr));
+        // lit unless a sphere or plane crosses the segment (approximate local_lights)
+        bool blocked = false;
+        for (size_t i = 0; i < S.obj.size() && !blocked; i++) {
+          double tt;
+          bool in;
+          if (S.obj[i].type == RTX_SPHERE) {
+            Sphere64 s;
+            for (int a = 0; a < 3; a++) s.c[a] = S.obj[i].center[a];
+            s.r = S.obj[i].radius;
+            if (S.sph64.size() > 256) continue;     // (C4: skip the brute-force occlusion estimate)
+            blocked = sphere_hit(s, T, lt, tt, in) && tt < 1.0;
+          }
+        }
+        if (!blocked) nl++;
+      }
+      if (ray.depth - 1 <= 0) continue;
+      const V3 nn = vnorm(n, e);
+      const V3 dn = vnorm(ray.d, e);
+      const V3 ra = vmul(ray.att, v3p(ob.reflective_attenuation));
+      if (vr(ra) >= 1e-4) {
+        const V3 rd = vsub(dn, vsc(nn, 2.0 * vdot(dn, nn)));
+        next.push_back(Ray{T, rd, ra, ray.depth - 1});
+      }
+      const V3 fa = vmul(ray.att, v3p(ob.refractive_attenuation));
+      if (ob.type == RTX_SPHERE && vr(fa) >= 1e-4) {
+        const double eta = inside ? ob.refractive_rate : 1.0 / ob.refractive_rate;
+        const double ci = -vdot(dn, nn), k = 1 - eta * eta * (1 - ci * ci);
+        if (k >= 0) {
+          const V3 td = vadd(vsc(dn, eta), vsc(nn, eta * ci - sqrt(k)));
+          next.push_back(Ray{vsub(hit, vsc(nn, 1e-5)), td, fa, ray.depth - 1});
+        }
+      }
+      if (nl == 0 && cam.monte_carlo_diffusion_times > 0) {
+        std::uniform_real_distribution<double> U(0, 1);
+        for (int k = 0; k < cam.monte_carlo_diffusion_times; k++) {
+          V3 dir = v3(U(rng) - 0.5, U(rng) - 0.5, U(rng) - 0.5);
+          if (vdot(dir, nn) < 0) dir = vneg(dir);
+          const V3 pa = vmul(ray.att, vsc(v3p(ob.diffuse_rate), 1.0 / cam.monte_carlo_diffusion_times));
+          if (vr(pa) >= 1e-4) next.push_back(Ray{T, dir, pa, ray.depth - 1});
+        }
+      }
+    }
+    printf("level %d: rays %zu, hits %zu\n", lev, level.size(), hits);
+    printf("  extend   per walk: nodes %6.2f tests %6.2f leaves %6.2f spheres %6.2f\n", ext.nodes / ext.walks,
+           ext.tests / ext.walks, ext.leaves / ext.walks, ext.spheres / ext.walks);
+    for (int rr = 0; rr < NRULE; rr++)
+      printf("  %-8s per walk: nodes %6.2f tests %6.2f leaves %6.2f spheres %6.2f band %8.5f\n", rule_name[rr],
+             sh[rr].nodes / sh[rr].walks, sh[rr].tests / sh[rr].walks, sh[rr].leaves / sh[rr].walks,
+             sh[rr].spheres / sh[rr].walks, sh[rr].band / sh[rr].walks);
+    for (int rr = 0; rr < NRULE; rr++) tot_sh[rr].add(sh[rr]);
+    tot_ext.add(ext);
+    level.swap(next);
+  }
+  printf("all levels:\n  extend   per walk: nodes %6.2f tests %6.2f leaves %6.2f spheres %6.2f\n",
+         tot_ext.nodes / tot_ext.walks, tot_ext.tests / tot_ext.walks, tot_ext.leaves / tot_ext.walks,
+         tot_ext.spheres / tot_ext.walks);
+  for (int rr = 0; rr < NRULE; rr++)
+    printf("  %-8s per walk: nodes %6.2f tests %6.2f leaves %6.2f spheres %6.2f band %8.5f %8.5f %8.5f (x seg leaves %.2f)\n",
+           rule_name[rr], tot_sh[rr].nodes / tot_sh[rr].walks, tot_sh[rr].tests / tot_sh[rr].walks,
+           tot_sh[rr].leaves / tot_sh[rr].walks, tot_sh[rr].spheres / tot_sh[rr].walks,
+           tot_sh[rr].band / tot_sh[rr].walks, tot_sh[rr].band2 / tot_sh[rr].walks, tot_sh[rr].band3 / tot_sh[rr].walks,
+           tot_sh[rr].leaves / tot_sh[SEG].leaves);
+  return 0;
+}
