@@ -37,12 +37,13 @@ def build_cli(force=False, verbose=False):
     if not force and os.path.exists(CLI_OUT) and all(
             os.path.getmtime(p) <= os.path.getmtime(CLI_OUT) for p in CLI_DEPS + [OUT]):
         return CLI_OUT
-    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", CLI_OUT + ".tmp", CLI_SRC, "-L" + HERE, "-l:librtx.so",
+    tmp = "%s.%d.tmp" % (CLI_OUT, os.getpid())   # (parallel test workers may rebuild it at once)
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", tmp, CLI_SRC, "-L" + HERE, "-l:librtx.so",
            "-lz", "-lpthread", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(CLI_OUT + ".tmp", CLI_OUT)
+    os.replace(tmp, CLI_OUT)
     return CLI_OUT
 
 
