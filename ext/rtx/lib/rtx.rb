@@ -72,6 +72,9 @@ module RTX
   extern 'int rtx_render_tile_list_device(void*, void*, int, int, unsigned long long, void*, void*)'
   extern 'int rtx_tile_rays(void*, void*, int)'
   extern 'int rtx_render_multi(void*, int, int, unsigned long long, void*, size_t)'
+  extern 'int rtx_render_multi_plan(void*, int, int, void*, int, unsigned long long, void*, size_t)'
+  extern 'int rtx_tile_probe(void*, void*, int)'
+  extern 'int rtx_lpt_plan(void*, int, int, void*, int, void*)'
   extern 'int rtx_device_count()'
   extern 'int rtx_sync(void*, void*)'
   extern 'int rtx_render_at(void*, int, int, unsigned long long, void*)'

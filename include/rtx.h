@@ -221,6 +221,31 @@ rtx_status rtx_render_tiles(rtx_context* ctx, int32_t tile_rows, int32_t rank, i
 rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, uint64_t seed,
                             double* out_rgb, size_t row_stride);
 
+/* rtx_render_multi with an explicit split (camera.rb:53-65's bands replaced by
+ * cost-balanced tile lists): rank k renders the tiles plan[k * per_rank ..
+ * k * per_rank + per_rank) (rtx_render_tile_list_device; an index past the
+ * image bottom is padding), the packed lists are gathered the same way and
+ * unpacked by the plan.  Every tile must appear in exactly one list
+ * (RTX_EINVAL otherwise).  Same bits as rtx_render. */
+rtx_status rtx_render_multi_plan(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, const int32_t* plan,
+                                 int32_t per_rank, uint64_t seed, double* out_rgb, size_t row_stride);
+
+/* A cheap work map without rendering: per 8x8 tile of the frame (row-major,
+ * ceil(width/8) x ceil(height/8)) the weight of 4 probe rays (sample 0's lens
+ * rays at the quadrant centres, one nearest-hit walk each: 1 per hit, +1
+ * reflective, +3 refractive material; the expensive-tiles-first class of the
+ * lanes engine).  Synchronous. */
+rtx_status rtx_tile_probe(rtx_context* ctx, int64_t* out, int32_t n);
+
+/* Longest-processing-time split of n_tiles tiles (costs[t]) over nranks:
+ * tiles by decreasing cost (ties: lower index), each to the rank with the
+ * least total so far (ties: fewer tiles, lower rank); every list ascending and
+ * padded to one width with n_tiles.  *per_rank = that width; plan (nranks x
+ * width, rank-major, cap >= width entries per rank) may be NULL to query it.
+ * Host-only, deterministic (raytracing_rb_amd/tiles.py lpt_plan). */
+rtx_status rtx_lpt_plan(const int64_t* costs, int32_t n_tiles, int32_t nranks, int32_t* plan, int32_t cap,
+                        int32_t* per_rank);
+
 /* Number of HIP devices visible to this process (the node's GPUs). */
 int32_t    rtx_device_count(void);
 

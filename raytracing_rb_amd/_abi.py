@@ -88,6 +88,9 @@ SIGNATURES = [
     ("rtx_render_tile_list_device", _I, [_P, C.POINTER(C.c_int32), _I, _I, _U64, _P, _P]),
     ("rtx_tile_rays", _I, [_P, C.POINTER(C.c_int64), _I]),
     ("rtx_render_multi", _I, [C.POINTER(_P), _I, _I, _U64, _DP, _SZ]),
+    ("rtx_render_multi_plan", _I, [C.POINTER(_P), _I, _I, C.POINTER(C.c_int32), _I, _U64, _DP, _SZ]),
+    ("rtx_tile_probe", _I, [_P, C.POINTER(C.c_int64), _I]),
+    ("rtx_lpt_plan", _I, [C.POINTER(C.c_int64), _I, _I, C.POINTER(C.c_int32), _I, C.POINTER(C.c_int32)]),
     ("rtx_device_count", _I, []),
     ("rtx_sync", _I, [_P, _P]),
     ("rtx_render_at", _I, [_P, _I, _I, _U64, _DP]),

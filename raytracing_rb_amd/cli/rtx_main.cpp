@@ -3,9 +3,11 @@
 //   rtx s  out.png world.yml camera.yml      Camera#render_sync  (main.rb:17-18)
 //   rtx N  out.png world.yml camera.yml      Camera#render_fork with N workers
 //                                             (main.rb:19-21): the frame's 8-row
-//                                             tiles dealt round-robin to N workers
-//                                             over the node's GPUs (one librtx
-//                                             context per worker thread)
+//                                             tiles split over N workers on the
+//                                             node's GPUs (one librtx context per
+//                                             worker): round-robin, or from 8
+//                                             workers cost-balanced lists (LPT over
+//                                             rtx_tile_probe's work map)
 // options:
 //   --seed S             RNG seed (main.rb:10 seeds Random with 1; default 1)
 //   --device D           first GPU (default 0)
@@ -13,6 +15,8 @@
 //   --remap old=new      texture path substitution (a missing reference texture)
 //   --float-out F        also write the float64 framebuffer (H*W*3 doubles, rows top-down)
 //   --no-blend           plain array_to_color bytes (no png-gem Color#blend over black)
+//   --balance B          rtx N's split: rr (round-robin tiles), lpt (tile lists by the
+//                        probe's costs), auto (lpt from 8 workers, the default)
 //   --dump-scene         print the scene/camera descriptors as JSON and exit (no GPU)
 //   --decode-png P       print W, H and an FNV-1a hash of P's RGB8 decode and exit (no GPU)
 //
@@ -43,6 +47,7 @@ struct Opts {
   uint64_t seed = 1;
   int device = 0;
   bool blend = true, dump = false;
+  std::string balance = "auto";
   std::map<std::string, double> set;
   std::map<std::string, std::string> remap;
   std::map<std::string, long long> opt;          // --option key=value: rtx_set_option
@@ -130,10 +135,10 @@ rtx_context* make_context(int device, const Scene& sc, const rtx_camera_desc& ca
   return c;
 }
 
-// Camera#render_fork (camera.rb:41-68): worker k of n renders the tiles t
-// with t % n == k on GPU (device + k) % ngpu; rtx_render_multi gathers the
-// packed tiles to the first worker's GPU with one RCCL send/recv group (device
-// copies when workers share a GPU) and returns the frame.
+// Camera#render_fork (camera.rb:41-68): worker k of n renders its tiles on GPU
+// (device + k) % ngpu (round-robin t % n == k, or an LPT list); the packed
+// tiles are gathered to the first worker's GPU with one RCCL send/recv group
+// (device copies when workers share a GPU) and the frame returned.
 std::vector<double> render_fork(const Opts& o, const Scene& sc, const rtx_camera_desc& cam, int n) {
   const int W = cam.width, H = cam.height;
   const int ngpu = rtx_device_count();
@@ -143,7 +148,23 @@ std::vector<double> render_fork(const Opts& o, const Scene& sc, const rtx_camera
   for (int k = 0; k < n; k++)
     for (const auto& kv : o.opt) check(ctx[k], rtx_set_option(ctx[k], kv.first.c_str(), kv.second), "option");
   std::vector<double> fb((size_t)W * H * 3);
-  const rtx_status s = rtx_render_multi(ctx.data(), n, TILE_ROWS, o.seed, fb.data(), (size_t)W * 3);
+  rtx_status s;
+  if (o.balance == "lpt" || (o.balance == "auto" && n >= 8)) {
+    // cost-balanced tile lists: the probe's work map (no render), summed per
+    // 8-row tile (= one row of 8x8 tiles), longest processing time first
+    const int tx = (W + 7) / 8, ty = (H + 7) / 8;
+    std::vector<int64_t> probe((size_t)tx * ty), cost(ty, 0);
+    check(ctx[0], rtx_tile_probe(ctx[0], probe.data(), (int32_t)probe.size()), "tile probe");
+    for (int y = 0; y < ty; y++)
+      for (int x = 0; x < tx; x++) cost[y] += probe[(size_t)y * tx + x];
+    int32_t per = 0;
+    check(ctx[0], rtx_lpt_plan(cost.data(), ty, n, nullptr, 0, &per), "lpt plan");
+    std::vector<int32_t> plan((size_t)n * per);
+    check(ctx[0], rtx_lpt_plan(cost.data(), ty, n, plan.data(), per, &per), "lpt plan");
+    s = rtx_render_multi_plan(ctx.data(), n, TILE_ROWS, plan.data(), per, o.seed, fb.data(), (size_t)W * 3);
+  } else {
+    s = rtx_render_multi(ctx.data(), n, TILE_ROWS, o.seed, fb.data(), (size_t)W * 3);
+  }
   if (s) die(std::string("render_fork: ") + rtx_status_string(s) + " (" + rtx_last_error(ctx[0]) + ")");
   for (rtx_context* c : ctx) rtx_context_destroy(c);
   return fb;
@@ -168,6 +189,10 @@ Opts parse_args(int argc, char** argv) {
     else if (a == "--device") o.device = atoi(val().c_str());
     else if (a == "--float-out") o.float_out = val();
     else if (a == "--no-blend") o.blend = false;
+    else if (a == "--balance") {
+      o.balance = val();
+      if (o.balance != "rr" && o.balance != "lpt" && o.balance != "auto") die("--balance must be rr, lpt or auto");
+    }
     else if (a == "--dump-scene") o.dump = true;
     else if (a == "--decode-png") o.decode_png = val();
     else if (a == "--set") {

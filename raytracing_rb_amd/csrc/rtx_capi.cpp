@@ -1193,11 +1193,15 @@ static rtx_status grow(rtx_context* c, double** buf, size_t* cap, size_t bytes) 
   return RTX_OK;
 }
 
-rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, uint64_t seed, double* out,
-                            size_t row_stride) {
+// rtx_render_multi / rtx_render_multi_plan: plan == nullptr deals the tiles
+// round-robin, else rank k renders the list plan[k * per_rank .. + per_rank).
+static rtx_status render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, const int32_t* plan,
+                               int32_t per_rank, uint64_t seed, double* out, size_t row_stride) {
   if (!ctxs || n < 1 || !ctxs[0]) return RTX_EINVAL;
   rtx_context* c0 = ctxs[0];
   if (!out || tile_rows <= 0) return fail(c0, RTX_EINVAL, "bad arguments");
+  if (plan && (per_rank < 1 || (int64_t)per_rank * tile_rows > INT32_MAX / 2))
+    return fail(c0, RTX_EINVAL, "bad plan: %d tiles per rank", per_rank);
   std::vector<int> devs(n);
   for (int k = 0; k < n; k++) {
     rtx_context* c = ctxs[k];
@@ -1208,7 +1212,23 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
   }
   const int W = c0->cam.width, H = c0->cam.height;
   if (row_stride < (size_t)W * 3) return fail(c0, RTX_EINVAL, "row_stride too small");
-  const int R = rtx_tiles_rows_per_rank(H, tile_rows, n);
+  const int ntiles = (H + tile_rows - 1) / tile_rows;
+  std::vector<int32_t> pl;                                     // the plan, padding clamped to ntiles
+  if (plan) {
+    pl.assign(plan, plan + (size_t)n * per_rank);
+    std::vector<char> seen(ntiles, 0);
+    for (int32_t& t : pl) {
+      if (t < 0) return fail(c0, RTX_EINVAL, "plan: negative tile index %d", t);
+      if (t >= ntiles) {
+        t = ntiles;
+        continue;
+      }
+      if (seen[t]++) return fail(c0, RTX_EINVAL, "plan: tile %d listed twice", t);
+    }
+    for (int t = 0; t < ntiles; t++)
+      if (!seen[t]) return fail(c0, RTX_EINVAL, "plan: tile %d in no rank's list", t);
+  }
+  const int R = plan ? per_rank * tile_rows : rtx_tiles_rows_per_rank(H, tile_rows, n);
   const size_t count = (size_t)R * W * 3;                      // doubles per rank
   // clear stale device errors (as rtx_render: unsynced raises of earlier
   // asynchronous calls on these contexts are discarded, include/rtx.h)
@@ -1218,14 +1238,21 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
     rtx_context* c = ctxs[k];
     HIPCHK(c0, hipSetDevice(c->device));
     rtx_status s = grow(c, &c->d_multi, &c->multi_bytes, count * sizeof(double));
-    if (!s) s = rtx_render_tiles_device(c, tile_rows, k, n, seed, c->d_multi, nullptr);
+    if (!s)
+      s = plan ? rtx_render_tile_list_device(c, pl.data() + (size_t)k * per_rank, per_rank, tile_rows, seed,
+                                             c->d_multi, nullptr)
+               : rtx_render_tiles_device(c, tile_rows, k, n, seed, c->d_multi, nullptr);
     if (s) return fail(c0, s, "rank %d: %s", k, rtx_last_error(c));
   }
   HIPCHK(c0, hipSetDevice(c0->device));
-  rtx_status s = grow(c0, &c0->d_gather, &c0->gather_bytes, ((size_t)n * count + (size_t)W * H * 3) * sizeof(double));
+  const size_t plan_dbl = plan ? ((size_t)n * per_rank * sizeof(int32_t) + 7) / 8 : 0;
+  rtx_status s = grow(c0, &c0->d_gather, &c0->gather_bytes,
+                      ((size_t)n * count + (size_t)W * H * 3 + plan_dbl) * sizeof(double));
   if (s) return s;
   double* gathered = c0->d_gather;
   double* frame = c0->d_gather + (size_t)n * count;
+  int32_t* d_plan = plan ? reinterpret_cast<int32_t*>(frame + (size_t)W * H * 3) : nullptr;
+  if (plan) HIPCHK(c0, hipMemcpy(d_plan, pl.data(), pl.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   bool distinct = true;
   for (int a = 0; a < n; a++)
     for (int b = a + 1; b < n; b++) distinct = distinct && devs[a] != devs[b];
@@ -1288,7 +1315,8 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
     }
   }
   HIPCHK(c0, hipSetDevice(devs[0]));
-  HIPCHK(c0, launch_unpack(gathered, W, H, tile_rows, n, R, frame, (size_t)W * 3, nullptr));
+  HIPCHK(c0, plan ? launch_unpack_plan(gathered, W, H, tile_rows, n, per_rank, d_plan, frame, (size_t)W * 3, nullptr)
+                  : launch_unpack(gathered, W, H, tile_rows, n, R, frame, (size_t)W * 3, nullptr));
   HIPCHK(c0, hipMemcpy2D(out, row_stride * sizeof(double), frame, (size_t)W * 3 * sizeof(double),
                          (size_t)W * 3 * sizeof(double), H, hipMemcpyDeviceToHost));
   // the ranks' reference raises, merged: the first in render_sync order over
@@ -1319,6 +1347,68 @@ rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_ro
 int32_t rtx_device_count(void) {
   int n = 0;
   return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+rtx_status rtx_render_multi(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, uint64_t seed, double* out,
+                            size_t row_stride) {
+  return render_multi(ctxs, n, tile_rows, nullptr, 0, seed, out, row_stride);
+}
+
+rtx_status rtx_render_multi_plan(rtx_context* const* ctxs, int32_t n, int32_t tile_rows, const int32_t* plan,
+                                 int32_t per_rank, uint64_t seed, double* out, size_t row_stride) {
+  if (!plan) return ctxs && n > 0 && ctxs[0] ? fail(ctxs[0], RTX_EINVAL, "null plan") : RTX_EINVAL;
+  return render_multi(ctxs, n, tile_rows, plan, per_rank, seed, out, row_stride);
+}
+
+rtx_status rtx_tile_probe(rtx_context* c, int64_t* out, int32_t n) {
+  if (!c || n < 0 || (n > 0 && !out)) return fail(c, RTX_EINVAL, "bad arguments");
+  KParams p;
+  rtx_status s = prep(c, p, 1);
+  if (s) return s;
+  HIPCHK(c, hipSetDevice(c->device));
+  p.x0 = 0;
+  p.nx = c->cam.width;
+  p.y0 = 0;
+  p.nrows = c->cam.height;
+  p.tile_rows = 0;
+  const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
+  int32_t* d = nullptr;
+  HIPCHK(c, hipMalloc(&d, (size_t)std::max(1, tiles) * sizeof(int32_t)));
+  std::vector<int32_t> v(tiles);
+  hipError_t e = launch_tile_probe(p, d, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(v.data(), d, (size_t)tiles * sizeof(int32_t), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  HIPCHK(c, e);
+  for (int k = 0; k < n; k++) out[k] = k < tiles ? (int64_t)v[k] : 0;
+  return RTX_OK;
+}
+
+rtx_status rtx_lpt_plan(const int64_t* costs, int32_t n_tiles, int32_t nranks, int32_t* plan, int32_t cap,
+                        int32_t* per_rank) {
+  if (n_tiles < 0 || nranks < 1 || (n_tiles > 0 && !costs) || !per_rank) return RTX_EINVAL;
+  std::vector<int32_t> order(n_tiles);
+  for (int32_t t = 0; t < n_tiles; t++) order[t] = t;
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return costs[a] > costs[b]; });
+  std::vector<int64_t> load(nranks, 0);
+  std::vector<std::vector<int32_t>> lists(nranks);
+  for (int32_t t : order) {                     // to the least-loaded rank (ties: fewer tiles, lower rank)
+    int r = 0;
+    for (int k = 1; k < nranks; k++)
+      if (load[k] < load[r] || (load[k] == load[r] && lists[k].size() < lists[r].size())) r = k;
+    lists[r].push_back(t);
+    load[r] += costs[t];
+  }
+  size_t width = 0;
+  for (auto& l : lists) {
+    std::sort(l.begin(), l.end());
+    width = std::max(width, l.size());
+  }
+  *per_rank = (int32_t)width;
+  if (!plan) return RTX_OK;                     // (a query of the width)
+  if ((size_t)cap < width) return RTX_EINVAL;
+  for (int k = 0; k < nranks; k++)
+    for (size_t j = 0; j < width; j++) plan[(size_t)k * width + j] = j < lists[k].size() ? lists[k][j] : n_tiles;
+  return RTX_OK;
 }
 
 rtx_status rtx_render_at(rtx_context* c, int32_t x, int32_t y, uint64_t seed, double rgb[3]) {

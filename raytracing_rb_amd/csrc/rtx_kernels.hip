@@ -630,6 +630,21 @@ __global__ void k_unpack(const double* __restrict__ gathered, int w, int h, int 
   out[(size_t)y * stride + (i - (long)src_row * per_row)] = gathered[i];
 }
 
+// The same for tile lists (rtx_render_multi_plan): rank k's packed row r is
+// image row plan[k * per_rank + r / tile_rows] * tile_rows + r % tile_rows.
+__global__ void k_unpack_plan(const double* __restrict__ gathered, int w, int h, int tile_rows, int n, int per_rank,
+                              const int32_t* __restrict__ plan, double* __restrict__ out, size_t stride) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per_row = (long)w * 3;
+  const int rows_per_rank = per_rank * tile_rows;
+  if (i >= (long)n * rows_per_rank * per_row) return;
+  const int src_row = (int)(i / per_row);
+  const int k = src_row / rows_per_rank, r = src_row - k * rows_per_rank;
+  const long y = (long)plan[k * per_rank + r / tile_rows] * tile_rows + r % tile_rows;
+  if (y >= h) return;                              // padding tiles (index past the bottom)
+  out[(size_t)y * stride + (i - (long)src_row * per_row)] = gathered[i];
+}
+
 // Camera#array_to_color (camera.rb:153-156) + PNG::Canvas#point over black.
 __global__ void k_quantize(const double* __restrict__ rgb, int w, int h, size_t stride, int blend,
                            uint8_t* __restrict__ out) {
@@ -883,6 +898,24 @@ hipError_t launch_unpack(const double* gathered, int w, int h, int tile_rows, in
   if (total == 0) return hipSuccess;
   hipLaunchKernelGGL(k_unpack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, gathered, w, h, tile_rows, n,
                      rows_per_rank, out, stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_plan(const double* gathered, int w, int h, int tile_rows, int n, int per_rank,
+                              const int32_t* d_plan, double* out, size_t stride, hipStream_t s) {
+  const long total = (long)n * per_rank * tile_rows * w * 3;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_plan, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, gathered, w, h, tile_rows,
+                     n, per_rank, d_plan, out, stride);
+  return hipGetLastError();
+}
+
+// The k_tile_cost probe over a whole frame (rtx_tile_probe): the class of every
+// 8x8 tile into cls (device, one int per tile).
+hipError_t launch_tile_probe(KParams p, int32_t* cls, hipStream_t s) {
+  const int tiles = ((p.nx + 7) / 8) * ((p.nrows + 7) / 8);
+  if (tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tile_cost, dim3((unsigned)((tiles * 4 + 255) / 256)), dim3(256), 0, s, p, cls);
   return hipGetLastError();
 }
 

@@ -201,5 +201,8 @@ hipError_t launch_quantize(const double* rgb, int w, int h, size_t stride, int b
 // Rank-major packed tiles (n ranks x rows_per_rank rows x w x 3) -> frame rows.
 hipError_t launch_unpack(const double* gathered, int w, int h, int tile_rows, int n, int rows_per_rank,
                          double* out, size_t stride, hipStream_t s);
+hipError_t launch_unpack_plan(const double* gathered, int w, int h, int tile_rows, int n, int per_rank,
+                              const int32_t* d_plan, double* out, size_t stride, hipStream_t s);
+hipError_t launch_tile_probe(KParams p, int32_t* cls, hipStream_t s);
 
 }  // namespace rtx

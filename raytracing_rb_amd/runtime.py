@@ -132,6 +132,13 @@ class Renderer:
                                                          tile_rows, seed, C.c_void_p(d_packed),
                                                          C.c_void_p(stream or 0)))
 
+    def tile_probe(self):
+        """Probe weights per 8x8 tile [ceil(H/8), ceil(W/8)] without rendering (rtx_tile_probe)."""
+        tx, ty = (self.width + 7) // 8, (self.height + 7) // 8
+        out = np.zeros(tx * ty, np.int64)
+        self._check(self.lib.rtx_tile_probe(self.h, out.ctypes.data_as(C.POINTER(C.c_int64)), len(out)))
+        return out.reshape(ty, tx)
+
     def tile_rays(self):
         """Rays per 8x8 tile [ceil(H/8), ceil(W/8)] of the last whole-frame level render (rtx_tile_rays)."""
         ty, tx = (self.height + 7) // 8, (self.width + 7) // 8
@@ -198,6 +205,41 @@ def render_multi(renderers, tile_rows=8, seed=1):
     return out
 
 
+def render_multi_plan(renderers, plan, tile_rows=8, seed=1):
+    """render_multi with explicit tile lists (rtx_render_multi_plan): plan[k] is
+    renderer k's list of tile_rows-row tiles (equal lengths, padded past the
+    bottom, e.g. tiles.lpt_plan).  Returns the float64 frame [H, W, 3]."""
+    if not renderers or len(plan) != len(renderers):
+        raise ValueError("one tile list per renderer")
+    lib = load_library()
+    r0 = renderers[0]
+    per = len(plan[0])
+    flat = np.ascontiguousarray(np.asarray(plan, np.int32).reshape(-1))
+    hs = (C.c_void_p * len(renderers))(*[r.h.value for r in renderers])
+    out = np.empty((r0.height, r0.width, 3), np.float64)
+    st = lib.rtx_render_multi_plan(hs, len(renderers), tile_rows, flat.ctypes.data_as(C.POINTER(C.c_int32)), per,
+                                   seed, _dp(out), r0.width * 3)
+    if st:
+        raise RtxError(st, lib.rtx_last_error(r0.h).decode())
+    return out
+
+
+def lpt_plan_native(costs, nranks):
+    """rtx_lpt_plan (host C++): the same plan as tiles.lpt_plan."""
+    lib = load_library()
+    c = np.ascontiguousarray(np.asarray(costs, np.int64))
+    per = C.c_int32(0)
+    st = lib.rtx_lpt_plan(c.ctypes.data_as(C.POINTER(C.c_int64)), len(c), nranks, None, 0, C.byref(per))
+    if st:
+        raise RtxError(st, "rtx_lpt_plan failed")
+    out = np.zeros(nranks * per.value, np.int32)
+    st = lib.rtx_lpt_plan(c.ctypes.data_as(C.POINTER(C.c_int64)), len(c), nranks,
+                          out.ctypes.data_as(C.POINTER(C.c_int32)), per.value, C.byref(per))
+    if st:
+        raise RtxError(st, "rtx_lpt_plan failed")
+    return [list(map(int, out[k * per.value:(k + 1) * per.value])) for k in range(nranks)]
+
+
 def device_count():
     return load_library().rtx_device_count()
 
@@ -218,4 +260,5 @@ def vec3_lib():
     return load_library()
 
 
-__all__ = ["Renderer", "RtxError", "quantize", "render_multi", "device_count", "_abi"]
+__all__ = ["Renderer", "RtxError", "quantize", "render_multi", "render_multi_plan", "lpt_plan_native", "device_count",
+           "_abi"]

@@ -168,15 +168,16 @@ def test_cli_png_decoder_formats(cli, tmp_path, mode, bits):
 # ------------------------------------------------------------------ GPU
 @pytest.mark.gpu
 def test_cli_render_matches_python_api(gpu, cli, tmp_path):
-    """`rtx s` and `rtx 3` (three workers) render the frame the Python API renders,
+    """`rtx s`, `rtx 3` (three workers, round-robin tiles or LPT lists) and `rtx 8`
+    (LPT lists by the probe's costs) render the frame the Python API renders,
     bit for bit, and write the same PNG bytes."""
     from raytracing_rb_amd.api import Camera, World
     w, c = os.path.join(SCENES, "mix_world.yml"), os.path.join(SCENES, "mix_camera.yml")
     cam = Camera(World(w), c, width=40, height=23)
     fb = cam.render_sync(str(tmp_path / "py.png"))
-    for mode in ("s", "3"):
+    for mode, extra in (("s", []), ("3", []), ("3", ["--balance", "lpt"]), ("8", [])):   # 8 workers: LPT lists
         out, raw = str(tmp_path / ("cli_%s.png" % mode)), str(tmp_path / ("cli_%s.f64" % mode))
-        r = subprocess.run([cli, mode, out, w, c, "--set", "width=40", "--set", "height=23", "--float-out", raw],
+        r = subprocess.run([cli, mode, out, w, c, "--set", "width=40", "--set", "height=23", "--float-out", raw] + extra,
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
         got = np.fromfile(raw, np.float64).reshape(fb.shape)

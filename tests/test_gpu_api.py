@@ -90,3 +90,35 @@ def test_render_multi_rccl_gather_matches_render(gpu):
     rs3 = [Renderer(sd, cd, device=k % n) for k in range(3)]
     got3 = render_multi(rs3, tile_rows=5, seed=4)
     assert np.array_equal(got3.view(np.uint64), full.view(np.uint64))
+
+
+def test_render_multi_plan_lpt_matches_render(gpu):
+    """rtx_render_multi_plan (ADVICE / VERDICT r04 item 8): LPT tile lists from
+    the measured rays (rtx_tile_rays) and from the probe (rtx_tile_probe, no
+    render) for 3 contexts on one device (the device-copy gather) and one per
+    visible GPU (RCCL): every frame bit-identical to rtx_render; a plan that
+    lists a tile twice or omits one is refused."""
+    from raytracing_rb_amd import config
+    from raytracing_rb_amd.runtime import Renderer, RtxError, device_count, lpt_plan_native, render_multi_plan
+    from raytracing_rb_amd.tiles import lpt_plan, row_tile_costs
+    sd, cd = config.load_scene(os.path.join(SCENES, "c2_world.yml"), os.path.join(SCENES, "c2_camera.yml"),
+                               camera_overrides=dict(width=200, height=77))
+    n = device_count()
+    r0 = Renderer(sd, cd, device=0)
+    full = r0.render(seed=4)
+    rays = row_tile_costs(r0.tile_rays(), 8)
+    probe = r0.tile_probe().sum(axis=1)
+    assert probe.shape == rays.shape and (probe > 0).any()
+    for ranks in (3, n):
+        rs = [Renderer(sd, cd, device=k % n) for k in range(ranks)]
+        for costs in (rays, probe):
+            plan = lpt_plan(costs, ranks)
+            assert lpt_plan_native(costs, ranks) == plan
+            got = render_multi_plan(rs, plan, tile_rows=8, seed=4)
+            assert np.array_equal(got.view(np.uint64), full.view(np.uint64)), (ranks, list(costs))
+    rs = [Renderer(sd, cd, device=k % n) for k in range(3)]
+    plan = lpt_plan(rays, 3)
+    bad = [list(l) for l in plan]
+    bad[1][0] = bad[0][0]                               # listed twice (and one tile in no list)
+    with pytest.raises(RtxError):
+        render_multi_plan(rs, bad, tile_rows=8, seed=4)

@@ -406,3 +406,15 @@ def test_library_is_the_build_of_this_tree():
     from raytracing_rb_amd import _abi, _build
     lib = _abi.load_library()
     assert lib.rtx_build_id().decode() == _build.source_sha()
+
+
+def test_native_lpt_plan_matches_python():
+    """rtx_lpt_plan (host C++, used by the CLI's `rtx N`) == tiles.lpt_plan,
+    ties included (equal costs, zeros, more ranks than tiles)."""
+    from raytracing_rb_amd.runtime import lpt_plan_native
+    from raytracing_rb_amd.tiles import lpt_plan
+    rs = np.random.RandomState(3)
+    for n_tiles, ranks in ((135, 8), (136, 8), (23, 3), (5, 8), (1, 1), (64, 2)):
+        for costs in (rs.randint(0, 1000, n_tiles), np.full(n_tiles, 7), rs.randint(0, 3, n_tiles)):
+            assert lpt_plan_native(costs, ranks) == lpt_plan(costs, ranks), (n_tiles, ranks)
+
