@@ -590,10 +590,13 @@ __device__ __forceinline__ float slab_key(const NR& node, int k, const SlabRay& 
 // direction on a) + mg, so for every axis with |d_a| > radius: t <= tf going
 // towards the light, -t <= tb going away from it.  The child boxes are then
 // slab-tested dilated by radius max(tb, tf) + mg over t in [-tb, tf], which
-// holds the segment's own boxes (t in [0, 1], dilated by m S <= mg).  False
+// holds the segment's own boxes (t in [0, 1], dilated by m S <= mg).  ok false
 // when no finite bound exists (the caller walks every sphere).
-__device__ __forceinline__ bool xr_setup(const SceneDev& S, SlabRay& s, double radius, float& tlo, float& thi) {
-  if (!s.fin) return false;
+__device__ __forceinline__ SlabRay xr_setup(const SceneDev& S, const SlabRay& s0, double radius, float& tlo,
+                                            float& thi, bool& ok) {
+  SlabRay s = s0;
+  ok = false;
+  if (!s.fin) return s;
   const float rad = (float)radius;
   const float mg = CULL_M * s.Sx * (1.0f + rad * __builtin_amdgcn_rsqf(s.dd));   // (node boxes are exact: no decoding error)
   float tf = __builtin_inff(), tb = __builtin_inff();
@@ -610,7 +613,7 @@ __device__ __forceinline__ bool xr_setup(const SceneDev& S, SlabRay& s, double r
   }
   tf = fmaxf(tf, 0.0f) * (1.0f + 1e-5f);
   tb = fmaxf(tb, 0.0f) * (1.0f + 1e-5f);
-  if (!(tf < 1e30f && tb < 1e30f)) return false;
+  if (!(tf < 1e30f && tb < 1e30f)) return s;
   const float r = __builtin_fmaf(rad, fmaxf(tf, tb), mg) * (1.0f + 1e-5f);   // >= m S: the covers' dilation too
   const float ix = s.pix.x, iy = s.piy.x, iz = s.piz.x;
   s.pax = F2{-((s.ox + r) * ix), -((s.ox - r) * ix)};
@@ -618,7 +621,8 @@ __device__ __forceinline__ bool xr_setup(const SceneDev& S, SlabRay& s, double r
   s.paz = F2{-((s.oz + r) * iz), -((s.oz - r) * iz)};
   tlo = -tb;
   thi = tf;
-  return __builtin_isfinite(r);
+  ok = __builtin_isfinite(r);
+  return s;
 }
 
 // Planes and boxes first, in run order (their order does not matter either).
@@ -794,16 +798,18 @@ __device__ __forceinline__ bool query_bvh(const SceneDev& S, NP nodes, LP leaf4,
   const double r2 = r * r;                        // front.r2
   V3 dn = d;
   if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r); // front.normalize (same bits as the walk)
-  SlabRay s = slab_setup(S, o, d);
+  const SlabRay s0 = slab_setup(S, o, d);
   xr = xr && !ext;                                // exact_raises: the shadow walk also checks the raises
   constexpr bool Q16 = std::is_same<LP, QLeaf>::value;   // 16-bit leaf records: their decoding error
   const float rf = (float)r;
   // ray parameter range: EXTEND [0, the current best hit], SHADOW [0, the light]; with
   // exact_raises the cone bound [-tm, tm] (xr_setup), the child boxes dilated to its radius
   float tlo = 0.0f;
-  float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + s.mS / rf;
+  float thi = ext ? (float)(best / r * (1.0 + 1e-6)) : 1.0f + 1e-5f + s0.mS / rf;
+  bool xok = true;
+  const SlabRay s = xr ? xr_setup(S, s0, radius, tlo, thi, xok) : s0;
   // A non-finite or zero ray makes no cull (comparisons would be unordered).
-  if (!s.fin || (xr && !xr_setup(S, s, radius, tlo, thi))) {
+  if (!s.fin || !xok) {
     // no float32 cull is valid for this ray: the ordered linear walk (same result)
     if (!ext) total = 1.0;
     query<false>(S, cptr(S.sph32), ext, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr, xr);
