@@ -109,31 +109,6 @@ __device__ __forceinline__ void lv_hl_defer(const KParams& p, bool want, const R
   q[3] = make_double2(__builtin_bit_cast(double, (uint64_t)rec), 0.0);
 }
 
-// The same check inline (RTX_HL_INLINE, the default): the firing lane runs
-// lit_area(ray.position, light.position, radius)'s own walk with the raise
-// check of exact_raises (its covers' penumbras and the factor-0 band,
-// rtx_device.h xr_band) in the level kernel, on its own LDS stack and cover
-// list (no walk of the lane is in flight before its nearest-hit walk).  With
-// the band filter that walk is short, so no list and no k_hl_raise launch.
-#ifndef RTX_HL_INLINE
-#define RTX_HL_INLINE 1
-#endif
-template <int SPH, int BS>
-__device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V3 o, V3 d, V3 L, double rad,
-                                        double& best, int& besti, V3& hit, bool& hin, double& total, uint32_t& err,
-                                        bool xr);
-
-template <int SPH, int BS>
-__device__ __forceinline__ bool lv_lit_area_raises(const KParams& p, char* lds, V3 T, V3 L, double rad) {
-  double tot = 1.0, b2 = 0.0;
-  int bi2 = -1;
-  V3 h2 = T;
-  bool in2 = true;
-  uint32_t e2 = 0;
-  lv_walk<SPH, BS>(p, lds, false, T, vsub(L, T), L, rad, b2, bi2, h2, in2, tot, e2, true);
-  return (e2 & 0xffu) != 0;
-}
-
 // root: the level-0 item of the ray's tree; (x, y, sample): its RNG key.
 __device__ __forceinline__ void lv_store_ray(const KParams& p, double* dst, const Ray& r, V3 att, uint64_t path,
                                              int root, int x, int y, int sample) {
@@ -673,8 +648,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
         leafp[3 * nleaf + 1] = c.y;
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
-      }, errA, [&](V3 T, V3 Lp, double rad) {     // lit_area's raise: inline, or deferred to k_hl_raise
-        if (RTX_HL_INLINE) return lv_lit_area_raises<SPH, BS>(p, lds, T, Lp, rad);
+      }, errA, [&](V3, V3, double) {              // lit_area's raise: deferred to k_hl_raise
         hl_defer = true;
         return false;
       });
@@ -864,8 +838,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
             leafp[3 * nleaf + 1] = c.y;
             leafp[3 * nleaf + 2] = c.z;
             nleaf++;
-          }, errA, [&](V3 T, V3 Lp, double rad) {     // lit_area's raise: inline, or deferred to k_hl_raise
-        if (RTX_HL_INLINE) return lv_lit_area_raises<SPH, BS>(p, lds, T, Lp, rad);
+          }, errA, [&](V3, V3, double) {              // lit_area's raise: deferred to k_hl_raise
         hl_defer = true;
         return false;
       });
@@ -1101,8 +1074,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
         leafp[3 * nleaf + 1] = c.y;
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
-      }, errA, [&](V3 T, V3 Lp, double rad) {     // lit_area's raise: inline, or deferred to k_hl_raise
-        if (RTX_HL_INLINE) return lv_lit_area_raises<SPH, BS>(p, lds, T, Lp, rad);
+      }, errA, [&](V3, V3, double) {              // lit_area's raise: deferred to k_hl_raise
         hl_defer = true;
         return false;
       });
@@ -1835,7 +1807,7 @@ static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_ma
       e = launch_level_mode(q, mode, 2, d, hits * q.scene.n_light, s, kev);
     if (e == hipSuccess) e = launch_shade(q, d, hits, s, kev);
   }
-  if (e == hipSuccess && !RTX_HL_INLINE) e = launch_hl_raise(q, s);
+  if (e == hipSuccess) e = launch_hl_raise(q, s);
   if (e == hipSuccess) e = launch_redo(q, mode, maxs, n0_max, s);
   if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
   return e;

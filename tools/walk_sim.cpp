@@ -337,6 +337,7 @@ struct Ray {
 
 }  // namespace
 
+#ifndef WALK_SIM_NO_MAIN
 int main(int argc, char** argv) {
   if (argc < 3) {
     fprintf(stderr, "usage: %s world.yml camera.yml [stride] [max_rays_per_level]\n", argv[0]);
@@ -465,3 +466,4 @@ int main(int argc, char** argv) {
            tot_sh[rr].leaves / tot_sh[SEG].leaves);
   return 0;
 }
+#endif  // WALK_SIM_NO_MAIN
