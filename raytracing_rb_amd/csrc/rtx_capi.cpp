@@ -92,6 +92,7 @@ struct rtx_context {
   int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
   int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also check the acos raises of the covers they skip
                                      // (C2 +10 %, C4 +108 %, r09c; so not the default)
+  int64_t opt_lv_sort = 0;           // bounce levels: 1 = levels >= 1 visited bin by bin (direction octant, origin cell)
   int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
@@ -261,7 +262,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
       {"lv_redo_blocks", c->opt_lv_redo_blocks},
       {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
-      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}};
+      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_sort", c->opt_lv_sort}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -353,6 +354,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "exact_raises")) {      // every shadow walk also checks the skipped covers' acos raises
     if (value != 0 && value != 1) return fail(c, RTX_EINVAL, "exact_raises must be 0 or 1");
     c->opt_exact_raises = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_sort")) {           // bounce levels: bin each level's rays before its launch (same bits)
+    if (value != 0 && value != 1) return fail(c, RTX_EINVAL, "lv_sort must be 0 or 1");
+    c->opt_lv_sort = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_ray_bytes")) {      // bounce levels: staged ray record size (0 auto)
@@ -804,13 +810,19 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   const size_t hcap = (size_t)LV_SLICES << hlog2;
   const size_t sz_hit = split ? al256(hcap * LV_HIT_BYTES) : 0,
                sz_area = split ? al256(hcap * (size_t)std::max(1, c->scene.n_light) * 16) : 0;
+  // ray binning (lv_sort, fused levels only): a bin per staged slot, the
+  // level's bin list, the bin counts and cursors
+  const bool sort = c->opt_lv_sort != 0 && !split;
+  const size_t sz_key = sort ? al256(scap * 2) : 0, sz_perm = sort ? al256(scap * 8) : 0,
+               sz_bins = sort ? al256((size_t)LV_BINS * 8) : 0;
   // One buffer set per part: with lv_streams = P the region's tiles are
   // rendered in P interleaved parts at once, parts 1.. on the context's aux
   // streams (one part's level tails, launch gaps and reductions overlap the
   // others' levels).  The extra-sample list and the statistics are shared
   // (appended / added atomically); each part has its own level buffers, its
   // own lanes-engine work counter and ray stacks for its overflow re-render.
-  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq;
+  const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_key +
+                     sz_perm + sz_bins;
   const size_t total = parts * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
@@ -827,6 +839,10 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_area = split ? (double*)q : nullptr; q += sz_area;
     k.lv_hlq = (double*)q;                    q += sz_hlq;
     k.lv_hlq_cap = (uint32_t)hlcap;
+    k.lv_key = sort ? (uint16_t*)q : nullptr;      q += sz_key;
+    k.lv_perm = sort ? (uint2*)q : nullptr;        q += sz_perm;
+    k.lv_bins = sort ? (uint32_t*)q : nullptr;     q += sz_bins;
+    k.lv_sort = sort ? 1 : 0;
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;

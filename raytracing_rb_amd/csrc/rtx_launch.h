@@ -24,6 +24,7 @@ constexpr int LV_MAXL = 64;                     // levels (= trace_depth) the en
 constexpr int LV_SLICES = 64;                   // slices per queue (one per lane of a consumer wave)
 constexpr int LV_CLAIMS = 16;                   // sharded chunk-claim counters per launch
 constexpr int LV_DONE = 16;                     // wave-completion counters per level launch (lv_level_done)
+constexpr int LV_BINS = 4096;                   // ray bins (option lv_sort): 8 direction octants x 512 origin cells
 struct LevelCtl {
   uint32_t count0;                              // level-0 items of the batch
   uint32_t redo_n;                              // level-0 items handed to the lanes engine (capacity overflow)
@@ -112,6 +113,13 @@ struct KParams {
   int32_t exact_raises;            // 1: every shadow walk (local_lights) also checks its covers' acos raises (option exact_raises)
   uint32_t lv_hlq_cap;             // entries of lv_hlq
   double* lv_hlq;                  // highlight rays of the batch whose lit_area raise k_hl_raise checks (8 doubles each)
+  // ray binning (option lv_sort): a level >= 1 is processed in the order of its
+  // rays' bins (lv_ray_bin: direction octant, origin cell), records still at
+  // their dense index
+  int32_t lv_sort;                 // 1: bin levels >= 1 before their launch
+  uint16_t* lv_key;                // bin of each staged ray of the level being binned, by queue slot (k_lv_bin)
+  uint2* lv_perm;                  // the level's rays in bin order: {queue slot, dense index}
+  uint32_t* lv_bins;               // LV_BINS counts, LV_BINS cursors
 };
 
 // Where the sphere walk reads its records:

@@ -224,6 +224,54 @@ __device__ __forceinline__ void lv_in_queue(const KParams& p, int level, LvQueue
   q.chunks = (uint32_t)__shfl((int)q.cin, 63);
 }
 
+// Ray binning (option lv_sort).  A level >= 1 holds its rays
+// in the order their parents were shaded, so a wave's 64 rays start from
+// scattered points in all directions and its lanes walk different parts of the
+// hierarchy.  With lv_sort the producer tags every staged ray with a bin: the
+// octant of its direction and the cell of its origin in an 8 x 8 x 8 grid over
+// the spheres' box (Morton order): before the level's launch k_lv_bin (count:
+// each staged ray's bin) / k_lv_bin_scan / k_lv_bin (scatter), one
+// counting-sort pass, list the level's rays bin by bin, and the level takes its
+// chunks from that list.  (The bins are computed there, not by the producer:
+// one more live value in k_level_c's shading spilled registers.)  Only the visiting order changes: every ray writes its record at its
+// dense index and allocates its children as before, so the trees, hence the
+// frames, are bit-identical (order independence, §3.7).
+__device__ __forceinline__ uint32_t lv_ray_bin(const SceneDev& S, const Ray& r) {
+  const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
+  uint32_t m = 0;
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    const float lo = S.root_c[a] - S.root_h[a];
+    const float f = (o[a] - lo) * (4.0f / fmaxf(S.root_h[a], 1e-30f));   // 8 cells over 2 h
+    const uint32_t c = (uint32_t)fminf(fmaxf(f, 0.0f), 7.0f);            // (NaN: cell 0)
+    m |= ((c & 1u) | (c & 2u) << 2 | (c & 4u) << 4) << a;
+  }
+  const uint32_t oct = (r.d.x < 0 ? 1u : 0u) | (r.d.y < 0 ? 2u : 0u) | (r.d.z < 0 ? 4u : 0u);
+  return oct << 9 | m;
+}
+
+// The level's chunks, and chunk c's ray for this lane: its queue slot and
+// dense index (binned: from the bin list; else the slices).  All lanes call it.
+__device__ __forceinline__ uint32_t lv_chunks(const KParams& p, const LvQueue& in, int level) {
+  return level > 0 && p.lv_sort ? (in.total + 63u) >> 6 : in.chunks;
+}
+__device__ __forceinline__ bool lv_chunk_item(const KParams& p, const LvQueue& in, int level, uint32_t c,
+                                              uint32_t& slot, uint32_t& i) {
+  if (level > 0 && p.lv_sort) {
+    const uint32_t k = c * 64u + (uint32_t)__lane_id();
+    slot = i = 0;
+    if (k >= in.total) return false;
+    const uint2 e = p.lv_perm[k];
+    slot = e.x;
+    i = e.y;
+    return true;
+  }
+  uint32_t s, off;
+  const bool a = in.item(c, s, off, i);
+  slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
+  return a;
+}
+
 // The end of a launch that allocated level e's rays (k_level, k_level_c,
 // k_lv_shade of level e - 1): the grid's last wave to finish writes level e's
 // compact layout: per slice the ray count (clamped to the slice), the
@@ -613,20 +661,21 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
     t0 = t1;             \
   }
   uint32_t chunk;
-  while (sched.claim(in.chunks, chunk)) {
+  const uint32_t nch = lv_chunks(p, in, level);
+  while (sched.claim(nch, chunk)) {
     if (RTX_STAMPS) {
       t0 = stamp();
       nchunks++;
     }
-    uint32_t s, off, i;
-    bool active = in.item(chunk, s, off, i);  // i: the ray's dense index in the level
+    uint32_t slot, i;
+    bool active = lv_chunk_item(p, in, level, chunk, slot, i);   // i: the ray's dense index in the level
     // ---- the ray: a camera sample (level 0) or a staged child
     Item cur;
     int root = 0, x = 0, y = 0, sample = 0;
     bool alive = false;
     if (active) {
       bool valid;
-      lv_ray(p, level, level == 0 ? i : (s << p.lv_slice_log2) + off, cur, root, x, y, sample, valid);
+      lv_ray(p, level, slot, cur, root, x, y, sample, valid);
       if (level == 0) p.lv_redo_of[i] = -1;   // no overflow yet (lv_redo)
       active = valid;                         // tile padding: no record
       alive = valid && (level > 0 || !(depth <= 0 || vr(cur.att) < 0.0001));   // rt_map's cutoff (ray_tracer.rb:52)
@@ -778,6 +827,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   double* ring = reinterpret_cast<double*>(lds + p.lds_ring + (threadIdx.x >> 6) * ((size_t)LV_RING * RF * 8));
   uint32_t head = 0, pend = 0;                // wave-uniform: first parked slot, parked hits
   bool got = true;
+  const uint32_t nch = lv_chunks(p, in, level);
 
   unsigned long long tS[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1, nchunks = 0;   // RTX_STAMPS diagnostic build only
   unsigned long long nA = 0, nE = 0, nS = 0;
@@ -790,14 +840,13 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   while (true) {
     {                                         // first half, chunk by chunk, until 64 hits are parked
       uint32_t chunk = 0;
-      if (got) got = sched.claim(in.chunks, chunk);   // (never again once exhausted)
+      if (got) got = sched.claim(nch, chunk);   // (never again once exhausted)
       if (RTX_STAMPS) t0 = stamp();
       if (got) {
         if (RTX_STAMPS) nchunks++;
         // ---- first half: the ray, rt_map's cutoff, highlights, World#intersect
-        uint32_t s, off, i;
-        bool active = in.item(chunk, s, off, i);
-        const uint32_t slot = level == 0 ? i : (s << p.lv_slice_log2) + off;
+        uint32_t slot, i;
+        bool active = lv_chunk_item(p, in, level, chunk, slot, i);
         // A staged child's first half needs its origin and direction only: the
         // attenuation is read if a highlight fires, the root if the ray
         // overflows the record arena (the second half reloads the rest), so
@@ -1592,10 +1641,86 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
     (&p.lv_ctl->sc[0][0])[w] = 0;
     (&p.lv_ctl->sh[0][0])[w] = 0;
   }
+  if (p.lv_sort)
+    for (int w = t; w < LV_BINS; w += nt) p.lv_bins[w] = 0;   // (k_lv_bin_scan zeroes them after each level)
   const int cwords = (nlev < LV_MAXL + 1 ? nlev : LV_MAXL + 1) * LV_CLAIMS * 32;
   for (int w = t; w < cwords; w += nt)
     for (int k = 0; k < 3; k++) (&p.lv_ctl->claim[k][0][0])[w] = 0;
 }
+
+// ----------------------------------------------------------------- ray binning
+// One counting-sort pass over a level's rays by bin (option lv_sort; lv_ray_bin
+// above): counts (and each ray's bin into lv_key), exclusive prefix, scatter
+// into lv_perm.  The count and the
+// scatter walk the level's chunks like its launch does (LvQueue), one wave per
+// chunk, and add a wave's rays bin by bin: one atomic per distinct bin of the
+// chunk (a level's chunks hold few: children of neighbouring parents).  The
+// order inside a bin is the atomics' order, which cannot change a result.
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void k_lv_bin(KParams p, int level) {
+  LvQueue in;
+  lv_in_queue(p, level, in);
+  const uint32_t W = gridDim.x * 4u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
+  uint16_t* key = p.lv_key;
+  uint32_t* ctr = p.lv_bins + (SCATTER ? LV_BINS : 0);
+  const uint64_t below = (1ull << __lane_id()) - 1ull;
+  for (uint32_t c = w; c < in.chunks; c += W) {
+    uint32_t s, off, i;
+    bool todo = in.item(c, s, off, i);
+    const uint32_t slot = (s << p.lv_slice_log2) + off;
+    uint32_t b = 0;
+    if (todo && SCATTER) {
+      b = key[slot];
+    } else if (todo) {                        // the staged ray's bin (its origin and direction)
+      const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
+      const double2 a = q[0], bb = q[1], cc = q[2];
+      Ray r;
+      r.o = v3(a.x, a.y, bb.x);
+      r.d = v3(bb.y, cc.x, cc.y);
+      b = lv_ray_bin(p.scene, r);
+      key[slot] = (uint16_t)b;
+    }
+    while (true) {
+      const uint64_t m = __ballot(todo);
+      if (!m) break;
+      const int lead = __builtin_ctzll(m);
+      const uint32_t lb = (uint32_t)__shfl((int)b, lead);
+      const uint64_t same = __ballot(todo && b == lb);
+      uint32_t at = 0;
+      if ((int)__lane_id() == lead) at = atomicAdd(&ctr[lb], (uint32_t)__popcll(same));
+      if (SCATTER) {
+        at = (uint32_t)__shfl((int)at, lead);
+        if (todo && b == lb) p.lv_perm[at + (uint32_t)__popcll(same & below)] = make_uint2(slot, i);
+      }
+      if (todo && b == lb) todo = false;
+    }
+  }
+}
+
+// The bins' exclusive prefix into the cursors; the counts zeroed for the next
+// level.  One workgroup of 1024 threads, 4 bins each.
+__global__ __launch_bounds__(1024) void k_lv_bin_scan(KParams p, int level) {
+  __shared__ uint32_t part[16];
+  const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[k] = p.lv_bins[4 * t + k];
+    sum += v[k];
+  }
+  const uint32_t incl = wave_scan_incl(sum);
+  if (lane == 63) part[wv] = incl;
+  __syncthreads();
+  uint32_t pre = incl - sum;
+  for (int k = 0; k < wv; k++) pre += part[k];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    p.lv_bins[LV_BINS + 4 * t + k] = pre;
+    p.lv_bins[4 * t + k] = 0u;
+    pre += v[k];
+  }
+}
+static_assert(LV_BINS == 4 * 1024, "k_lv_bin_scan: 4 bins per thread");
 
 // Diagnostic builds: this unit's stamps (k_level), added by rtxdbg_read_stamps.
 int read_level_stamps(unsigned long long* out, int reset) {
@@ -1753,6 +1878,19 @@ static hipError_t launch_shade(const KParams& p, int level, long cap_items, hipS
                       0, s, kev, p, level);
 }
 
+// A level's binning (option lv_sort): count, prefix, scatter; grids sized for
+// the level's capacity (cap rays), at most 8 workgroups per CU.
+static hipError_t launch_bins(const KParams& q, int level, long cap, hipStream_t s) {
+  int cus = 0, per_cu = 0;
+  const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(k_lv_bin<false>), 256, 0, cus, per_cu);
+  if (e != hipSuccess) return e;
+  const long grid = std::max<long>(1, std::min<long>((cap / 64 + 3) / 4, (long)cus * 8));
+  hipLaunchKernelGGL(k_lv_bin<false>, dim3((unsigned)grid), dim3(256), 0, s, q, level);
+  hipLaunchKernelGGL(k_lv_bin_scan, dim3(1), dim3(1024), 0, s, q, level);
+  hipLaunchKernelGGL(k_lv_bin<true>, dim3((unsigned)grid), dim3(256), 0, s, q, level);
+  return hipGetLastError();
+}
+
 template <int SD>
 static hipError_t launch_finalize_sd(const KParams& q, int nlev, int n, hipStream_t s) {
   const size_t stack = (size_t)nlev * 64 * 4 + (SD > 16 ? 0 : (size_t)SD * 2 * 256 * 4);
@@ -1798,7 +1936,8 @@ static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_ma
   for (int d = 0; d < nlev && e == hipSuccess; d++) {
     const long cap = d == 0 ? (long)n0_max : scap;
     if (!q.lv_split) {
-      e = launch_level_mode(q, mode, 0, d, cap, s, kev);
+      if (d > 0 && q.lv_sort) e = launch_bins(q, d, cap, s);
+      if (e == hipSuccess) e = launch_level_mode(q, mode, 0, d, cap, s, kev);
       continue;
     }
     const long hits = std::min(cap, hcap);

@@ -690,3 +690,48 @@ def test_grid_stride_reduction_changes_no_bit(gpu, world, camera, ov):
             r = _renderer(sd, cd, 1, lv_fin_grid=k, lv_streams=1, **opts)
             assert _same(r.render(seed=4), lanes), (k, opts)
             r.close()
+
+
+# ---- ray binning (option lv_sort: levels >= 1 visited bin by bin, records at their dense index)
+@pytest.mark.parametrize("world,camera,ov", SCENES_SMALL)
+def test_binned_levels_bit_identical(gpu, world, camera, ov):
+    sd, cd = _scene(world, camera, **ov)
+    lanes = _renderer(sd, cd, 0).render(seed=3)
+    for opts in (dict(), dict(lv_compact=0), dict(lv_compact=2), dict(lv_streams=1)):
+        r = _renderer(sd, cd, 1, lv_sort=1, **opts)
+        assert r.get_option("lv_sort") == 1
+        assert _same(r.render(seed=3), lanes), opts
+
+
+@pytest.mark.parametrize("opts", [
+    dict(lv_batch=512),
+    dict(lv_stage_pct=5, lv_floor=0),                    # staging overflow (clamped slices) + re-render
+    dict(lv_rec_pct=101, lv_floor=0),
+    dict(lv_static=0),                                   # every chunk claimed
+    dict(lv_split=1),                                    # split phases: lv_sort has no effect there
+])
+def test_binned_levels_batches_overflow_schedule(gpu, opts):
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
+    lanes = _renderer(sd, cd, 0).render(seed=5)
+    r = _renderer(sd, cd, 1, lv_sort=1, **opts)
+    assert _same(r.render(seed=5), lanes)
+    if "lv_stage_pct" in opts:
+        assert r.level_stats()["redo"] > 0
+
+
+def test_binned_levels_c4_and_c2_full_frame(gpu):
+    """Binning on the C4 hierarchy (16-bit leaves, compact ring) and on C2 at
+    full size: the same frame as without it."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_scenes
+    make_scenes.ensure_c4()
+    sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=192, height=108, pre_sample_times=2, max_sample_times=2)
+    plain = _renderer(sd, cd, 1).render(seed=4)
+    assert _same(_renderer(sd, cd, 1, lv_sort=1).render(seed=4), plain)
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml")
+    plain = _renderer(sd, cd, 1).render()
+    r = _renderer(sd, cd, 1, lv_sort=1)
+    assert _same(r.render(), plain)
+    st = r.level_stats()
+    assert st["redo"] == 0 and st["dropped"] == 0

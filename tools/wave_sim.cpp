@@ -227,23 +227,41 @@ uint32_t spread10(uint32_t x) {
   return x;
 }
 
-enum Order { BASE = 0, OCT, MORTON, OCTM, NORDER };
-const char* order_name[NORDER] = {"base", "oct", "morton", "octm"};
+enum Order { BASE = 0, OCT, MORTON, OCTM, W128, W256, W512, W4096, M6, M9, M12, O_M6, O_M9, NORDER };
+const char* order_name[NORDER] = {"base", "oct", "morton", "octm", "w128", "w256", "w512", "w4096",
+                                  "m6", "m9", "m12", "o+m6", "o+m9"};
 
+// the key of a ray: (direction octant, Morton code of the origin in the scene box)
+uint32_t ray_key(const Sim& S, const WRay& r, bool oct_only, bool morton_only) {
+  const uint32_t oct = (r.d.x < 0) | ((r.d.y < 0) << 1) | ((r.d.z < 0) << 2);
+  uint32_t m = 0;
+  const double p[3] = {r.o.x, r.o.y, r.o.z};
+  for (int a = 0; a < 3; a++) {
+    const double lo = S.root_c[a] - S.root_h[a], w = 2.0 * S.root_h[a];
+    const double f = std::min(std::max((p[a] - lo) / w, 0.0), 0.999999);
+    m |= spread10((uint32_t)(f * 1024)) << a;
+  }
+  return oct_only ? oct : morton_only ? m : (oct << 29) | (m >> 3);
+}
+
+// whole-level orders, coarse buckets (mN, o+mN), or (wN) the octant-Morton sort inside consecutive windows
+// of N rays (what a wave or workgroup could sort of the chunks it takes)
 void order_level(const Sim& S, std::vector<WRay>& lv, Order ord) {
   if (ord == BASE) return;
   for (WRay& r : lv) {
-    const uint32_t oct = (r.d.x < 0) | ((r.d.y < 0) << 1) | ((r.d.z < 0) << 2);
-    uint32_t m = 0;
-    const double p[3] = {r.o.x, r.o.y, r.o.z};
-    for (int a = 0; a < 3; a++) {
-      const double lo = S.root_c[a] - S.root_h[a], w = 2.0 * S.root_h[a];
-      const double f = std::min(std::max((p[a] - lo) / w, 0.0), 0.999999);
-      m |= spread10((uint32_t)(f * 1024)) << a;
-    }
-    r.key = ord == OCT ? oct : ord == MORTON ? m : (oct << 29) | (m >> 3);
+    r.key = ray_key(S, r, ord == OCT, ord == MORTON || (ord >= M6 && ord <= M12));
+    // coarse buckets (one counting-sort pass; stable = arrival order inside a bucket):
+    // the top 6 / 9 / 12 Morton bits of the origin, with or without the octant
+    if (ord == M6) r.key >>= 24;
+    if (ord == M9) r.key >>= 21;
+    if (ord == M12) r.key >>= 18;
+    if (ord == O_M6) r.key >>= 23;
+    if (ord == O_M9) r.key >>= 20;
   }
-  std::stable_sort(lv.begin(), lv.end(), [](const WRay& a, const WRay& b) { return a.key < b.key; });
+  const size_t win = ord == W128 ? 128 : ord == W256 ? 256 : ord == W512 ? 512 : ord == W4096 ? 4096 : lv.size();
+  for (size_t a = 0; a < lv.size(); a += win)
+    std::stable_sort(lv.begin() + a, lv.begin() + std::min(lv.size(), a + win),
+                     [](const WRay& x, const WRay& y) { return x.key < y.key; });
 }
 
 }  // namespace
@@ -253,7 +271,11 @@ int main(int argc, char** argv) {
     fprintf(stderr, "usage: %s world.yml camera.yml [tile_step] [max_rays_per_level]\n", argv[0]);
     return 2;
   }
+  // tile_step > 0: every tile_step-th tile of the frame; < 0: the dense block of
+  // -tile_step x -tile_step tiles at the frame's centre (ray density as in a full frame)
   const int tstep = argc > 3 ? atoi(argv[3]) : 16;
+  const bool only_spec = getenv("WAVE_SIM_SPEC_ONLY") != nullptr;
+  const int nwalk = only_spec ? 1 : NWALK;
   const size_t cap = argc > 4 ? (size_t)atoll(argv[4]) : 400000;
   rtxcli::Scene sc;
   rtxcli::load_world(argv[1], sc);
@@ -273,7 +295,15 @@ int main(int argc, char** argv) {
   // level 0: every tstep-th 8x8 tile, decode_item order, pre samples per pixel
   std::vector<WRay> lv0;
   const int tiles_x = (cam.width + 7) / 8, tiles_y = (cam.height + 7) / 8;
-  for (int tile = 0; tile < tiles_x * tiles_y; tile += tstep)
+  std::vector<int> tiles;
+  if (tstep > 0) {
+    for (int tile = 0; tile < tiles_x * tiles_y; tile += tstep) tiles.push_back(tile);
+  } else {
+    const int b = -tstep, x0 = (tiles_x - b) / 2, y0 = (tiles_y - b) / 2;
+    for (int ty = y0; ty < y0 + b; ty++)
+      for (int tx = x0; tx < x0 + b; tx++) tiles.push_back(ty * tiles_x + tx);
+  }
+  for (int tile : tiles)
     for (int l = 0; l < 64; l++)
       for (int smp = 0; smp < cam.pre_sample_times; smp++) {
         const int x = (tile % tiles_x) * 8 + ((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));
@@ -288,7 +318,7 @@ int main(int argc, char** argv) {
         const V3 lo = vadd(pos, vadd(vsc(left, a * cam.aperture_radius), vsc(upn, b * cam.aperture_radius)));
         lv0.push_back(WRay{lo, vsub(focus, lo), v3(1, 1, 1), cam.trace_depth});
       }
-  printf("level-0 rays %zu (every %d-th tile)\n", lv0.size(), tstep);
+  printf("level-0 rays %zu (tile_step %d)\n", lv0.size(), tstep);
   Occ tot_e[NORDER][NWALK], tot_s[NORDER][NWALK];
   for (int ord = 0; ord < NORDER; ord++) {
     std::vector<WRay> level = lv0;
@@ -304,7 +334,7 @@ int main(int argc, char** argv) {
       for (size_t c0 = 0; c0 < level.size(); c0 += 64) {
         const size_t c1 = std::min(level.size(), c0 + 64);
         std::vector<Lane> ln[NWALK];
-        for (int w = 0; w < NWALK; w++) {
+        for (int w = 0; w < nwalk; w++) {
           ln[w].resize(c1 - c0);
           for (size_t k = c0; k < c1; k++) lane_start(S, ln[w][k - c0], true, level[k].o, level[k].d);
           le[w].add(run_wave(S, ln[w], (Walk)w));
@@ -337,7 +367,7 @@ int main(int argc, char** argv) {
       for (const rtx_light_desc& Lt : S.lights) {
         for (size_t c0 = 0; c0 < hits.size(); c0 += 64) {
           const size_t c1 = std::min(hits.size(), c0 + 64);
-          for (int w = 0; w < NWALK; w++) {
+          for (int w = 0; w < nwalk; w++) {
             std::vector<Lane> ln(c1 - c0);
             for (size_t k = c0; k < c1; k++)
               lane_start(S, ln[k - c0], false, hits[k].o, vsub(v3p(Lt.position), hits[k].o));
@@ -387,7 +417,7 @@ int main(int argc, char** argv) {
           }
         }
       }
-      for (int w = 0; w < NWALK; w++) {
+      for (int w = 0; w < nwalk; w++) {
         printf("order %-6s level %d rays %7zu hits %7zu walk %-6s | extend node %5.1f leaf %5.1f exact %5.1f occ %5.1f "
                "time/ray %6.1f | shadow node %5.1f leaf %5.1f exact %5.1f occ %5.1f time/ray %6.1f\n",
                order_name[ord], lev, level.size(), hits.size(), walk_name[w], le[w].lanes[0] / std::max(1.0, le[w].steps[0]),
@@ -404,7 +434,7 @@ int main(int argc, char** argv) {
   }
   printf("\nall levels (time: VALU-instruction proxy per wave, summed; occ: cost-weighted active lanes)\n");
   for (int ord = 0; ord < NORDER; ord++)
-    for (int w = 0; w < NWALK; w++)
+    for (int w = 0; w < nwalk; w++)
       printf("order %-6s walk %-6s | extend occ %5.1f time %10.4g | shadow occ %5.1f time %10.4g | total %10.4g (x base/spec %.3f)\n",
              order_name[ord], walk_name[w], tot_e[ord][w].occ(), tot_e[ord][w].time(), tot_s[ord][w].occ(),
              tot_s[ord][w].time(), tot_e[ord][w].time() + tot_s[ord][w].time(),
