@@ -253,7 +253,7 @@ RTX_SHADE_FN double penumbra(V3 C, double R, V3 T, V3 lt, double radius, uint32_
 // the penumbra of spheres whose factor is 0, so these raises need their own
 // check: World#high_lights' lit_area (world.rb:92-93) by its own walk
 // (lit_area_raises), World#local_lights' (world.rb:76) inside the shadow walk
-// (option exact_raises, the default: xr_setup / xr_band below).
+// (option exact_raises = 1: xr_setup / xr_band below; off by default, §2.4).
 //
 // penumbra_raises: the reference's own operations up to the two acos
 // arguments (the bits of penumbra() and of rt_oracle.c's cover_area).
@@ -281,11 +281,12 @@ __device__ __forceinline__ bool penumbra_raises(V3 C, double R, V3 T, V3 lt, dou
 //     quantities: l = rho^2 |d|^2 up to 14 ulps of |oc|^2 |d|^2, q = (C - T).d,
 //     r1 = radius |q| / |d|^2); those go to the binary64 test (penumbra_raises);
 //   * a box that holds one meets the cone: a point P of the spheres' box within
-//     radius |t| (+ mg) of Q(t) has, on each axis, |t| (|d_a| - radius) <=
-//     |c_a - T_a| + h_a + mg, which bounds |t| by tm (xr_setup), so the walk
-//     slab-tests the child boxes dilated by radius tm + mg over t in [-tm, tm];
-//     the segment's own boxes (t in [0, 1], dilated by m S <= mg) are among
-//     them, so the covers' walk is unchanged.
+//     radius |t| (+ mg) of Q(t) has, on each axis, |t| (|d_a| - radius) <= the
+//     box's far side from T along that nappe's direction + mg, which bounds t
+//     to [-tb, tf] (xr_setup), so the walk slab-tests the child boxes dilated by
+//     radius max(tb, tf) + mg over t in [-tb, tf]; the segment's own boxes (t in
+//     [0, 1], dilated by m S <= mg) are among them, so the covers' walk is
+//     unchanged.
 // The box dilation mg = 2e-5 S (1 + radius / |d|) is ten times the float32
 // error of T, d and the box bounds (as the covers' m S, §2.2).  The band's own
 // half-width is 32 float32 ulps of S (1 + radius / |d|): the float32 geometry

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Phase breakdown of k_level from a -DRTX_STAMPS=1 build (diagnostic only):
-    RTX_LIB=_variants/librtx_stamps.so python tools/stamps_levels.py c2
-Per-wave shader-clock cycles (s_memtime) summed over every level launch of one frame."""
+"""Phase breakdown of k_level from a -DRTX_STAMPS=1 build, and / or the hierarchy
+walks' lane occupancy from a -DRTX_WALKSTATS=1 build (diagnostic only):
+    RTX_LIB=_variants/librtx_stamps.so python tools/stamps_levels.py c2 [option=value ...]
+Per-wave shader-clock cycles (s_memtime) summed over every level launch of one frame;
+walk counters: wave iterations of the inner-node loop and of the leaf visits, and the
+lanes active in each (query_bvh)."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -35,7 +38,7 @@ lib.rtxdbg_read_stamps(st, 1)
 lib.rtxdbg_read_level_stamps(lv, 1)
 lib.rtxdbg_read_walkstats(ws, 1)
 v = list(st)
-tot = sum(v[:6])
+tot = sum(v[:6]) or 1          # (0 without RTX_STAMPS: e.g. a walk-counter build alone)
 names = ["A claim/load/lens/highlight", "B EXTEND walk", "C hit_info/normal/cos", "D SHADOW walks + lights",
          "E (unused)", "F mask, slot alloc, children, leaf, record"]
 print("waves %d  chunks %d  cycles/chunk %.0f" % (v[7], v[6], tot / max(1, v[6])))

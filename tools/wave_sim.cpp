@@ -435,9 +435,14 @@ int main(int argc, char** argv) {
   printf("\nall levels (time: VALU-instruction proxy per wave, summed; occ: cost-weighted active lanes)\n");
   for (int ord = 0; ord < NORDER; ord++)
     for (int w = 0; w < nwalk; w++)
-      printf("order %-6s walk %-6s | extend occ %5.1f time %10.4g | shadow occ %5.1f time %10.4g | total %10.4g (x base/spec %.3f)\n",
+      printf("order %-6s walk %-6s | extend occ %5.1f time %10.4g | shadow occ %5.1f time %10.4g | total %10.4g (x base/spec %.3f)"
+             " | lanes per step (RTX_WALKSTATS form): extend node %.1f leaf %.1f, shadow node %.1f leaf %.1f\n",
              order_name[ord], walk_name[w], tot_e[ord][w].occ(), tot_e[ord][w].time(), tot_s[ord][w].occ(),
              tot_s[ord][w].time(), tot_e[ord][w].time() + tot_s[ord][w].time(),
-             (tot_e[ord][w].time() + tot_s[ord][w].time()) / (tot_e[BASE][SPEC].time() + tot_s[BASE][SPEC].time()));
+             (tot_e[ord][w].time() + tot_s[ord][w].time()) / (tot_e[BASE][SPEC].time() + tot_s[BASE][SPEC].time()),
+             tot_e[ord][w].lanes[0] / std::max(1.0, tot_e[ord][w].steps[0]),
+             tot_e[ord][w].lanes[1] / std::max(1.0, tot_e[ord][w].steps[1]),
+             tot_s[ord][w].lanes[0] / std::max(1.0, tot_s[ord][w].steps[0]),
+             tot_s[ord][w].lanes[1] / std::max(1.0, tot_s[ord][w].steps[1]));
   return 0;
 }
