@@ -198,7 +198,10 @@ rtx_status rtx_render_tile_list_device(rtx_context* ctx, const int32_t* tiles, i
  * camera samples' trees; extra samples not counted) in the last whole-frame
  * render of this context with the bounce-level engine, row-major over the
  * frame's ceil(width/8) x ceil(height/8) tiles: a measured work map for
- * balancing tile splits.  Synchronous; zeros before such a render. */
+ * balancing tile splits.  Every whole-frame level render rewrites every
+ * tile's count.  A sample re-rendered by the lanes engine (a capacity
+ * overflow, rtx_level_stats' redo) has no tree records and counts 0 rays.
+ * Synchronous; zeros before such a render. */
 rtx_status rtx_tile_rays(rtx_context* ctx, int64_t* out, int32_t n);
 
 /* Host-buffer variant of rtx_render_tiles_device (synchronous): packed holds
@@ -366,7 +369,11 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          colours),
          "lv_hl_cap" (bounce levels: entries of the batch's list of highlight rays whose lit_area raise is checked
          after the levels (k_hl_raise); 0 [default] = 1/256 of the tree-record capacity, at least 4096; a ray that
-         finds it full has its sample re-rendered by the lanes engine; same bits). */
+         finds it full has its sample re-rendered by the lanes engine; same bits), "lv_sort" (bounce levels, fused
+         level launches: 1 = before each level >= 1 one counting-sort pass lists its rays by bin, the direction's
+         octant and the origin's cell in an 8x8x8 grid over the spheres' box, and the level takes its 64-ray
+         chunks in that order, so a wave's rays start close together and point alike; records and children are
+         placed as without it; 0 off, -1 [default] = 1 above 512 spheres; same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

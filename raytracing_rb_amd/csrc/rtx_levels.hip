@@ -224,18 +224,17 @@ __device__ __forceinline__ void lv_in_queue(const KParams& p, int level, LvQueue
   q.chunks = (uint32_t)__shfl((int)q.cin, 63);
 }
 
-// Ray binning (option lv_sort, DESIGN.md §3.7).  A level >= 1 holds its rays
+// Ray binning (option lv_sort, DESIGN.md §3.17).  A level >= 1 holds its rays
 // in the order their parents were shaded, so a wave's 64 rays start from
 // scattered points in all directions and its lanes walk different parts of the
-// hierarchy.  With lv_sort the producer tags every staged ray with a bin: the
+// hierarchy.  With lv_sort the producer tags every staged ray with a bin (the
 // octant of its direction and the cell of its origin in an 8 x 8 x 8 grid over
-// the spheres' box (Morton order): before the level's launch k_lv_bin (count:
-// each staged ray's bin) / k_lv_bin_scan / k_lv_bin (scatter), one
-// counting-sort pass, list the level's rays bin by bin, and the level takes its
-// chunks from that list.  (The bins are computed there, not by the producer:
-// one more live value in k_level_c's shading spilled registers.)  Only the visiting order changes: every ray writes its record at its
-// dense index and allocates its children as before, so the trees, hence the
-// frames, are bit-identical (order independence, §3.7).
+// the spheres' box, Morton order); before the level's launch k_lv_bin (count)
+// / k_lv_bin_scan / k_lv_bin (scatter), one counting-sort pass, list the
+// level's rays bin by bin, and the level takes its chunks from that list.
+// Only the visiting order changes: every ray writes its record at its dense
+// index and allocates its children as before, so the trees, hence the frames,
+// are bit-identical (order independence, §3.7).
 __device__ __forceinline__ uint32_t lv_ray_bin(const SceneDev& S, const Ray& r) {
   const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
   uint32_t m = 0;
@@ -496,7 +495,7 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
                                           const Item& cur, int root, int x, int y, int sample, int besti, bool hin,
                                           V3 hit, V3 delta, V3 nrm, V3 nn, double c, V3 lc, int nl, char* rec,
                                           int nleaf, uint32_t errA, uint32_t errS, uint32_t errL, uint32_t errP,
-                                          const Material* m, bool last = false) {
+                                          const Material* m, bool last = false, bool keys = false) {
   const SceneDev& S = p.scene;
   const CameraDev& cam = *p.cam;
   const int depth = last ? 1 : cam.depth - level;   // last: the batch's last level (every child is cut off)
@@ -594,10 +593,11 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
     double* __restrict__ outs = p.lv_stage[(level + 1) & 1];
     uint32_t off = off0;
     auto put = [&](const Ray& r, V3 att, uint64_t path) {
-      if (off < cap)
-        lv_store_ray(p, outs + (size_t)(((uint32_t)slice << log2cap) + off) * p.lv_ray_dbl, r, att, path, root, x, y,
-                     sample);
-      else {
+      if (off < cap) {
+        const uint32_t at = ((uint32_t)slice << log2cap) + off;
+        lv_store_ray(p, outs + (size_t)at * p.lv_ray_dbl, r, att, path, root, x, y, sample);
+        if (keys) p.lv_key[at] = (uint16_t)lv_ray_bin(S, r);   // (the next level's binning)
+      } else {
         lv_redo(p, root);
         atomicAdd(&p.lv_ctl->dropped, 1u);
       }
@@ -754,7 +754,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
     }
     RTX_LV_STAMP(3)
     lv_finish(p, level, slice, shade, active, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec,
-              nleaf, errA, errS, errL, errP, shade ? &S.mat[besti] : S.mat);
+              nleaf, errA, errS, errL, errP, shade ? &S.mat[besti] : S.mat, false, p.lv_sort != 0);
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
@@ -808,7 +808,7 @@ constexpr int LV_RING_FIELDS_SMALL = 5;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
 constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMALL * 8;
 
-template <int SPH, int BS, int RF, bool LAST, bool XR>
+template <int SPH, int BS, int RF, bool LAST, bool XR, bool SORT>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
   constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
@@ -1031,7 +1031,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
     }
     RTX_LV_STAMP(3)
     lv_finish(p, level, slice, shade, shade, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec, 0,
-              errA, errS, errL, errP, m, LAST);
+              errA, errS, errL, errP, m, LAST, SORT);
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
@@ -1049,9 +1049,9 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS, int RF, bool LAST, bool XR>
+template <int SPH, int BS, int RF, bool LAST, bool XR, bool SORT>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
-  k_level_c_body<SPH, BS, RF, LAST, XR>(p, level);
+  k_level_c_body<SPH, BS, RF, LAST, XR, SORT>(p, level);
   lv_level_done(p, level + 1);
 }
 
@@ -1650,51 +1650,58 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
 
 // ----------------------------------------------------------------- ray binning
 // One counting-sort pass over a level's rays by bin (option lv_sort; lv_ray_bin
-// above): counts (and each ray's bin into lv_key), exclusive prefix, scatter
-// into lv_perm.  The count and the
-// scatter walk the level's chunks like its launch does (LvQueue), one wave per
-// chunk, and add a wave's rays bin by bin: one atomic per distinct bin of the
-// chunk (a level's chunks hold few: children of neighbouring parents).  The
-// order inside a bin is the atomics' order, which cannot change a result.
+// above): counts, exclusive prefix (k_lv_bin_scan), scatter into lv_perm.  The
+// producing level wrote each staged ray's bin beside it (lv_key, by queue
+// slot).  Workgroup g takes a contiguous range of the level's chunks (the
+// queue order, LvQueue), counts its rays per bin in LDS and then touches each
+// bin it saw once in global memory: the count adds its range's count, the
+// scatter reserves its range's places and, in a second pass over the range,
+// places each ray (LDS cursors).  A popular bin's counter word takes one
+// atomic per workgroup: one per wave and distinct bin measured 0.5 ms per C2
+// level (r10b), one per 1,024 rays 0.1 ms (r10c).  The order inside a bin is
+// the workgroups' order, which cannot change a result.
+constexpr int BIN_UNROLL = 4;              // chunks a wave has in flight
 template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_lv_bin(KParams p, int level) {
+  __shared__ uint32_t hist[LV_BINS];        // the range's count per bin (scatter: then its next place)
   LvQueue in;
   lv_in_queue(p, level, in);
-  const uint32_t W = gridDim.x * 4u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
-  uint16_t* key = p.lv_key;
-  uint32_t* ctr = p.lv_bins + (SCATTER ? LV_BINS : 0);
-  const uint64_t below = (1ull << __lane_id()) - 1ull;
-  for (uint32_t c = w; c < in.chunks; c += W) {
-    uint32_t s, off, i;
-    bool todo = in.item(c, s, off, i);
-    const uint32_t slot = (s << p.lv_slice_log2) + off;
-    uint32_t b = 0;
-    if (todo && SCATTER) {
-      b = key[slot];
-    } else if (todo) {                        // the staged ray's bin (its origin and direction)
-      const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
-      const double2 a = q[0], bb = q[1], cc = q[2];
-      Ray r;
-      r.o = v3(a.x, a.y, bb.x);
-      r.d = v3(bb.y, cc.x, cc.y);
-      b = lv_ray_bin(p.scene, r);
-      key[slot] = (uint16_t)b;
-    }
-    while (true) {
-      const uint64_t m = __ballot(todo);
-      if (!m) break;
-      const int lead = __builtin_ctzll(m);
-      const uint32_t lb = (uint32_t)__shfl((int)b, lead);
-      const uint64_t same = __ballot(todo && b == lb);
-      uint32_t at = 0;
-      if ((int)__lane_id() == lead) at = atomicAdd(&ctr[lb], (uint32_t)__popcll(same));
-      if (SCATTER) {
-        at = (uint32_t)__shfl((int)at, lead);
-        if (todo && b == lb) p.lv_perm[at + (uint32_t)__popcll(same & below)] = make_uint2(slot, i);
+  const int t = (int)threadIdx.x, wv = t >> 6;
+  const uint16_t* key = p.lv_key;
+  const uint32_t per = (in.chunks + gridDim.x - 1) / gridDim.x;
+  const uint32_t c0 = blockIdx.x * per, c1 = c0 + per < in.chunks ? c0 + per : in.chunks;
+  for (int k = t; k < LV_BINS; k += 256) hist[k] = 0u;
+  __syncthreads();
+  // chunks c0 + wv + 4 (u + BIN_UNROLL k): each wave BIN_UNROLL chunks at a time
+  auto sweep = [&](auto&& fn) {
+    for (uint32_t c = c0 + (uint32_t)wv; c < c1; c += 4u * BIN_UNROLL) {
+      uint32_t slot[BIN_UNROLL], idx[BIN_UNROLL], bin[BIN_UNROLL];
+      bool ok[BIN_UNROLL];
+#pragma unroll
+      for (int u = 0; u < BIN_UNROLL; u++) {
+        const uint32_t cu = c + 4u * (uint32_t)u;             // (uniform per wave)
+        uint32_t s = 0, off = 0, i = 0;
+        ok[u] = cu < c1 && in.item(cu, s, off, i);
+        slot[u] = (s << p.lv_slice_log2) + off;
+        idx[u] = i;
+        bin[u] = ok[u] ? key[slot[u]] : 0u;
       }
-      if (todo && b == lb) todo = false;
+#pragma unroll
+      for (int u = 0; u < BIN_UNROLL; u++)
+        if (ok[u]) fn(bin[u], slot[u], idx[u]);
     }
+  };
+  sweep([&](uint32_t b, uint32_t, uint32_t) { atomicAdd(&hist[b], 1u); });
+  __syncthreads();
+  for (int k = t; k < LV_BINS; k += 256) {
+    const uint32_t n = hist[k];
+    if (!n) continue;
+    if (SCATTER) hist[k] = atomicAdd(&p.lv_bins[LV_BINS + k], n);   // this range's first place in bin k
+    else atomicAdd(&p.lv_bins[k], n);
   }
+  if (!SCATTER) return;
+  __syncthreads();
+  sweep([&](uint32_t b, uint32_t slot, uint32_t i) { p.lv_perm[atomicAdd(&hist[b], 1u)] = make_uint2(slot, i); });
 }
 
 // The bins' exclusive prefix into the cursors; the counts zeroed for the next
@@ -1789,11 +1796,14 @@ static hipError_t launch_timed(K kern, long blocks, int bs, size_t lds, hipStrea
   return e;
 }
 
-// k_level_c for a level: the batch's last level compiled apart.
+// k_level_c for a level: the batch's last level compiled apart; with ray
+// binning (lv_sort) the other levels write their children's bins (SORT: a
+// kernel of its own, the key's registers would cost the default one spills).
 template <int SPH, int BS, int RF>
-static void (*level_c_kernel(bool last, bool xr))(KParams, int) {
-  if (xr) return last ? k_level_c<SPH, BS, RF, true, true> : k_level_c<SPH, BS, RF, false, true>;
-  return last ? k_level_c<SPH, BS, RF, true, false> : k_level_c<SPH, BS, RF, false, false>;
+static void (*level_c_kernel(bool last, bool xr, bool sort))(KParams, int) {
+  if (last) return xr ? k_level_c<SPH, BS, RF, true, true, false> : k_level_c<SPH, BS, RF, true, false, false>;
+  if (sort) return xr ? k_level_c<SPH, BS, RF, false, true, true> : k_level_c<SPH, BS, RF, false, false, true>;
+  return xr ? k_level_c<SPH, BS, RF, false, true, false> : k_level_c<SPH, BS, RF, false, false, false>;
 }
 
 #ifndef RTX_LV_FUSED_BS
@@ -1824,11 +1834,11 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
     if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level, xr);
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level, xr, q.lv_sort != 0);
     } else if (BVH && need_small <= budget) {  // the compact ring (C4-sized hierarchies)
       q.lds_ring = (int32_t)ring;
       lds = need_small;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, xr);
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, xr, q.lv_sort != 0);
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)
@@ -1879,12 +1889,12 @@ static hipError_t launch_shade(const KParams& p, int level, long cap_items, hipS
 }
 
 // A level's binning (option lv_sort): count, prefix, scatter; grids sized for
-// the level's capacity (cap rays), at most 8 workgroups per CU.
+// the level's capacity (cap rays): four workgroups per CU, each a contiguous range of chunks.
 static hipError_t launch_bins(const KParams& q, int level, long cap, hipStream_t s) {
   int cus = 0, per_cu = 0;
   const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(k_lv_bin<false>), 256, 0, cus, per_cu);
   if (e != hipSuccess) return e;
-  const long grid = std::max<long>(1, std::min<long>((cap / 64 + 3) / 4, (long)cus * 8));
+  const long grid = std::max<long>(1, std::min<long>(cap / 1024, (long)cus * 4));   // (<= 1,024 atomics per hot bin)
   hipLaunchKernelGGL(k_lv_bin<false>, dim3((unsigned)grid), dim3(256), 0, s, q, level);
   hipLaunchKernelGGL(k_lv_bin_scan, dim3(1), dim3(1024), 0, s, q, level);
   hipLaunchKernelGGL(k_lv_bin<true>, dim3((unsigned)grid), dim3(256), 0, s, q, level);

@@ -727,11 +727,19 @@ def test_binned_levels_c4_and_c2_full_frame(gpu):
     import make_scenes
     make_scenes.ensure_c4()
     sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=192, height=108, pre_sample_times=2, max_sample_times=2)
-    plain = _renderer(sd, cd, 1).render(seed=4)
-    assert _same(_renderer(sd, cd, 1, lv_sort=1).render(seed=4), plain)
+    auto = _renderer(sd, cd, 1)
+    assert auto.get_option("lv_sort") == -1 and auto.get_option("lv_sort_effective") == 1   # > 512 spheres
+    plain = _renderer(sd, cd, 1, lv_sort=0)
+    assert plain.get_option("lv_sort_effective") == 0
+    plain = plain.render(seed=4)
+    assert _same(auto.render(seed=4), plain)
+    assert _same(_renderer(sd, cd, 1, lv_sort=1, lv_compact=0).render(seed=4), plain)
     sd, cd = _scene("c2_world.yml", "c2_camera.yml")
-    plain = _renderer(sd, cd, 1).render()
+    plain = _renderer(sd, cd, 1)
+    assert plain.get_option("lv_sort_effective") == 0                                       # 64 spheres
+    plain = plain.render()
     r = _renderer(sd, cd, 1, lv_sort=1)
+    assert r.get_option("lv_sort_effective") == 1
     assert _same(r.render(), plain)
     st = r.level_stats()
     assert st["redo"] == 0 and st["dropped"] == 0

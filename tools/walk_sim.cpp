@@ -24,6 +24,7 @@
 //   tools/walk_sim scenes/c2_world.yml scenes/c2_camera.yml [stride] [max_rays_per_level]
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <random>
 #include <string>
@@ -79,7 +80,15 @@ struct Sim {
     bb = new Bvh4Builder{*bs, sph64, sph32, sph_obj};
     bb->sah = sah;
     root = bs->empty() ? BVH_NONE : bb->build(0, (int)bs->size(), 0);
-    if (sah && lds_bytes((int)bb->nodes.size(), (int)bb->slot_obj.size(), bb->stack + 1) > 160 * 1024) {
+    // (the library's rule: the median tree when only it fits LDS; WAVE_SIM_TREE=sah keeps the SAH tree)
+    const char* force = getenv("WAVE_SIM_TREE");
+    if (force && !strcmp(force, "median") && sah) {
+      *bs = in;
+      bb = new Bvh4Builder{*bs, sph64, sph32, sph_obj};
+      bb->sah = false;
+      root = bs->empty() ? BVH_NONE : bb->build(0, (int)bs->size(), 0);
+    }
+    if (sah && !force && lds_bytes((int)bb->nodes.size(), (int)bb->slot_obj.size(), bb->stack + 1) > 160 * 1024) {
       std::vector<BSph>* b2 = new std::vector<BSph>(in);
       Bvh4Builder* med = new Bvh4Builder{*b2, sph64, sph32, sph_obj};
       med->sah = false;

@@ -275,6 +275,7 @@ int main(int argc, char** argv) {
   // -tile_step x -tile_step tiles at the frame's centre (ray density as in a full frame)
   const int tstep = argc > 3 ? atoi(argv[3]) : 16;
   const bool only_spec = getenv("WAVE_SIM_SPEC_ONLY") != nullptr;
+  const int norder = getenv("WAVE_SIM_BASE_ONLY") ? 1 : NORDER;   // (WAVE_SIM_TREE=sah|median: the hierarchy)
   const int nwalk = only_spec ? 1 : NWALK;
   const size_t cap = argc > 4 ? (size_t)atoll(argv[4]) : 400000;
   rtxcli::Scene sc;
@@ -285,8 +286,9 @@ int main(int argc, char** argv) {
   S.lights = sc.lights;
   S.maxd = sc.desc.max_distance;
   S.build(true);
-  printf("scene: %zu spheres, %zu nodes, stack %d, q16 %d\n", S.sph64.size(), S.bb->nodes.size(), S.bb->stack + 1,
-         (int)S.q16);
+  printf("scene: %zu spheres, %zu nodes, %zu leaf slots, stack %d, q16 %d, tree %s\n", S.sph64.size(),
+         S.bb->nodes.size(), S.bb->slot_obj.size(), S.bb->stack + 1, (int)S.q16,
+         getenv("WAVE_SIM_TREE") ? getenv("WAVE_SIM_TREE") : "library rule");
   const V3 pos = v3p(cam.position), front = v3p(cam.front), up = v3p(cam.up);
   uint32_t e = 0;
   const V3 left = vnorm(vcross(up, front), e), upn = vnorm(up, e), fn = vnorm(front, e);
@@ -320,7 +322,7 @@ int main(int argc, char** argv) {
       }
   printf("level-0 rays %zu (tile_step %d)\n", lv0.size(), tstep);
   Occ tot_e[NORDER][NWALK], tot_s[NORDER][NWALK];
-  for (int ord = 0; ord < NORDER; ord++) {
+  for (int ord = 0; ord < norder; ord++) {
     std::vector<WRay> level = lv0;
     std::mt19937_64 rng2(7);
     for (int lev = 0; lev < cam.trace_depth && !level.empty(); lev++) {
@@ -433,7 +435,7 @@ int main(int argc, char** argv) {
     }
   }
   printf("\nall levels (time: VALU-instruction proxy per wave, summed; occ: cost-weighted active lanes)\n");
-  for (int ord = 0; ord < NORDER; ord++)
+  for (int ord = 0; ord < norder; ord++)
     for (int w = 0; w < nwalk; w++)
       printf("order %-6s walk %-6s | extend occ %5.1f time %10.4g | shadow occ %5.1f time %10.4g | total %10.4g (x base/spec %.3f)"
              " | lanes per step (RTX_WALKSTATS form): extend node %.1f leaf %.1f, shadow node %.1f leaf %.1f\n",
