@@ -227,9 +227,9 @@ uint32_t spread10(uint32_t x) {
   return x;
 }
 
-enum Order { BASE = 0, OCT, MORTON, OCTM, W128, W256, W512, W4096, M6, M9, M12, O_M6, O_M9, NORDER };
+enum Order { BASE = 0, OCT, MORTON, OCTM, W128, W256, W512, W4096, M6, M9, M12, O_M6, O_M9, O_M12, D6_M6, NORDER };
 const char* order_name[NORDER] = {"base", "oct", "morton", "octm", "w128", "w256", "w512", "w4096",
-                                  "m6", "m9", "m12", "o+m6", "o+m9"};
+                                  "m6", "m9", "m12", "o+m6", "o+m9", "o+m12", "d6+m6"};
 
 // the key of a ray: (direction octant, Morton code of the origin in the scene box)
 uint32_t ray_key(const Sim& S, const WRay& r, bool oct_only, bool morton_only) {
@@ -257,6 +257,12 @@ void order_level(const Sim& S, std::vector<WRay>& lv, Order ord) {
     if (ord == M12) r.key >>= 18;
     if (ord == O_M6) r.key >>= 23;
     if (ord == O_M9) r.key >>= 20;
+    if (ord == O_M12) r.key >>= 17;
+    if (ord == D6_M6) {                     // 6 direction bits (octant + which components dominate) + 6 origin bits
+      const double ax = fabs(r.d.x), ay = fabs(r.d.y), az = fabs(r.d.z), n = sqrt(ax * ax + ay * ay + az * az);
+      const uint32_t dom = (ax > 0.577 * n ? 1u : 0u) | (ay > 0.577 * n ? 2u : 0u) | (az > 0.577 * n ? 4u : 0u);
+      r.key = ((r.key >> 23) & ~63u) << 3 | dom << 6 | ((r.key >> 23) & 63u);
+    }
   }
   const size_t win = ord == W128 ? 128 : ord == W256 ? 256 : ord == W512 ? 512 : ord == W4096 ? 4096 : lv.size();
   for (size_t a = 0; a < lv.size(); a += win)
@@ -322,7 +328,14 @@ int main(int argc, char** argv) {
       }
   printf("level-0 rays %zu (tile_step %d)\n", lv0.size(), tstep);
   Occ tot_e[NORDER][NWALK], tot_s[NORDER][NWALK];
+  const char* only = getenv("WAVE_SIM_ORDERS");   // e.g. "base,o+m9,octm": these orders only
+  auto wanted = [&](int ord) {
+    if (!only) return true;
+    const std::string list = std::string(",") + only + ",";
+    return list.find(std::string(",") + order_name[ord] + ",") != std::string::npos;
+  };
   for (int ord = 0; ord < norder; ord++) {
+    if (!wanted(ord)) continue;
     std::vector<WRay> level = lv0;
     std::mt19937_64 rng2(7);
     for (int lev = 0; lev < cam.trace_depth && !level.empty(); lev++) {
@@ -436,7 +449,7 @@ int main(int argc, char** argv) {
   }
   printf("\nall levels (time: VALU-instruction proxy per wave, summed; occ: cost-weighted active lanes)\n");
   for (int ord = 0; ord < norder; ord++)
-    for (int w = 0; w < nwalk; w++)
+    for (int w = 0; w < nwalk && wanted(ord); w++)
       printf("order %-6s walk %-6s | extend occ %5.1f time %10.4g | shadow occ %5.1f time %10.4g | total %10.4g (x base/spec %.3f)"
              " | lanes per step (RTX_WALKSTATS form): extend node %.1f leaf %.1f, shadow node %.1f leaf %.1f\n",
              order_name[ord], walk_name[w], tot_e[ord][w].occ(), tot_e[ord][w].time(), tot_s[ord][w].occ(),
