@@ -24,7 +24,11 @@ constexpr int LV_MAXL = 64;                     // levels (= trace_depth) the en
 constexpr int LV_SLICES = 64;                   // slices per queue (one per lane of a consumer wave)
 constexpr int LV_CLAIMS = 16;                   // sharded chunk-claim counters per launch
 constexpr int LV_DONE = 16;                     // wave-completion counters per level launch (lv_level_done)
-constexpr int LV_BINS = 4096;                   // ray bins (option lv_sort): 8 direction octants x 512 origin cells
+#ifndef RTX_LV_CELL_BITS
+#define RTX_LV_CELL_BITS 4                      // (diagnostic builds may change the bin resolution)
+#endif
+constexpr int LV_CELL_BITS = RTX_LV_CELL_BITS;  // ray bins (option lv_sort): origin cells per axis = 2^LV_CELL_BITS,
+constexpr int LV_BINS = 8 << (3 * LV_CELL_BITS); // x 8 direction octants (32,768 bins)
 struct LevelCtl {
   uint32_t count0;                              // level-0 items of the batch
   uint32_t redo_n;                              // level-0 items handed to the lanes engine (capacity overflow)

@@ -228,26 +228,29 @@ __device__ __forceinline__ void lv_in_queue(const KParams& p, int level, LvQueue
 // in the order their parents were shaded, so a wave's 64 rays start from
 // scattered points in all directions and its lanes walk different parts of the
 // hierarchy.  With lv_sort the producer tags every staged ray with a bin (the
-// octant of its direction and the cell of its origin in an 8 x 8 x 8 grid over
-// the spheres' box, Morton order); before the level's launch k_lv_bin (count)
+// octant of its direction and the cell of its origin in a 16 x 16 x 16 grid
+// over the spheres' box, Morton order); before the level's launch k_lv_bin (count)
 // / k_lv_bin_scan / k_lv_bin (scatter), one counting-sort pass, list the
 // level's rays bin by bin, and the level takes its chunks from that list.
 // Only the visiting order changes: every ray writes its record at its dense
 // index and allocates its children as before, so the trees, hence the frames,
 // are bit-identical (order independence, §3.7).
 __device__ __forceinline__ uint32_t lv_ray_bin(const SceneDev& S, const Ray& r) {
+  constexpr int cells = 1 << LV_CELL_BITS;
   const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
   uint32_t m = 0;
 #pragma unroll
   for (int a = 0; a < 3; a++) {
     const float lo = S.root_c[a] - S.root_h[a];
-    const float f = (o[a] - lo) * (4.0f / fmaxf(S.root_h[a], 1e-30f));   // 8 cells over 2 h
-    const uint32_t c = (uint32_t)fminf(fmaxf(f, 0.0f), 7.0f);            // (NaN: cell 0)
-    m |= ((c & 1u) | (c & 2u) << 2 | (c & 4u) << 4) << a;
+    const float f = (o[a] - lo) * ((0.5f * cells) / fmaxf(S.root_h[a], 1e-30f));   // cells over 2 h
+    const uint32_t c = (uint32_t)fminf(fmaxf(f, 0.0f), (float)(cells - 1));      // (NaN: cell 0)
+#pragma unroll
+    for (int b = 0; b < LV_CELL_BITS; b++) m |= ((c >> b) & 1u) << (3 * b + a);   // Morton order
   }
   const uint32_t oct = (r.d.x < 0 ? 1u : 0u) | (r.d.y < 0 ? 2u : 0u) | (r.d.z < 0 ? 4u : 0u);
-  return oct << 9 | m;
+  return oct << (3 * LV_CELL_BITS) | m;
 }
+static_assert(LV_BINS <= 65536, "bins are 16-bit keys");
 
 // The level's chunks, and chunk c's ray for this lane: its queue slot and
 // dense index (binned: from the bin list; else the slices).  All lanes call it.
@@ -1661,25 +1664,27 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
 // level (r10b), one per 1,024 rays 0.1 ms (r10c).  The order inside a bin is
 // the workgroups' order, which cannot change a result.
 constexpr int BIN_UNROLL = 4;              // chunks a wave has in flight
+constexpr int BIN_BS = 1024;               // one workgroup per CU: the counts take 128 KB of LDS
+constexpr int BIN_WAVES = BIN_BS / 64;
 template <bool SCATTER>
-__global__ __launch_bounds__(256) void k_lv_bin(KParams p, int level) {
-  __shared__ uint32_t hist[LV_BINS];        // the range's count per bin (scatter: then its next place)
+__global__ __launch_bounds__(BIN_BS) void k_lv_bin(KParams p, int level) {
+  extern __shared__ uint32_t hist[];        // [LV_BINS] the range's count per bin (scatter: then its next place)
   LvQueue in;
   lv_in_queue(p, level, in);
   const int t = (int)threadIdx.x, wv = t >> 6;
   const uint16_t* key = p.lv_key;
   const uint32_t per = (in.chunks + gridDim.x - 1) / gridDim.x;
   const uint32_t c0 = blockIdx.x * per, c1 = c0 + per < in.chunks ? c0 + per : in.chunks;
-  for (int k = t; k < LV_BINS; k += 256) hist[k] = 0u;
+  for (int k = t; k < LV_BINS; k += BIN_BS) hist[k] = 0u;
   __syncthreads();
-  // chunks c0 + wv + 4 (u + BIN_UNROLL k): each wave BIN_UNROLL chunks at a time
+  // chunks c0 + wv + W (u + BIN_UNROLL k): each wave BIN_UNROLL chunks at a time
   auto sweep = [&](auto&& fn) {
-    for (uint32_t c = c0 + (uint32_t)wv; c < c1; c += 4u * BIN_UNROLL) {
+    for (uint32_t c = c0 + (uint32_t)wv; c < c1; c += (uint32_t)(BIN_WAVES * BIN_UNROLL)) {
       uint32_t slot[BIN_UNROLL], idx[BIN_UNROLL], bin[BIN_UNROLL];
       bool ok[BIN_UNROLL];
 #pragma unroll
       for (int u = 0; u < BIN_UNROLL; u++) {
-        const uint32_t cu = c + 4u * (uint32_t)u;             // (uniform per wave)
+        const uint32_t cu = c + (uint32_t)(BIN_WAVES * u);     // (uniform per wave)
         uint32_t s = 0, off = 0, i = 0;
         ok[u] = cu < c1 && in.item(cu, s, off, i);
         slot[u] = (s << p.lv_slice_log2) + off;
@@ -1693,7 +1698,7 @@ __global__ __launch_bounds__(256) void k_lv_bin(KParams p, int level) {
   };
   sweep([&](uint32_t b, uint32_t, uint32_t) { atomicAdd(&hist[b], 1u); });
   __syncthreads();
-  for (int k = t; k < LV_BINS; k += 256) {
+  for (int k = t; k < LV_BINS; k += BIN_BS) {
     const uint32_t n = hist[k];
     if (!n) continue;
     if (SCATTER) hist[k] = atomicAdd(&p.lv_bins[LV_BINS + k], n);   // this range's first place in bin k
@@ -1705,29 +1710,26 @@ __global__ __launch_bounds__(256) void k_lv_bin(KParams p, int level) {
 }
 
 // The bins' exclusive prefix into the cursors; the counts zeroed for the next
-// level.  One workgroup of 1024 threads, 4 bins each.
+// level.  One workgroup of 1024 threads, LV_BINS / 1024 consecutive bins each.
 __global__ __launch_bounds__(1024) void k_lv_bin_scan(KParams p, int level) {
+  constexpr int PER = LV_BINS / 1024;
   __shared__ uint32_t part[16];
   const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
-  uint32_t v[4], sum = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    v[k] = p.lv_bins[4 * t + k];
-    sum += v[k];
-  }
+  uint32_t sum = 0;
+  for (int k = 0; k < PER; k++) sum += p.lv_bins[PER * t + k];
   const uint32_t incl = wave_scan_incl(sum);
   if (lane == 63) part[wv] = incl;
   __syncthreads();
   uint32_t pre = incl - sum;
   for (int k = 0; k < wv; k++) pre += part[k];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    p.lv_bins[LV_BINS + 4 * t + k] = pre;
-    p.lv_bins[4 * t + k] = 0u;
-    pre += v[k];
+  for (int k = 0; k < PER; k++) {
+    const uint32_t v = p.lv_bins[PER * t + k];
+    p.lv_bins[LV_BINS + PER * t + k] = pre;
+    p.lv_bins[PER * t + k] = 0u;
+    pre += v;
   }
 }
-static_assert(LV_BINS == 4 * 1024, "k_lv_bin_scan: 4 bins per thread");
+static_assert(LV_BINS % 1024 == 0, "k_lv_bin_scan: whole bins per thread");
 
 // Diagnostic builds: this unit's stamps (k_level), added by rtxdbg_read_stamps.
 int read_level_stamps(unsigned long long* out, int reset) {
@@ -1889,15 +1891,17 @@ static hipError_t launch_shade(const KParams& p, int level, long cap_items, hipS
 }
 
 // A level's binning (option lv_sort): count, prefix, scatter; grids sized for
-// the level's capacity (cap rays): four workgroups per CU, each a contiguous range of chunks.
+// the level's capacity (cap rays): one workgroup per CU, each a contiguous range of chunks.
 static hipError_t launch_bins(const KParams& q, int level, long cap, hipStream_t s) {
-  int cus = 0, per_cu = 0;
-  const hipError_t e = cus_and_fit(reinterpret_cast<const void*>(k_lv_bin<false>), 256, 0, cus, per_cu);
+  const size_t lds = (size_t)LV_BINS * 4;
+  int cus = 0, per_cu = 0;                     // (also raises the kernels' dynamic-LDS limit)
+  hipError_t e = cus_and_fit(reinterpret_cast<const void*>(k_lv_bin<false>), BIN_BS, lds, cus, per_cu);
+  if (e == hipSuccess) e = cus_and_fit(reinterpret_cast<const void*>(k_lv_bin<true>), BIN_BS, lds, cus, per_cu);
   if (e != hipSuccess) return e;
-  const long grid = std::max<long>(1, std::min<long>(cap / 1024, (long)cus * 4));   // (<= 1,024 atomics per hot bin)
-  hipLaunchKernelGGL(k_lv_bin<false>, dim3((unsigned)grid), dim3(256), 0, s, q, level);
+  const long grid = std::max<long>(1, std::min<long>(cap / 4096, (long)cus * std::max(1, per_cu)));
+  hipLaunchKernelGGL(k_lv_bin<false>, dim3((unsigned)grid), dim3(BIN_BS), lds, s, q, level);
   hipLaunchKernelGGL(k_lv_bin_scan, dim3(1), dim3(1024), 0, s, q, level);
-  hipLaunchKernelGGL(k_lv_bin<true>, dim3((unsigned)grid), dim3(256), 0, s, q, level);
+  hipLaunchKernelGGL(k_lv_bin<true>, dim3((unsigned)grid), dim3(BIN_BS), lds, s, q, level);
   return hipGetLastError();
 }
 
