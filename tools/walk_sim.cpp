@@ -98,6 +98,22 @@ struct Sim {
         root = r;
       }
     }
+    if (const char* qb = getenv("WAVE_SIM_QUANT")) {   // child boxes on an 2^bits grid over the node's own box, rounded out
+      const float steps = (float)((1 << atoi(qb)) - 1);
+      for (Bvh4Node& n : bb->nodes)
+        for (int a = 0; a < 3; a++) {
+          float lo = INFINITY, hi = -INFINITY;
+          for (int k = 0; k < 4; k++)
+            if (n.child[k] != BVH_NONE) lo = fminf(lo, n.lh[a][k][0]), hi = fmaxf(hi, n.lh[a][k][1]);
+          const float ext = (hi - lo) / steps;
+          if (!(ext > 0)) continue;
+          for (int k = 0; k < 4; k++) {
+            if (n.child[k] == BVH_NONE) continue;
+            n.lh[a][k][0] = lo + floorf((n.lh[a][k][0] - lo) / ext) * ext;
+            n.lh[a][k][1] = fminf(hi, lo + ceilf((n.lh[a][k][1] - lo) / ext) * ext);
+          }
+        }
+    }
     const QuantLeaves ql = quantize_leaves(*bb, sph_scale);
     q16 = ql.ok && sph64.size() > 256;        // C4-sized scenes run SPH_BVH_QLDS
     q_err = (float)((ql.max_err + 2.0 * (double)ql.rstep) * 1.01 + 1e-9 * ql.max_r);
