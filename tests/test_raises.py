@@ -260,7 +260,8 @@ def test_oracles_raise_at_the_pixel_of_a_factor0_cover(oracle_lib, tmp_path, cas
 ENGINES = [(0, {}), (1, {}), (1, dict(lv_split=1)), (1, dict(lv_compact=0)), (1, dict(lv_compact=2)),
            (0, dict(bvh=2)), (1, dict(bvh=2)), (1, dict(bvh=2, sphere_src=2)), (1, dict(bvh=2, sphere_src=4)),
            (1, dict(bvh=0)), (1, dict(bvh=2, sphere_src=4, lv_split=1)),
-           (1, dict(lv_hl_cap=1)), (1, dict(lv_hl_cap=1, lv_split=1))]   # deferred-check list overflow: re-render
+           (1, dict(lv_hl_cap=1)), (1, dict(lv_hl_cap=1, lv_split=1)),   # deferred-check list overflow: re-render
+           (1, dict(lv_sort=1)), (1, dict(lv_sort=1, bvh=2, sphere_src=4))]  # binned levels (SORT kernels)
 
 
 def _renderer(sd, cd, engine, **opts):
