@@ -371,9 +371,12 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          after the levels (k_hl_raise); 0 [default] = 1/256 of the tree-record capacity, at least 4096; a ray that
          finds it full has its sample re-rendered by the lanes engine; same bits), "lv_sort" (bounce levels, fused
          level launches: 1 = before each level >= 1 one counting-sort pass lists its rays by bin, the direction's
-         octant and the origin's cell in an 8x8x8 grid over the spheres' box, and the level takes its 64-ray
+         octant and the origin's cell in a grid over the spheres' box (lv_sort_bits), and the level takes its 64-ray
          chunks in that order, so a wave's rays start close together and point alike; records and children are
-         placed as without it; 0 off, -1 [default] = 1 above 512 spheres; same bits). */
+         placed as without it; 0 off, 1 / -1 [default] on; same bits), "lv_sort_from" (the first level binned;
+         0 [default] = level 1 above 512 spheres, else the last level only; the levels before it keep the queue
+         order), "lv_sort_bits" (2^bits origin cells per axis of a bin, 3 or 4; 0 [default] = 4 above 512
+         spheres, else 3). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

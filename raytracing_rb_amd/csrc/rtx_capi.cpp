@@ -92,8 +92,11 @@ struct rtx_context {
   int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
   int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also check the acos raises of the covers they skip
                                      // (C2 +10 %, C4 +108 %, r09c; so not the default)
-  int64_t opt_lv_sort = -1;          // bounce levels: 1 = levels >= 1 visited bin by bin (direction octant, origin cell),
-                                     // -1 auto: above 512 spheres (C4 354 -> 318 ms; C2 4.65 -> 4.88 ms, r10d)
+  int64_t opt_lv_sort = -1;          // bounce levels: 1 = levels visited bin by bin (direction octant, origin cell), 0 off,
+                                     // -1 auto = on
+  int64_t opt_lv_sort_from = 0;      // bounce levels: the first level binned; 0 auto: level 1 above 512 spheres (C4 354 ->
+                                     // 307 ms), else the last level only (C2 4.60 -> 4.57 ms; all levels 4.65 -> 4.88, r10d/r10k)
+  int64_t opt_lv_sort_bits = 0;      // bounce levels: 2^bits origin cells per axis (3 or 4); 0 auto: 4 above 512 spheres, else 3
   int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
@@ -269,7 +272,8 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_streams", c->opt_lv_streams}, {"lv_grid_div", c->opt_lv_grid_div},
       {"lv_redo_blocks", c->opt_lv_redo_blocks},
       {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
-      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_sort", c->opt_lv_sort}};
+      {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_sort", c->opt_lv_sort},
+      {"lv_sort_from", c->opt_lv_sort_from}, {"lv_sort_bits", c->opt_lv_sort_bits}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -366,6 +370,16 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_sort")) {           // bounce levels: bin each level's rays before its launch (same bits)
     if (value < -1 || value > 1) return fail(c, RTX_EINVAL, "lv_sort must be -1, 0 or 1");
     c->opt_lv_sort = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_sort_from")) {      // bounce levels: the first level binned (with lv_sort), 0 auto
+    if (value < 0 || value > LV_MAXL) return fail(c, RTX_EINVAL, "lv_sort_from must be in [0, %d]", LV_MAXL);
+    c->opt_lv_sort_from = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_sort_bits")) {      // bounce levels: 2^bits origin cells per axis of a ray bin, 0 auto
+    if (value != 0 && value != 3 && value != 4) return fail(c, RTX_EINVAL, "lv_sort_bits must be 0, 3 or 4");
+    c->opt_lv_sort_bits = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_ray_bytes")) {      // bounce levels: staged ray record size (0 auto)
@@ -772,10 +786,21 @@ static bool lv_paths32(const rtx_context* c) {
 }
 
 // ray binning (option lv_sort) for the fused level launches
-static bool lv_sort_on(const rtx_context* c) {
+// The first level binned (0: none) and the bins' resolution.  Large scenes
+// bin every level >= 1 (C4 354 -> 307 ms); small ones only the last, where the
+// rays are most incoherent and most numerous (C2: binning every level costs
+// more than it gains, r10d; the last level alone gains 0.5 %, r10k).
+static int lv_sort_from(const rtx_context* c) {
   const bool split = c->opt_lv_split != 0 && c->scene.n_light <= LV_SPLIT_MAX_LIGHTS;
-  return (c->opt_lv_sort == 1 || (c->opt_lv_sort == -1 && c->scene.n_sphere > 512)) && !split;
+  if (c->opt_lv_sort == 0 || split) return 0;
+  const bool large = c->scene.n_sphere > 512;
+  const int from = c->opt_lv_sort_from > 0 ? (int)c->opt_lv_sort_from : large ? 1 : c->cam.depth - 1;
+  return from >= 1 && from < c->cam.depth ? from : 0;
 }
+static int lv_sort_bits(const rtx_context* c) {
+  return c->opt_lv_sort_bits ? (int)c->opt_lv_sort_bits : c->scene.n_sphere > 512 ? 4 : 3;
+}
+static bool lv_sort_on(const rtx_context* c) { return lv_sort_from(c) > 0; }
 
 static bool levels_engine(const rtx_context* c) {
   return c->opt_engine == 1 && c->cam.depth <= LV_MAXL && c->cam.pt + 2 <= 16 && c->scene.n_light <= 255;
@@ -855,7 +880,8 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_key = sort ? (uint16_t*)q : nullptr;      q += sz_key;
     k.lv_perm = sort ? (uint2*)q : nullptr;        q += sz_perm;
     k.lv_bins = sort ? (uint32_t*)q : nullptr;     q += sz_bins;
-    k.lv_sort = sort ? 1 : 0;
+    k.lv_sort = sort ? lv_sort_from(c) : 0;
+    k.lv_cell_bits = lv_sort_bits(c);
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;

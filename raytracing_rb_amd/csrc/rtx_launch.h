@@ -24,11 +24,8 @@ constexpr int LV_MAXL = 64;                     // levels (= trace_depth) the en
 constexpr int LV_SLICES = 64;                   // slices per queue (one per lane of a consumer wave)
 constexpr int LV_CLAIMS = 16;                   // sharded chunk-claim counters per launch
 constexpr int LV_DONE = 16;                     // wave-completion counters per level launch (lv_level_done)
-#ifndef RTX_LV_CELL_BITS
-#define RTX_LV_CELL_BITS 4                      // (diagnostic builds may change the bin resolution)
-#endif
-constexpr int LV_CELL_BITS = RTX_LV_CELL_BITS;  // ray bins (option lv_sort): origin cells per axis = 2^LV_CELL_BITS,
-constexpr int LV_BINS = 8 << (3 * LV_CELL_BITS); // x 8 direction octants (32,768 bins)
+constexpr int LV_CELL_BITS_MAX = 4;             // ray bins (option lv_sort): origin cells per axis = 2^lv_cell_bits
+constexpr int LV_BINS = 8 << (3 * LV_CELL_BITS_MAX); // x 8 direction octants: at most 32,768 bins
 struct LevelCtl {
   uint32_t count0;                              // level-0 items of the batch
   uint32_t redo_n;                              // level-0 items handed to the lanes engine (capacity overflow)
@@ -120,10 +117,11 @@ struct KParams {
   // ray binning (option lv_sort): a level >= 1 is processed in the order of its
   // rays' bins (lv_ray_bin: direction octant, origin cell), records still at
   // their dense index
-  int32_t lv_sort;                 // 1: bin levels >= 1 before their launch
+  int32_t lv_sort;                 // 0, or the first level binned before its launch (option lv_sort_from)
+  int32_t lv_cell_bits;            // origin cells per axis of a bin = 2^lv_cell_bits (3 or 4: 4,096 or 32,768 bins)
   uint16_t* lv_key;                // bin of each staged ray of the level being binned, by queue slot (k_lv_bin)
   uint2* lv_perm;                  // the level's rays in bin order: {queue slot, dense index}
-  uint32_t* lv_bins;               // LV_BINS counts, LV_BINS cursors
+  uint32_t* lv_bins;               // LV_BINS counts, LV_BINS cursors (the first 8 << 3 lv_cell_bits used)
 };
 
 // Where the sphere walk reads its records:

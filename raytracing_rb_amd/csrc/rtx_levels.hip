@@ -235,31 +235,31 @@ __device__ __forceinline__ void lv_in_queue(const KParams& p, int level, LvQueue
 // Only the visiting order changes: every ray writes its record at its dense
 // index and allocates its children as before, so the trees, hence the frames,
 // are bit-identical (order independence, §3.7).
-__device__ __forceinline__ uint32_t lv_ray_bin(const SceneDev& S, const Ray& r) {
-  constexpr int cells = 1 << LV_CELL_BITS;
+__device__ __forceinline__ uint32_t lv_ray_bin(const SceneDev& S, const Ray& r, int bits) {
+  const float cells = (float)(1 << bits);
   const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
   uint32_t m = 0;
 #pragma unroll
   for (int a = 0; a < 3; a++) {
     const float lo = S.root_c[a] - S.root_h[a];
     const float f = (o[a] - lo) * ((0.5f * cells) / fmaxf(S.root_h[a], 1e-30f));   // cells over 2 h
-    const uint32_t c = (uint32_t)fminf(fmaxf(f, 0.0f), (float)(cells - 1));      // (NaN: cell 0)
+    const uint32_t c = (uint32_t)fminf(fmaxf(f, 0.0f), cells - 1.0f);            // (NaN: cell 0)
 #pragma unroll
-    for (int b = 0; b < LV_CELL_BITS; b++) m |= ((c >> b) & 1u) << (3 * b + a);   // Morton order
+    for (int b = 0; b < LV_CELL_BITS_MAX; b++) m |= ((c >> b) & 1u) << (3 * b + a);   // Morton order
   }
   const uint32_t oct = (r.d.x < 0 ? 1u : 0u) | (r.d.y < 0 ? 2u : 0u) | (r.d.z < 0 ? 4u : 0u);
-  return oct << (3 * LV_CELL_BITS) | m;
+  return oct << (3 * bits) | m;
 }
 static_assert(LV_BINS <= 65536, "bins are 16-bit keys");
 
 // The level's chunks, and chunk c's ray for this lane: its queue slot and
 // dense index (binned: from the bin list; else the slices).  All lanes call it.
 __device__ __forceinline__ uint32_t lv_chunks(const KParams& p, const LvQueue& in, int level) {
-  return level > 0 && p.lv_sort ? (in.total + 63u) >> 6 : in.chunks;
+  return p.lv_sort && level >= p.lv_sort ? (in.total + 63u) >> 6 : in.chunks;
 }
 __device__ __forceinline__ bool lv_chunk_item(const KParams& p, const LvQueue& in, int level, uint32_t c,
                                               uint32_t& slot, uint32_t& i) {
-  if (level > 0 && p.lv_sort) {
+  if (p.lv_sort && level >= p.lv_sort) {
     const uint32_t k = c * 64u + (uint32_t)__lane_id();
     slot = i = 0;
     if (k >= in.total) return false;
@@ -599,7 +599,7 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
       if (off < cap) {
         const uint32_t at = ((uint32_t)slice << log2cap) + off;
         lv_store_ray(p, outs + (size_t)at * p.lv_ray_dbl, r, att, path, root, x, y, sample);
-        if (keys) p.lv_key[at] = (uint16_t)lv_ray_bin(S, r);   // (the next level's binning)
+        if (keys) p.lv_key[at] = (uint16_t)lv_ray_bin(S, r, p.lv_cell_bits);   // (the next level's binning)
       } else {
         lv_redo(p, root);
         atomicAdd(&p.lv_ctl->dropped, 1u);
@@ -757,7 +757,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
     }
     RTX_LV_STAMP(3)
     lv_finish(p, level, slice, shade, active, cur, root, x, y, sample, besti, hin, hit, delta, nrm, nn, c, lc, nl, rec,
-              nleaf, errA, errS, errL, errP, shade ? &S.mat[besti] : S.mat, false, p.lv_sort != 0);
+              nleaf, errA, errS, errL, errP, shade ? &S.mat[besti] : S.mat, false, p.lv_sort && level + 1 >= p.lv_sort);
     RTX_LV_STAMP(5)
   }
 #undef RTX_LV_STAMP
@@ -1645,7 +1645,7 @@ __global__ __launch_bounds__(256) void k_level_begin(KParams p, int n0_max, int 
     (&p.lv_ctl->sh[0][0])[w] = 0;
   }
   if (p.lv_sort)
-    for (int w = t; w < LV_BINS; w += nt) p.lv_bins[w] = 0;   // (k_lv_bin_scan zeroes them after each level)
+    for (int w = t; w < (8 << (3 * p.lv_cell_bits)); w += nt) p.lv_bins[w] = 0;   // (k_lv_bin_scan zeroes them after each level)
   const int cwords = (nlev < LV_MAXL + 1 ? nlev : LV_MAXL + 1) * LV_CLAIMS * 32;
   for (int w = t; w < cwords; w += nt)
     for (int k = 0; k < 3; k++) (&p.lv_ctl->claim[k][0][0])[w] = 0;
@@ -1668,14 +1668,15 @@ constexpr int BIN_BS = 1024;               // one workgroup per CU: the counts t
 constexpr int BIN_WAVES = BIN_BS / 64;
 template <bool SCATTER>
 __global__ __launch_bounds__(BIN_BS) void k_lv_bin(KParams p, int level) {
-  extern __shared__ uint32_t hist[];        // [LV_BINS] the range's count per bin (scatter: then its next place)
+  extern __shared__ uint32_t hist[];        // [nb] the range's count per bin (scatter: then its next place)
+  const int nb = 8 << (3 * p.lv_cell_bits);
   LvQueue in;
   lv_in_queue(p, level, in);
   const int t = (int)threadIdx.x, wv = t >> 6;
   const uint16_t* key = p.lv_key;
   const uint32_t per = (in.chunks + gridDim.x - 1) / gridDim.x;
   const uint32_t c0 = blockIdx.x * per, c1 = c0 + per < in.chunks ? c0 + per : in.chunks;
-  for (int k = t; k < LV_BINS; k += BIN_BS) hist[k] = 0u;
+  for (int k = t; k < nb; k += BIN_BS) hist[k] = 0u;
   __syncthreads();
   // chunks c0 + wv + W (u + BIN_UNROLL k): each wave BIN_UNROLL chunks at a time
   auto sweep = [&](auto&& fn) {
@@ -1698,7 +1699,7 @@ __global__ __launch_bounds__(BIN_BS) void k_lv_bin(KParams p, int level) {
   };
   sweep([&](uint32_t b, uint32_t, uint32_t) { atomicAdd(&hist[b], 1u); });
   __syncthreads();
-  for (int k = t; k < LV_BINS; k += BIN_BS) {
+  for (int k = t; k < nb; k += BIN_BS) {
     const uint32_t n = hist[k];
     if (!n) continue;
     if (SCATTER) hist[k] = atomicAdd(&p.lv_bins[LV_BINS + k], n);   // this range's first place in bin k
@@ -1710,26 +1711,25 @@ __global__ __launch_bounds__(BIN_BS) void k_lv_bin(KParams p, int level) {
 }
 
 // The bins' exclusive prefix into the cursors; the counts zeroed for the next
-// level.  One workgroup of 1024 threads, LV_BINS / 1024 consecutive bins each.
+// level.  One workgroup of 1024 threads, nb / 1024 consecutive bins each.
 __global__ __launch_bounds__(1024) void k_lv_bin_scan(KParams p, int level) {
-  constexpr int PER = LV_BINS / 1024;
+  const int per = (8 << (3 * p.lv_cell_bits)) / 1024;
   __shared__ uint32_t part[16];
   const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
   uint32_t sum = 0;
-  for (int k = 0; k < PER; k++) sum += p.lv_bins[PER * t + k];
+  for (int k = 0; k < per; k++) sum += p.lv_bins[per * t + k];
   const uint32_t incl = wave_scan_incl(sum);
   if (lane == 63) part[wv] = incl;
   __syncthreads();
   uint32_t pre = incl - sum;
   for (int k = 0; k < wv; k++) pre += part[k];
-  for (int k = 0; k < PER; k++) {
-    const uint32_t v = p.lv_bins[PER * t + k];
-    p.lv_bins[LV_BINS + PER * t + k] = pre;
-    p.lv_bins[PER * t + k] = 0u;
+  for (int k = 0; k < per; k++) {
+    const uint32_t v = p.lv_bins[per * t + k];
+    p.lv_bins[LV_BINS + per * t + k] = pre;
+    p.lv_bins[per * t + k] = 0u;
     pre += v;
   }
 }
-static_assert(LV_BINS % 1024 == 0, "k_lv_bin_scan: whole bins per thread");
 
 // Diagnostic builds: this unit's stamps (k_level), added by rtxdbg_read_stamps.
 int read_level_stamps(unsigned long long* out, int reset) {
@@ -1836,11 +1836,11 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
     if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level, xr, q.lv_sort != 0);
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level, xr, q.lv_sort && level + 1 >= q.lv_sort);
     } else if (BVH && need_small <= budget) {  // the compact ring (C4-sized hierarchies)
       q.lds_ring = (int32_t)ring;
       lds = need_small;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, xr, q.lv_sort != 0);
+      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, xr, q.lv_sort && level + 1 >= q.lv_sort);
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)
@@ -1893,7 +1893,7 @@ static hipError_t launch_shade(const KParams& p, int level, long cap_items, hipS
 // A level's binning (option lv_sort): count, prefix, scatter; grids sized for
 // the level's capacity (cap rays): one workgroup per CU, each a contiguous range of chunks.
 static hipError_t launch_bins(const KParams& q, int level, long cap, hipStream_t s) {
-  const size_t lds = (size_t)LV_BINS * 4;
+  const size_t lds = (size_t)(8 << (3 * q.lv_cell_bits)) * 4;
   int cus = 0, per_cu = 0;                     // (also raises the kernels' dynamic-LDS limit)
   hipError_t e = cus_and_fit(reinterpret_cast<const void*>(k_lv_bin<false>), BIN_BS, lds, cus, per_cu);
   if (e == hipSuccess) e = cus_and_fit(reinterpret_cast<const void*>(k_lv_bin<true>), BIN_BS, lds, cus, per_cu);
@@ -1950,7 +1950,7 @@ static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_ma
   for (int d = 0; d < nlev && e == hipSuccess; d++) {
     const long cap = d == 0 ? (long)n0_max : scap;
     if (!q.lv_split) {
-      if (d > 0 && q.lv_sort) e = launch_bins(q, d, cap, s);
+      if (q.lv_sort && d >= q.lv_sort) e = launch_bins(q, d, cap, s);
       if (e == hipSuccess) e = launch_level_mode(q, mode, 0, d, cap, s, kev);
       continue;
     }

@@ -709,6 +709,9 @@ def test_binned_levels_bit_identical(gpu, world, camera, ov):
     dict(lv_rec_pct=101, lv_floor=0),
     dict(lv_static=0),                                   # every chunk claimed
     dict(lv_split=1),                                    # split phases: lv_sort has no effect there
+    dict(lv_sort_from=2), dict(lv_sort_from=4),          # the first levels in queue order
+    dict(lv_sort_from=9),                                # past the last level: nothing binned
+    dict(lv_sort_bits=3, lv_sort_from=1), dict(lv_sort_bits=4, lv_sort_from=1),
 ])
 def test_binned_levels_batches_overflow_schedule(gpu, opts):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
@@ -735,11 +738,13 @@ def test_binned_levels_c4_and_c2_full_frame(gpu):
     assert _same(auto.render(seed=4), plain)
     assert _same(_renderer(sd, cd, 1, lv_sort=1, lv_compact=0).render(seed=4), plain)
     sd, cd = _scene("c2_world.yml", "c2_camera.yml")
-    plain = _renderer(sd, cd, 1)
-    assert plain.get_option("lv_sort_effective") == 0                                       # 64 spheres
+    plain = _renderer(sd, cd, 1, lv_sort=0)
+    assert plain.get_option("lv_sort_effective") == 0
     plain = plain.render()
-    r = _renderer(sd, cd, 1, lv_sort=1)
+    r = _renderer(sd, cd, 1)                      # 64 spheres: the last level binned, 8^3 cells
     assert r.get_option("lv_sort_effective") == 1
+    assert _same(r.render(), plain)
+    r = _renderer(sd, cd, 1, lv_sort=1, lv_sort_from=1, lv_sort_bits=4)
     assert _same(r.render(), plain)
     st = r.level_stats()
     assert st["redo"] == 0 and st["dropped"] == 0
