@@ -35,7 +35,9 @@ namespace {
 // step costs in VALU instructions per lane (rough counts from the ISA of k_level_c):
 // an inner node (fetch, 4 slab tests, sort, pushes), a leaf's float pre-test of
 // its 4 spheres, one binary64 exact sphere test
-constexpr double C_NODE = 60, C_LEAF = 70, C_EXACT = 160;
+constexpr double C_LEAF = 70, C_EXACT = 160;
+// (WAVE_SIM_NODE_COST: another per-node cost, e.g. a node format that decodes its boxes)
+const double C_NODE = getenv("WAVE_SIM_NODE_COST") ? atof(getenv("WAVE_SIM_NODE_COST")) : 60.0;
 
 struct Occ {
   double steps[3] = {0, 0, 0}, lanes[3] = {0, 0, 0}, waves = 0;
