@@ -748,3 +748,18 @@ def test_binned_levels_c4_and_c2_full_frame(gpu):
     assert _same(r.render(), plain)
     st = r.level_stats()
     assert st["redo"] == 0 and st["dropped"] == 0
+
+
+def test_binning_options_validated(gpu):
+    from raytracing_rb_amd.runtime import RtxError
+    sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=32, height=18)
+    r = _renderer(sd, cd, 1)
+    assert (r.get_option("lv_sort"), r.get_option("lv_sort_from"), r.get_option("lv_sort_bits")) == (-1, 0, 0)
+    for k, v in (("lv_sort", 2), ("lv_sort", -2), ("lv_sort_from", -1), ("lv_sort_from", 65), ("lv_sort_bits", 5),
+                 ("lv_sort_bits", 2)):
+        with pytest.raises(RtxError):
+            r.set_option(k, v)
+    r.set_option("lv_sort_from", 5)               # past the last level (depth 5: levels 0-4): nothing binned
+    assert r.get_option("lv_sort_effective") == 0
+    r.set_option("lv_sort_from", 4)
+    assert r.get_option("lv_sort_effective") == 1

@@ -40,10 +40,11 @@ constexpr double C_LEAF = 70, C_EXACT = 160;
 const double C_NODE = getenv("WAVE_SIM_NODE_COST") ? atof(getenv("WAVE_SIM_NODE_COST")) : 60.0;
 
 struct Occ {
-  double steps[3] = {0, 0, 0}, lanes[3] = {0, 0, 0}, waves = 0;
+  double steps[3] = {0, 0, 0}, lanes[3] = {0, 0, 0}, waves = 0, exact_ideal = 0;
   void add(const Occ& o) {
     for (int k = 0; k < 3; k++) steps[k] += o.steps[k], lanes[k] += o.lanes[k];
     waves += o.waves;
+    exact_ideal += o.exact_ideal;
   }
   double time() const { return steps[0] * C_NODE + steps[1] * C_LEAF + steps[2] * C_EXACT; }
   double occ() const {
@@ -200,13 +201,17 @@ Occ run_wave(const Sim& S, std::vector<Lane>& lanes, Walk w) {
     if (!lf.empty()) {
       oc.steps[1]++;
       oc.lanes[1] += lf.size();
-      int cnt[4] = {0, 0, 0, 0};
+      // the exact tests: each lane loops over its own kept spheres (walk_leaf's
+      // while (keep)), so the wave runs max over lanes of their count passes
+      int passes = 0, total = 0;
       for (auto& [i, leaf] : lf) {
-        const int m = lane_leaf(S, lanes[i], leaf);
-        for (int u = 0; u < 4; u++) cnt[u] += m >> u & 1;
+        const int n = __builtin_popcount(lane_leaf(S, lanes[i], leaf));
+        passes = std::max(passes, n);
+        total += n;
       }
-      for (int u = 0; u < 4; u++)
-        if (cnt[u]) oc.steps[2]++, oc.lanes[2] += cnt[u];
+      oc.steps[2] += passes;
+      oc.lanes[2] += total;
+      oc.exact_ideal += (total + 63) / 64;       // (candidates compacted across the wave)
     }
     if (!spec)
       for (auto& [i, leaf] : lf) lanes[i].ref = lanes[i].pop();
@@ -453,13 +458,18 @@ int main(int argc, char** argv) {
   for (int ord = 0; ord < norder; ord++)
     for (int w = 0; w < nwalk && wanted(ord); w++)
       printf("order %-6s walk %-6s | extend occ %5.1f time %10.4g | shadow occ %5.1f time %10.4g | total %10.4g (x base/spec %.3f)"
-             " | lanes per step (RTX_WALKSTATS form): extend node %.1f leaf %.1f, shadow node %.1f leaf %.1f\n",
+             " | lanes per step (RTX_WALKSTATS form): extend node %.1f leaf %.1f, shadow node %.1f leaf %.1f"
+             " | steps node/leaf/exact: extend %.3g %.3g %.3g (exact %.1f lanes; compacted %.3g), shadow %.3g %.3g %.3g"
+             " (exact %.1f lanes; compacted %.3g)\n",
              order_name[ord], walk_name[w], tot_e[ord][w].occ(), tot_e[ord][w].time(), tot_s[ord][w].occ(),
              tot_s[ord][w].time(), tot_e[ord][w].time() + tot_s[ord][w].time(),
              (tot_e[ord][w].time() + tot_s[ord][w].time()) / (tot_e[BASE][SPEC].time() + tot_s[BASE][SPEC].time()),
              tot_e[ord][w].lanes[0] / std::max(1.0, tot_e[ord][w].steps[0]),
              tot_e[ord][w].lanes[1] / std::max(1.0, tot_e[ord][w].steps[1]),
              tot_s[ord][w].lanes[0] / std::max(1.0, tot_s[ord][w].steps[0]),
-             tot_s[ord][w].lanes[1] / std::max(1.0, tot_s[ord][w].steps[1]));
+             tot_s[ord][w].lanes[1] / std::max(1.0, tot_s[ord][w].steps[1]), tot_e[ord][w].steps[0],
+             tot_e[ord][w].steps[1], tot_e[ord][w].steps[2], tot_e[ord][w].lanes[2] / std::max(1.0, tot_e[ord][w].steps[2]),
+             tot_e[ord][w].exact_ideal, tot_s[ord][w].steps[0], tot_s[ord][w].steps[1], tot_s[ord][w].steps[2],
+             tot_s[ord][w].lanes[2] / std::max(1.0, tot_s[ord][w].steps[2]), tot_s[ord][w].exact_ideal);
   return 0;
 }
