@@ -12,7 +12,7 @@ streams, frame i on context i mod F, so one frame's last levels and tree
 reduction overlap the next frame's first levels.  Every one of the K timed
 frames is rendered completely (and, multi-GPU, gathered to rank 0) inside the
 timed region; `ms_per_step` is the time per frame of that stream of frames,
-`frame_latency_ms` one frame rendered alone.
+`frame_latency_ms` one frame rendered alone, as the library renders one frame by default (`frame_latency_parts` parts on the context's streams).
 
 Multi-GPU (C3, BASELINE.json configs[3]): one process per GPU.  Under
 torch.distributed.run (WORLD_SIZE set) this process is one rank; with
@@ -322,9 +322,11 @@ def main():
     # (lv_streams = 1: the overlap comes from the other frame; two parts per
     # frame on top of that measured slower, profiles/r03x).
     rs = []
+    parts_default = None
     for _ in range(F):
         rc = Renderer(scene, cam, device=local_rank)
         rc.set_option("bvh", args.bvh)
+        parts_default = rc.get_option("lv_streams")
         if F > 1:
             rc.set_option("lv_streams", 1)
         for kv in args.option:
@@ -447,16 +449,24 @@ def main():
         del full
 
     # ---- one frame alone (latency; F = 1 semantics), outside the timed region
-    latency_ms = None
+    # One frame alone renders as the library does by default (lv_streams parts
+    # on the context's streams); the contexts of the frames in flight render one
+    # part each (the other frame fills the tails), restored afterwards.
+    latency_ms, latency_parts = None, None
     if world == 1 and emulate is None:
+        parts_inflight = rs[0].get_option("lv_streams")
+        if not any(kv.split("=", 1)[0] == "lv_streams" for kv in args.option):
+            rs[0].set_option("lv_streams", parts_default)
+        latency_parts = rs[0].get_option("lv_streams")
         lat = []
-        for _ in range(5):
+        for _ in range(6):
             torch.cuda.synchronize(dev)
             a = time.perf_counter()
             render_full(0)
             torch.cuda.synchronize(dev)
             lat.append((time.perf_counter() - a) * 1e3)
-        latency_ms = float(np.median(lat))
+        latency_ms = float(np.median(lat[1:]))        # (the first: the parts' buffers allocated)
+        rs[0].set_option("lv_streams", parts_inflight)
 
     # ---- the dominant kernel alone: HIP events on its launch stream around
     # every ray-tree kernel launch (rtx_kernel_time), outside the timed region
@@ -610,6 +620,7 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "frames_in_flight": F,
             "frame_latency_ms": round(latency_ms, 4) if latency_ms is not None else None,
+            "frame_latency_parts": latency_parts,
             # SURVEY.md §8(d)'s one-frame-at-a-time rate: W*H / frame_latency_ms
             "value_single_frame": round(W * H / latency_ms / 1e3, 3) if latency_ms else None,
             "higher_is_better": True,
