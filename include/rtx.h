@@ -374,8 +374,8 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          octant and the origin's cell in a grid over the spheres' box (lv_sort_bits), and the level takes its 64-ray
          chunks in that order, so a wave's rays start close together and point alike; records and children are
          placed as without it; 0 off, 1 / -1 [default] on; same bits), "lv_sort_from" (the first level binned;
-         0 [default] = level 1 above 512 spheres, else the last level only; the levels before it keep the queue
-         order), "lv_sort_bits" (2^bits origin cells per axis of a bin, 3 or 4; 0 [default] = 4 above 512
+         0 [default] = level 1 above 512 spheres, else the last level only and only in batches of at least 2^22
+         camera samples; the levels before it keep the queue order), "lv_sort_bits" (2^bits origin cells per axis of a bin, 3 or 4; 0 [default] = 4 above 512
          spheres, else 3). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */

@@ -238,7 +238,8 @@ static bool levels_engine(const rtx_context* c);
 static bool lv_paths32(const rtx_context* c);
 static int sph_mode(const rtx_context* c);
 
-static bool lv_sort_on(const rtx_context* c);
+static int lv_sort_from(const rtx_context* c, size_t n0);
+static size_t lv_frame_items(const rtx_context* c);
 
 rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
   if (!c || !key || !value) return RTX_EINVAL;
@@ -247,7 +248,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
     return RTX_OK;
   }
   if (!strcmp(key, "lv_sort_effective")) {    // read-only: whether the next bounce-level render bins its levels
-    *value = lv_sort_on(c) ? 1 : 0;
+    *value = c->have_cam && lv_sort_from(c, lv_frame_items(c)) > 0 ? 1 : 0;
     return RTX_OK;
   }
   if (!strcmp(key, "sph_mode_effective")) {   // read-only: the SphMode of the next bounce-level render's walks
@@ -790,17 +791,25 @@ static bool lv_paths32(const rtx_context* c) {
 // bin every level >= 1 (C4 354 -> 307 ms); small ones only the last, where the
 // rays are most incoherent and most numerous (C2: binning every level costs
 // more than it gains, r10d; the last level alone gains 0.5 %, r10k).
-static int lv_sort_from(const rtx_context* c) {
+// n0: the camera samples of a batch (the last level of a small scene is binned
+// only from 2^22 of them: a 1/8 or 1/4 share of the C2 frame lost 4-5 % to the
+// binning passes' fixed cost, half of it neither gained nor lost, r10p).
+static int lv_sort_from(const rtx_context* c, size_t n0) {
   const bool split = c->opt_lv_split != 0 && c->scene.n_light <= LV_SPLIT_MAX_LIGHTS;
   if (c->opt_lv_sort == 0 || split) return 0;
   const bool large = c->scene.n_sphere > 512;
+  if (c->opt_lv_sort == -1 && c->opt_lv_sort_from == 0 && !large && n0 < ((size_t)1 << 22)) return 0;
   const int from = c->opt_lv_sort_from > 0 ? (int)c->opt_lv_sort_from : large ? 1 : c->cam.depth - 1;
   return from >= 1 && from < c->cam.depth ? from : 0;
+}
+// the samples of a whole-frame render's first batch (lv_sort_effective)
+static size_t lv_frame_items(const rtx_context* c) {
+  const size_t tiles = (size_t)((c->cam.width + 7) / 8) * (size_t)((c->cam.height + 7) / 8);
+  return std::min<size_t>((size_t)c->opt_lv_batch, tiles * 64 * (size_t)std::max(1, c->cam.pre));
 }
 static int lv_sort_bits(const rtx_context* c) {
   return c->opt_lv_sort_bits ? (int)c->opt_lv_sort_bits : c->scene.n_sphere > 512 ? 4 : 3;
 }
-static bool lv_sort_on(const rtx_context* c) { return lv_sort_from(c) > 0; }
 
 static bool levels_engine(const rtx_context* c) {
   return c->opt_engine == 1 && c->cam.depth <= LV_MAXL && c->cam.pt + 2 <= 16 && c->scene.n_light <= 255;
@@ -850,7 +859,8 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
                sz_area = split ? al256(hcap * (size_t)std::max(1, c->scene.n_light) * 16) : 0;
   // ray binning (lv_sort, fused levels only): a bin per staged slot, the
   // level's bin list, the bin counts and cursors
-  const bool sort = lv_sort_on(c);
+  const int sort_from = lv_sort_from(c, n0);
+  const bool sort = sort_from > 0;
   const size_t sz_key = sort ? al256(scap * 2) : 0, sz_perm = sort ? al256(scap * 8) : 0,
                sz_bins = sort ? al256((size_t)LV_BINS * 8) : 0;
   // One buffer set per part: with lv_streams = P the region's tiles are
@@ -880,7 +890,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_key = sort ? (uint16_t*)q : nullptr;      q += sz_key;
     k.lv_perm = sort ? (uint2*)q : nullptr;        q += sz_perm;
     k.lv_bins = sort ? (uint32_t*)q : nullptr;     q += sz_bins;
-    k.lv_sort = sort ? lv_sort_from(c) : 0;
+    k.lv_sort = sort_from;
     k.lv_cell_bits = lv_sort_bits(c);
   };
   carve(p, buf);
