@@ -1690,7 +1690,7 @@ __global__ __launch_bounds__(BIN_BS) void k_lv_bin(KParams p, int level) {
         ok[u] = cu < c1 && in.item(cu, s, off, i);
         slot[u] = (s << p.lv_slice_log2) + off;
         idx[u] = i;
-        bin[u] = ok[u] ? key[slot[u]] : 0u;
+        bin[u] = ok[u] ? key[slot[u]] & (uint32_t)(nb - 1) : 0u;   // (written for this resolution: < nb)
       }
 #pragma unroll
       for (int u = 0; u < BIN_UNROLL; u++)
