@@ -376,7 +376,10 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          placed as without it; 0 off, 1 / -1 [default] on; same bits), "lv_sort_from" (the first level binned;
          0 [default] = level 1 above 512 spheres, else the last level only and only in batches of at least 2^22
          camera samples; the levels before it keep the queue order), "lv_sort_bits" (2^bits origin cells per axis of a bin, 3 or 4; 0 [default] = 4 above 512
-         spheres, else 3). */
+         spheres, else 3), "lbuf" (bounce levels: 1 [default] = the shadow walks of scenes whose sphere records
+         are staged in LDS (sphere mode 3) visit only the leaves listed in a per-light cube map of the spheres
+         as seen from the light, built at upload, when it fits LDS next to the hit rings; 0 = the hierarchy
+         walk; same bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */

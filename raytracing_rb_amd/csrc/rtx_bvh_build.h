@@ -280,5 +280,114 @@ inline QuantLeaves quantize_leaves(const Bvh4Builder& bb, float sph_scale) {
   return ql;
 }
 
+// Light buffer: for each light, a cube map of 6 x n x n cells
+// around its position; cell c lists the hierarchy's leaves that hold a sphere
+// whose disc, as seen from the light, meets the cell.  A sphere that covers a
+// shadow ray's target T (World#lit_area: it crosses the segment from T to the
+// light L, short of L) meets the ray from L towards T, so its disc holds that
+// direction and its leaf is in the direction's cell: the shadow walk visits
+// those leaves only, with the same leaf tests.  The discs are widened by
+// DELTA radians, far more than the float32 cell lookup's error (the cell of
+// direction v is found on face 2a + (v_a < 0) of its dominant axis a, at
+// i = floor((s + 1) n / 2), s = v_b / |v_a|, b = (a + 1) mod 3, likewise j for
+// c = (a + 2) mod 3); a light inside or on a sphere puts that sphere's leaf in
+// every cell.  Layout per light (uint16 words, `stride` per light): 6 n n + 1
+// offsets into the light's leaf list, then the list (leaf references, int16).
+struct LightBuffer {
+  int n = 0, stride = 0;
+  std::vector<uint16_t> words;
+};
+
+inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const double (*lpos)[3], int n_light, int n,
+                                      size_t max_words) {
+  LightBuffer lb;
+  if (n_light <= 0 || root == BVH_NONE) return lb;
+  std::vector<int32_t> leaves;                     // every leaf reference of the hierarchy
+  if (root < 0) leaves.push_back(root);
+  for (const Bvh4Node& nd : bb.nodes)
+    for (int k = 0; k < 4; k++)
+      if (nd.child[k] < 0 && nd.child[k] != BVH_NONE) leaves.push_back(nd.child[k]);
+  const double DELTA = 1e-4;
+  const int cells = 6 * n * n;
+  std::vector<std::vector<uint16_t>> per(n_light);
+  auto dir = [](int face, double s, double t, double v[3]) {   // a point of face `face` at (s, t)
+    const int a = face >> 1, b = (a + 1) % 3, c = (a + 2) % 3;
+    v[a] = (face & 1) ? -1.0 : 1.0;
+    v[b] = s;
+    v[c] = t;
+    const double r = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    for (int k = 0; k < 3; k++) v[k] /= r;
+  };
+  auto angle = [](const double u[3], const double v[3]) {
+    const double d = u[0] * v[0] + u[1] * v[1] + u[2] * v[2];
+    return std::acos(std::max(-1.0, std::min(1.0, d)));
+  };
+  for (int li = 0; li < n_light; li++) {
+    const double* L = lpos[li];
+    // each sphere's disc: (direction, half-angle), or "everywhere"
+    struct Disc { double u[3], alpha; bool all; };
+    std::vector<std::vector<Disc>> discs(leaves.size());
+    for (size_t f = 0; f < leaves.size(); f++) {
+      const int v = ~leaves[f], slot0 = (v >> 2) * BVH_LEAF, cnt = (v & 3) + 1;
+      for (int u = 0; u < cnt; u++) {
+        const Sphere64& sp = bb.slot64[(size_t)slot0 + u];
+        if (!(sp.r >= 0.0)) continue;
+        Disc dc{};
+        const double w[3] = {sp.c[0] - L[0], sp.c[1] - L[1], sp.c[2] - L[2]};
+        const double D = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        const double scale = std::fabs(L[0]) + std::fabs(L[1]) + std::fabs(L[2]) + std::fabs(sp.c[0]) +
+                             std::fabs(sp.c[1]) + std::fabs(sp.c[2]) + sp.r;
+        dc.all = !(D > sp.r * (1.0 + 1e-9) + 1e-12 * scale) || !std::isfinite(D);
+        if (!dc.all) {
+          for (int k = 0; k < 3; k++) dc.u[k] = w[k] / D;
+          dc.alpha = std::asin(std::min(1.0, sp.r / D));
+        }
+        discs[f].push_back(dc);
+      }
+    }
+    std::vector<uint16_t> off(cells + 1, 0);
+    std::vector<uint16_t> list;
+    for (int face = 0; face < 6; face++)
+      for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+          const double s0 = -1.0 + 2.0 * i / n, s1 = -1.0 + 2.0 * (i + 1) / n;
+          const double t0 = -1.0 + 2.0 * j / n, t1 = -1.0 + 2.0 * (j + 1) / n;
+          double ctr[3];
+          dir(face, 0.5 * (s0 + s1), 0.5 * (t0 + t1), ctr);
+          double rho = 0.0;                          // the cell's angular radius about its center (boundary samples)
+          for (int k = 0; k <= 8; k++) {
+            const double e = k / 8.0;
+            const double pts[4][2] = {{s0 + e * (s1 - s0), t0}, {s0 + e * (s1 - s0), t1}, {s0, t0 + e * (t1 - t0)},
+                                      {s1, t0 + e * (t1 - t0)}};
+            for (const auto& q : pts) {
+              double v[3];
+              dir(face, q[0], q[1], v);
+              rho = std::max(rho, angle(ctr, v));
+            }
+          }
+          const int cell = (face * n + i) * n + j;
+          off[cell] = (uint16_t)list.size();
+          for (size_t f = 0; f < leaves.size(); f++) {
+            bool hit = false;
+            for (const Disc& dc : discs[f])
+              if (dc.all || angle(dc.u, ctr) <= dc.alpha + rho * (1.0 + 1e-6) + 2.0 * DELTA) hit = true;
+            if (hit) list.push_back((uint16_t)(int16_t)leaves[f]);
+          }
+          if (list.size() > 65535) return LightBuffer{};
+        }
+    off[cells] = (uint16_t)list.size();
+    per[li] = off;
+    per[li].insert(per[li].end(), list.begin(), list.end());
+  }
+  size_t stride = 0;
+  for (const auto& v : per) stride = std::max(stride, v.size());
+  stride = (stride + 7) & ~(size_t)7;               // (16-B aligned blocks)
+  if (stride * (size_t)n_light > max_words) return LightBuffer{};
+  lb.n = n;
+  lb.stride = (int)stride;
+  lb.words.assign(stride * (size_t)n_light, 0);
+  for (int li = 0; li < n_light; li++) std::copy(per[li].begin(), per[li].end(), lb.words.begin() + stride * li);
+  return lb;
+}
 
 }  // namespace rtx

@@ -97,6 +97,7 @@ struct rtx_context {
   int64_t opt_lv_sort_from = 0;      // bounce levels: the first level binned; 0 auto: level 1 above 512 spheres (C4 354 ->
                                      // 307 ms), else the last level only (C2 4.60 -> 4.57 ms; all levels 4.65 -> 4.88, r10d/r10k)
   int64_t opt_lv_sort_bits = 0;      // bounce levels: 2^bits origin cells per axis (3 or 4); 0 auto: 4 above 512 spheres, else 3
+  int64_t opt_lbuf = 1;              // bounce levels: 1 = shadow walks through the light buffer where it is staged (§3.18)
   int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
   uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
@@ -274,7 +275,7 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_redo_blocks", c->opt_lv_redo_blocks},
       {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
       {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_sort", c->opt_lv_sort},
-      {"lv_sort_from", c->opt_lv_sort_from}, {"lv_sort_bits", c->opt_lv_sort_bits}};
+      {"lv_sort_from", c->opt_lv_sort_from}, {"lv_sort_bits", c->opt_lv_sort_bits}, {"lbuf", c->opt_lbuf}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -381,6 +382,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_sort_bits")) {      // bounce levels: 2^bits origin cells per axis of a ray bin, 0 auto
     if (value != 0 && value != 3 && value != 4) return fail(c, RTX_EINVAL, "lv_sort_bits must be 0, 3 or 4");
     c->opt_lv_sort_bits = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lbuf")) {              // bounce levels: shadow walks through the light buffer (same bits)
+    if (value != 0 && value != 1) return fail(c, RTX_EINVAL, "lbuf must be 0 or 1");
+    c->opt_lbuf = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_ray_bytes")) {      // bounce levels: staged ray record size (0 auto)
@@ -623,6 +629,24 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
   S.n_slots = (int)bb.slot_obj.size();
   S.bvh_root = bvh_root;
   S.bvh_stack = bb.stack + 1;
+  {                                                  // the light buffer (scenes whose records the level kernels stage)
+    std::vector<double> lp(3 * (size_t)std::max(1, sd->n_lights));
+    for (int i = 0; i < sd->n_lights; i++)
+      for (int a = 0; a < 3; a++) lp[3 * i + a] = lights[i].pos[a];
+    LightBuffer lb;
+    if (sph64.size() <= 512 && sd->n_lights > 0)
+      for (int n : {24, 16, 12, 8}) {
+        lb = build_light_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), sd->n_lights, n,
+                                LBUF_MAX_WORDS);
+        if (lb.n) break;
+      }
+    if (lb.n) {
+      HIPCHK(c, up(lb.words.data(), lb.words.size() * sizeof(uint16_t), &ptr));
+      S.lbuf = (const uint16_t*)ptr;
+      S.lbuf_n = lb.n;
+      S.lbuf_stride = lb.stride;
+    }
+  }
   S.max_distance = sd->max_distance;
   S.sse = sd->soft_shadow_exponent;
   S.sph_scale = sph_scale;
@@ -892,6 +916,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_bins = sort ? (uint32_t*)q : nullptr;     q += sz_bins;
     k.lv_sort = sort_from;
     k.lv_cell_bits = lv_sort_bits(c);
+    k.lv_lbuf = (int32_t)c->opt_lbuf;
   };
   carve(p, buf);
   p.lv_split = split ? 1 : 0;

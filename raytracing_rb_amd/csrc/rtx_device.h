@@ -782,6 +782,56 @@ __device__ __forceinline__ void walk_covers(const SceneDev& S, V3 o, V3 d, V3 L,
   }
 }
 
+// World#lit_area's walk through the light buffer (SceneDev::
+// lbuf; lb: this light's block): planes and boxes first, then only the leaves
+// listed in the cell of the direction from the light towards o, each with the
+// hierarchy walk's own leaf test (walk_leaf), then the ordered cover sum.  Every
+// sphere that covers o lies in a listed leaf (the cell holds the direction of
+// its crossing point as seen from the light), and the covers are summed in
+// object order, so the result is the hierarchy walk's.  false: no usable cell
+// (a non-finite or zero ray); the caller walks the hierarchy.
+template <int BS, typename LP, typename XP, typename OP>
+__device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb, LP leaf4, XP x64, OP xobj, int* ci,
+                                           double* cv, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
+                                           V3& bhit, bool& bin, double& total, uint32_t& err) {
+  const SlabRay s = slab_setup(S, o, d);
+  if (!s.fin) return false;
+  // the cube-map cell of v = o - L = -d: face 2a + (v_a < 0) of the dominant
+  // axis a, cell (floor((v_b / |v_a| + 1) n / 2), likewise for c), b = a + 1, c = a + 2 (mod 3)
+  const float vx = -s.dx, vy = -s.dy, vz = -s.dz;
+  const float ax = fabsf(vx), ay = fabsf(vy), az = fabsf(vz);
+  int face;
+  float m, fs, ft;
+  if (ax >= ay && ax >= az) {
+    face = vx < 0.0f ? 1 : 0, m = ax, fs = vy, ft = vz;
+  } else if (ay >= az) {
+    face = vy < 0.0f ? 3 : 2, m = ay, fs = vz, ft = vx;
+  } else {
+    face = vz < 0.0f ? 5 : 4, m = az, fs = vx, ft = vy;
+  }
+  if (!(m > 0.0f)) return false;
+  const int n = S.lbuf_n;
+  const float h = 0.5f * (float)n / m;
+  const int i = min(max((int)floorf(__builtin_fmaf(fs, h, 0.5f * (float)n)), 0), n - 1);
+  const int j = min(max((int)floorf(__builtin_fmaf(ft, h, 0.5f * (float)n)), 0), n - 1);
+  const int cell = (face * n + i) * n + j;
+  const int k0 = lb[cell], k1 = lb[cell + 1];
+  const uint16_t* ent = lb + 6 * n * n + 1;
+  const double r = vr(d);
+  const double r2 = r * r;                        // front.r2
+  V3 dn = d;
+  if (r != 0) dn = v3(d.x / r, d.y / r, d.z / r); // front.normalize (the hierarchy walk's bits)
+  float thi = 1.0f + 1e-5f + s.mS / (float)r;
+  int ncov = 0;
+  bool ovf = false;
+  walk_planes_boxes<BS>(S, false, o, d, L, r, best, besti, bhit, bin, thi, ci, cv, ncov, ovf);
+  for (int k = k0; k < k1; k++)
+    walk_leaf<BS>((int)(int16_t)ent[k], leaf4, x64, xobj, s, false, o, d, dn, r, r2, L, radius, best, besti, bhit,
+                  bin, thi, err, ci, cv, ncov, ovf, false, 0.0f);
+  walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, false);
+  return true;
+}
+
 // Resumable: a lane whose walk is still running when fewer than `postpone`
 // lanes of its wave are is postponed (returns false) with its walk in
 // ref / sp (+ the LDS stack) / ncov / ovf (+ the LDS cover list) and best /
@@ -1466,7 +1516,7 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   const SceneDev& S = p.scene;
   size_t off = 0;
   if (mode == SPH_LIN_LDS) off = (size_t)(S.n_sphere + 4) * 16;
-  p.lds_x64 = p.lds_xobj = p.lds_mat = p.lds_sphr = -1;
+  p.lds_x64 = p.lds_xobj = p.lds_mat = p.lds_sphr = p.lds_lbuf = -1;
   if (mode == SPH_BVH_LDS || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX || mode == SPH_BVH_QLDS) {
     off = (size_t)S.n_nodes * sizeof(Bvh4Node);
     p.lds_leaf = (int32_t)off;

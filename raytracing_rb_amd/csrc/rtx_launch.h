@@ -63,6 +63,7 @@ struct KParams {
   // dynamic LDS layout (bytes), filled by launch_render/launch_trace
   int32_t lds_leaf, lds_stack, lds_cov, lds_items;
   int32_t lds_x64, lds_xobj;       // SPH_BVH_LDSX: staged Sphere64 records / object indices per leaf slot
+  int32_t lds_lbuf;                // the light buffer staged in LDS (byte offset), or -1: shadow walks use the hierarchy
   int32_t lds_mat, lds_sphr;       // SPH_BVH_LDSX: staged materials (per object) / Sphere64 records (per sphere)
   int32_t stk_slots;               // ray-stack entries per lane kept in LDS (set by the launcher)
   int32_t stk_slots_max;           // cap (option "lds_stack"; the stack bucket by default)
@@ -119,6 +120,7 @@ struct KParams {
   // their dense index
   int32_t lv_sort;                 // 0, or the first level binned before its launch (option lv_sort_from)
   int32_t lv_cell_bits;            // origin cells per axis of a bin = 2^lv_cell_bits (3 or 4: 4,096 or 32,768 bins)
+  int32_t lv_lbuf;                 // 1: the fused level kernels' shadow walks use the light buffer when staged (option lbuf)
   uint16_t* lv_key;                // bin of each staged ray of the level being binned, by queue slot (k_lv_bin)
   uint2* lv_perm;                  // the level's rays in bin order: {queue slot, dense index}
   uint32_t* lv_bins;               // LV_BINS counts, LV_BINS cursors (the first 8 << 3 lv_cell_bits used)

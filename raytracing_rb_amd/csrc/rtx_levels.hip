@@ -398,6 +398,11 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
       for (int i = threadIdx.x; i < nm; i += BS) m[i] = reinterpret_cast<const float4*>(S.mat)[i];
       float4* sr = reinterpret_cast<float4*>(lds + p.lds_sphr);
       for (int i = threadIdx.x; i < 2 * S.n_sphere; i += BS) sr[i] = reinterpret_cast<const float4*>(S.sph64)[i];
+      if (p.lds_lbuf >= 0) {                  // the light buffer (lbuf_stride words per light, a multiple of 8)
+        uint4* lb = reinterpret_cast<uint4*>(lds + p.lds_lbuf);
+        const int nw = S.lbuf_stride * S.n_light / 8;
+        for (int i = threadIdx.x; i < nw; i += BS) lb[i] = reinterpret_cast<const uint4*>(S.lbuf)[i];
+      }
     }
     __syncthreads();
   }
@@ -409,8 +414,18 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
 template <int SPH, int BS>
 __device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V3 o, V3 d, V3 L, double rad,
                                         double& best, int& besti, V3& hit, bool& hin, double& total, uint32_t& err,
-                                        bool xr) {
+                                        bool xr, int light = -1) {
   const SceneDev& S = p.scene;
+  if (SPH == SPH_BVH_LDSX && !ext && !xr && light >= 0 && p.lds_lbuf >= 0) {   // the light buffer's cell (§3.18)
+    int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
+    double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
+    const uint16_t* lb = reinterpret_cast<const uint16_t*>(lds + p.lds_lbuf) + (size_t)light * S.lbuf_stride;
+    if (query_lbuf<BS>(S, lb, reinterpret_cast<const float4*>(lds + p.lds_leaf),
+                       reinterpret_cast<const Sphere64*>(lds + p.lds_x64),
+                       reinterpret_cast<const int32_t*>(lds + p.lds_xobj), cov_i, cov_v, o, d, L, rad, best, besti,
+                       hit, hin, total, err))
+      return true;
+  }
   if (SPH == SPH_LIN_LDS) {
     query<false>(S, reinterpret_cast<const float*>(lds), ext, o, d, L, rad, best, besti, hit, hin, total, err,
                  nullptr, xr);
@@ -742,7 +757,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
       int bi2 = -1;
       V3 h2 = qo;
       bool in2 = true;
-      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL, XR);
+      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL, XR, li);
       const double area = tot > 0 ? tot : 0.0;
       if (area > 0) {
         nl++;
@@ -1019,7 +1034,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
       int bi2 = -1;
       V3 h2 = qo;
       bool in2 = true;
-      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL, XR);
+      lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, errL, XR, li);
       const double area = tot > 0 ? tot : 0.0;
       if (area > 0) {
         nl++;
@@ -1841,6 +1856,14 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
       q.lds_ring = (int32_t)ring;
       lds = need_small;
       kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, xr, q.lv_sort && level + 1 >= q.lv_sort);
+    }
+  }
+  // the light buffer (§3.18) after the rings, when it fits: the shadow walks read their cell's leaves
+  if constexpr (SPH == SPH_BVH_LDSX) if (kind == 0 && q.lv_lbuf && q.scene.lbuf) {
+    const size_t at = (lds + 15) & ~(size_t)15, bytes = (size_t)q.scene.lbuf_stride * q.scene.n_light * 2;
+    if (at + bytes <= LDS_TOTAL_BYTES) {
+      q.lds_lbuf = (int32_t)at;
+      lds = at + bytes;
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)

@@ -58,6 +58,7 @@ constexpr int BVH_LEAF = 4;
 constexpr float CULL_M = 2e-5f;            // pre-test margin (exact culls)
 constexpr int32_t BVH_NONE = 0x7fffffff;
 constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); more -> ordered re-walk
+constexpr size_t LBUF_MAX_WORDS = 8192;   // light buffer, all lights: at most 16 KB (staged in LDS next to the hit ring)
 struct Bvh4Node {
   float lh[3][4][2];      // [axis][child] = {lo, hi}: both slab planes of an axis in one 8-byte pair
                           // (one packed FP32 FMA, v_pk_fma_f32, gives both slab distances)
@@ -130,6 +131,10 @@ struct SceneDev {
   float q_err;            // bound on |decoded - true| of a 16-bit record's center and radius (exact_raises' band)
   // box of every sphere (float32, rounded outwards): center and half extents (exact_raises' cone bound)
   float root_c[3], root_h[3];
+  // light buffer (null when not built): per light lbuf_stride
+  // uint16 words, 6 lbuf_n^2 + 1 cell offsets, then the cells' leaf references
+  const uint16_t* lbuf;
+  int32_t lbuf_n, lbuf_stride;
 };
 
 struct CameraDev {

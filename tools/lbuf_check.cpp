@@ -1,0 +1,162 @@
+// Host-only check of the light buffer (tests/test_lbuf.py).
+// stdin: "light x y z" lines, then "x y z r" sphere lines.  Builds the
+// hierarchy as rtx_scene_upload does (binned SAH) and the light buffer
+// (build_light_buffer, cells per face side argv[1]), then for argv[2] random
+// shadow-ray targets T per light (in and around the spheres' box, on and just
+// off the spheres' surfaces, next to the light) finds every sphere within R of
+// the segment [T, L] in binary64 (a superset of the spheres whose cover the
+// reference counts) and checks that its leaf is listed in the cell the device
+// looks up (query_lbuf's float32 arithmetic, restated below).  Prints the
+// number of targets, of covering spheres and of misses (must be 0).
+#include <math.h>
+#include <stdio.h>
+
+#include <iostream>
+#include <random>
+#include <string>
+
+#include "../raytracing_rb_amd/csrc/rtx_bvh_build.h"
+
+using namespace rtx;
+
+namespace {
+
+// query_lbuf's cell of v = T - L (float32, the device's operations)
+int device_cell(float vx, float vy, float vz, int n) {
+  const float ax = fabsf(vx), ay = fabsf(vy), az = fabsf(vz);
+  int face;
+  float m, fs, ft;
+  if (ax >= ay && ax >= az) {
+    face = vx < 0.0f ? 1 : 0, m = ax, fs = vy, ft = vz;
+  } else if (ay >= az) {
+    face = vy < 0.0f ? 3 : 2, m = ay, fs = vz, ft = vx;
+  } else {
+    face = vz < 0.0f ? 5 : 4, m = az, fs = vx, ft = vy;
+  }
+  if (!(m > 0.0f)) return -1;
+  const float h = 0.5f * (float)n / m;
+  const int i = std::min(std::max((int)floorf(fmaf(fs, h, 0.5f * (float)n)), 0), n - 1);
+  const int j = std::min(std::max((int)floorf(fmaf(ft, h, 0.5f * (float)n)), 0), n - 1);
+  return (face * n + i) * n + j;
+}
+
+// distance from C to the segment [A, B] (binary64)
+double seg_dist(const double A[3], const double B[3], const double C[3]) {
+  double ab[3], ac[3];
+  for (int a = 0; a < 3; a++) ab[a] = B[a] - A[a], ac[a] = C[a] - A[a];
+  const double dd = ab[0] * ab[0] + ab[1] * ab[1] + ab[2] * ab[2];
+  double t = dd > 0 ? (ac[0] * ab[0] + ac[1] * ab[1] + ac[2] * ab[2]) / dd : 0.0;
+  t = std::min(1.0, std::max(0.0, t));
+  double e = 0.0;
+  for (int a = 0; a < 3; a++) {
+    const double q = A[a] + t * ab[a] - C[a];
+    e += q * q;
+  }
+  return sqrt(e);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 16;
+  const int per_light = argc > 2 ? atoi(argv[2]) : 100000;
+  std::vector<double> lp;
+  std::vector<Sphere64> s64;
+  std::vector<float> s32;
+  std::vector<int32_t> obj;
+  std::string tok;
+  while (std::cin >> tok) {
+    if (tok == "light") {
+      double x, y, z;
+      std::cin >> x >> y >> z;
+      lp.insert(lp.end(), {x, y, z});
+      continue;
+    }
+    Sphere64 s;
+    s.c[0] = std::stod(tok);
+    std::cin >> s.c[1] >> s.c[2] >> s.r;
+    s64.push_back(s);
+    for (float v : {(float)s.c[0], (float)s.c[1], (float)s.c[2], (float)(s.r * s.r)}) s32.push_back(v);
+    obj.push_back((int)obj.size());
+  }
+  std::vector<BSph> bs(s64.size());
+  for (size_t k = 0; k < s64.size(); k++) {
+    for (int a = 0; a < 3; a++) bs[k].c[a] = s64[k].c[a];
+    bs[k].r = s64[k].r;
+    bs[k].rec = (int)k;
+  }
+  Bvh4Builder bb{bs, s64, s32, obj};
+  bb.sah = true;
+  const int root = bs.empty() ? BVH_NONE : bb.build(0, (int)bs.size(), 0);
+  const int nl = (int)lp.size() / 3;
+  const LightBuffer lb = build_light_buffer(bb, root, reinterpret_cast<const double(*)[3]>(lp.data()), nl, n, 1u << 30);
+  if (!lb.n) {
+    printf("no light buffer\n");
+    return 1;
+  }
+  // sphere -> its leaf reference
+  std::vector<int32_t> leaf_of(s64.size(), BVH_NONE);
+  auto note = [&](int32_t ref) {
+    const int v = ~ref, slot0 = (v >> 2) * BVH_LEAF, cnt = (v & 3) + 1;
+    for (int u = 0; u < cnt; u++) {
+      const int rec = bb.slot_obj[(size_t)slot0 + u];
+      if (rec >= 0) leaf_of[(size_t)rec] = ref;
+    }
+  };
+  if (root < 0 && root != BVH_NONE) note(root);
+  for (const Bvh4Node& nd : bb.nodes)
+    for (int k = 0; k < 4; k++)
+      if (nd.child[k] < 0 && nd.child[k] != BVH_NONE) note(nd.child[k]);
+  double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  for (const Sphere64& s : s64)
+    for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], s.c[a] - s.r), hi[a] = std::max(hi[a], s.c[a] + s.r);
+  std::mt19937_64 rng(12345);
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  long targets = 0, covers = 0, misses = 0;
+  for (int li = 0; li < nl; li++) {
+    const double* L = &lp[3 * li];
+    const uint16_t* blk = lb.words.data() + (size_t)lb.stride * li;
+    const uint16_t* ent = blk + 6 * n * n + 1;
+    for (int k = 0; k < per_light; k++) {
+      double T[3];
+      const int kind = k % 4;
+      if (kind == 0 || s64.empty()) {                 // the box and around it
+        for (int a = 0; a < 3; a++) {
+          const double w = hi[a] - lo[a] + 1.0;
+          T[a] = lo[a] - 0.5 * w + 2.0 * w * U(rng);
+        }
+      } else if (kind <= 2) {                         // on or just off a sphere (shading targets)
+        const Sphere64& s = s64[(size_t)(U(rng) * s64.size()) % s64.size()];
+        double u[3], r2 = 0;
+        do {
+          r2 = 0;
+          for (int a = 0; a < 3; a++) u[a] = 2 * U(rng) - 1, r2 += u[a] * u[a];
+        } while (r2 > 1 || r2 < 1e-6);
+        const double off = kind == 1 ? 1e-5 : (U(rng) - 0.5) * 1e-3;
+        for (int a = 0; a < 3; a++) T[a] = s.c[a] + u[a] / sqrt(r2) * (s.r + off);
+      } else {                                        // near the light
+        for (int a = 0; a < 3; a++) T[a] = L[a] + (2 * U(rng) - 1) * 0.5;
+      }
+      const double d[3] = {L[0] - T[0], L[1] - T[1], L[2] - T[2]};
+      // the device's float images: d = L - T rounded, v = -d
+      const int cell = device_cell(-(float)d[0], -(float)d[1], -(float)d[2], n);
+      if (cell < 0) continue;                         // (the device walks the hierarchy)
+      targets++;
+      for (size_t si = 0; si < s64.size(); si++) {
+        if (!(seg_dist(T, L, s64[si].c) <= s64[si].r * (1 + 1e-9))) continue;
+        covers++;
+        bool found = false;
+        for (int e = blk[cell]; e < blk[cell + 1] && !found; e++) found = (int32_t)(int16_t)ent[e] == leaf_of[si];
+        if (!found) {
+          misses++;
+          if (misses < 10)
+            fprintf(stderr, "miss: light %d T (%.17g %.17g %.17g) sphere %zu cell %d\n", li, T[0], T[1], T[2], si, cell);
+        }
+      }
+    }
+  }
+  size_t words = 0;
+  for (int li = 0; li < nl; li++) words += lb.stride;
+  printf("n %d targets %ld covers %ld misses %ld words %zu\n", n, targets, covers, misses, words);
+  return misses ? 3 : 0;
+}
