@@ -301,16 +301,17 @@ struct LightBuffer {
 inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const double (*lpos)[3], int n_light, int n,
                                       size_t max_words) {
   LightBuffer lb;
-  if (n_light <= 0 || root == BVH_NONE) return lb;
+  if (n_light <= 0 || root == BVH_NONE || n <= 0) return lb;
   std::vector<int32_t> leaves;                     // every leaf reference of the hierarchy
   if (root < 0) leaves.push_back(root);
   for (const Bvh4Node& nd : bb.nodes)
     for (int k = 0; k < 4; k++)
       if (nd.child[k] < 0 && nd.child[k] != BVH_NONE) leaves.push_back(nd.child[k]);
-  const double DELTA = 1e-4;
+  const double DELTA = 1e-4, PI = 3.141592653589793;
   const int cells = 6 * n * n;
-  std::vector<std::vector<uint16_t>> per(n_light);
-  auto dir = [](int face, double s, double t, double v[3]) {   // a point of face `face` at (s, t)
+  const int B = n % 8 == 0 ? n / 8 : (n % 4 == 0 ? n / 4 : 1);   // cells per block side
+  const int nb = n / B;
+  auto dir = [](int face, double s, double t, double v[3]) {   // the direction of face `face` at (s, t)
     const int a = face >> 1, b = (a + 1) % 3, c = (a + 2) % 3;
     v[a] = (face & 1) ? -1.0 : 1.0;
     v[b] = s;
@@ -322,59 +323,83 @@ inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const dou
     const double d = u[0] * v[0] + u[1] * v[1] + u[2] * v[2];
     return std::acos(std::max(-1.0, std::min(1.0, d)));
   };
+  // a rectangle of face coordinates: its center direction and angular radius (from boundary samples)
+  auto region = [&](int face, double s0, double s1, double t0, double t1, double ctr[3]) {
+    dir(face, 0.5 * (s0 + s1), 0.5 * (t0 + t1), ctr);
+    double rho = 0.0;
+    for (int k = 0; k <= 8; k++) {
+      const double e = k / 8.0;
+      const double pts[4][2] = {{s0 + e * (s1 - s0), t0}, {s0 + e * (s1 - s0), t1}, {s0, t0 + e * (t1 - t0)},
+                                {s1, t0 + e * (t1 - t0)}};
+      for (const auto& q : pts) {
+        double v[3];
+        dir(face, q[0], q[1], v);
+        rho = std::max(rho, angle(ctr, v));
+      }
+    }
+    return rho * (1.0 + 1e-6);
+  };
+  std::vector<double> cctr(3 * (size_t)cells), crho(cells), bctr(3 * (size_t)6 * nb * nb), brho(6 * nb * nb);
+  for (int face = 0; face < 6; face++) {
+    for (int i = 0; i < n; i++)
+      for (int j = 0; j < n; j++) {
+        const int cell = (face * n + i) * n + j;
+        crho[cell] = region(face, -1.0 + 2.0 * i / n, -1.0 + 2.0 * (i + 1) / n, -1.0 + 2.0 * j / n,
+                            -1.0 + 2.0 * (j + 1) / n, &cctr[3 * (size_t)cell]);
+      }
+    for (int bi = 0; bi < nb; bi++)
+      for (int bj = 0; bj < nb; bj++) {
+        const int blk = (face * nb + bi) * nb + bj;
+        brho[blk] = region(face, -1.0 + 2.0 * bi * B / n, -1.0 + 2.0 * (bi + 1) * B / n, -1.0 + 2.0 * bj * B / n,
+                           -1.0 + 2.0 * (bj + 1) * B / n, &bctr[3 * (size_t)blk]);
+      }
+  }
+  auto within = [&](const double u[3], const double* c, double lim) {   // angle(u, c) <= lim
+    if (lim >= PI) return true;
+    return u[0] * c[0] + u[1] * c[1] + u[2] * c[2] >= std::cos(lim);
+  };
+  std::vector<std::vector<uint16_t>> per(n_light);
   for (int li = 0; li < n_light; li++) {
     const double* L = lpos[li];
-    // each sphere's disc: (direction, half-angle), or "everywhere"
-    struct Disc { double u[3], alpha; bool all; };
-    std::vector<std::vector<Disc>> discs(leaves.size());
+    std::vector<std::vector<int>> in_cell(cells);   // leaf numbers per cell, ascending
     for (size_t f = 0; f < leaves.size(); f++) {
       const int v = ~leaves[f], slot0 = (v >> 2) * BVH_LEAF, cnt = (v & 3) + 1;
+      std::vector<char> mark(cells, 0);
       for (int u = 0; u < cnt; u++) {
         const Sphere64& sp = bb.slot64[(size_t)slot0 + u];
         if (!(sp.r >= 0.0)) continue;
-        Disc dc{};
         const double w[3] = {sp.c[0] - L[0], sp.c[1] - L[1], sp.c[2] - L[2]};
         const double D = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         const double scale = std::fabs(L[0]) + std::fabs(L[1]) + std::fabs(L[2]) + std::fabs(sp.c[0]) +
                              std::fabs(sp.c[1]) + std::fabs(sp.c[2]) + sp.r;
-        dc.all = !(D > sp.r * (1.0 + 1e-9) + 1e-12 * scale) || !std::isfinite(D);
-        if (!dc.all) {
-          for (int k = 0; k < 3; k++) dc.u[k] = w[k] / D;
-          dc.alpha = std::asin(std::min(1.0, sp.r / D));
+        if (!(D > sp.r * (1.0 + 1e-9) + 1e-12 * scale) || !std::isfinite(D)) {   // the light in or on it
+          std::fill(mark.begin(), mark.end(), 1);
+          continue;
         }
-        discs[f].push_back(dc);
+        const double du[3] = {w[0] / D, w[1] / D, w[2] / D};
+        const double alpha = std::asin(std::min(1.0, sp.r / D)) + 2.0 * DELTA;
+        for (int face = 0; face < 6; face++)
+          for (int bi = 0; bi < nb; bi++)
+            for (int bj = 0; bj < nb; bj++) {
+              const int blk = (face * nb + bi) * nb + bj;
+              if (!within(du, &bctr[3 * (size_t)blk], alpha + brho[blk])) continue;
+              for (int i = bi * B; i < (bi + 1) * B; i++)
+                for (int j = bj * B; j < (bj + 1) * B; j++) {
+                  const int cell = (face * n + i) * n + j;
+                  if (!mark[cell] && within(du, &cctr[3 * (size_t)cell], alpha + crho[cell])) mark[cell] = 1;
+                }
+            }
       }
+      for (int cell = 0; cell < cells; cell++)
+        if (mark[cell]) in_cell[cell].push_back((int)f);
     }
     std::vector<uint16_t> off(cells + 1, 0);
     std::vector<uint16_t> list;
-    for (int face = 0; face < 6; face++)
-      for (int i = 0; i < n; i++)
-        for (int j = 0; j < n; j++) {
-          const double s0 = -1.0 + 2.0 * i / n, s1 = -1.0 + 2.0 * (i + 1) / n;
-          const double t0 = -1.0 + 2.0 * j / n, t1 = -1.0 + 2.0 * (j + 1) / n;
-          double ctr[3];
-          dir(face, 0.5 * (s0 + s1), 0.5 * (t0 + t1), ctr);
-          double rho = 0.0;                          // the cell's angular radius about its center (boundary samples)
-          for (int k = 0; k <= 8; k++) {
-            const double e = k / 8.0;
-            const double pts[4][2] = {{s0 + e * (s1 - s0), t0}, {s0 + e * (s1 - s0), t1}, {s0, t0 + e * (t1 - t0)},
-                                      {s1, t0 + e * (t1 - t0)}};
-            for (const auto& q : pts) {
-              double v[3];
-              dir(face, q[0], q[1], v);
-              rho = std::max(rho, angle(ctr, v));
-            }
-          }
-          const int cell = (face * n + i) * n + j;
-          off[cell] = (uint16_t)list.size();
-          for (size_t f = 0; f < leaves.size(); f++) {
-            bool hit = false;
-            for (const Disc& dc : discs[f])
-              if (dc.all || angle(dc.u, ctr) <= dc.alpha + rho * (1.0 + 1e-6) + 2.0 * DELTA) hit = true;
-            if (hit) list.push_back((uint16_t)(int16_t)leaves[f]);
-          }
-          if (list.size() > 65535) return LightBuffer{};
-        }
+    for (int cell = 0; cell < cells; cell++) {
+      off[cell] = (uint16_t)list.size();
+      for (int f : in_cell[cell]) list.push_back((uint16_t)(int16_t)leaves[(size_t)f]);
+      if (list.size() > 65535) return LightBuffer{};
+    }
     off[cells] = (uint16_t)list.size();
     per[li] = off;
     per[li].insert(per[li].end(), list.begin(), list.end());

@@ -633,11 +633,14 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
     std::vector<double> lp(3 * (size_t)std::max(1, sd->n_lights));
     for (int i = 0; i < sd->n_lights; i++)
       for (int a = 0; a < 3; a++) lp[3 * i + a] = lights[i].pos[a];
+    // small scenes: a table for LDS (<= 16 KB); larger ones: a finer one read
+    // from global memory (<= 512 KB, L2-resident; C4: 96 cells per face side)
     LightBuffer lb;
-    if (sph64.size() <= 512 && sd->n_lights > 0)
-      for (int n : {24, 16, 12, 8}) {
+    const bool small = sph64.size() <= 512;
+    if (sd->n_lights > 0 && !sph64.empty())
+      for (int n : small ? std::vector<int>{24, 16, 12, 8} : std::vector<int>{96, 64, 48, 32, 24}) {
         lb = build_light_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), sd->n_lights, n,
-                                LBUF_MAX_WORDS);
+                                small ? LBUF_MAX_WORDS : LBUF_MAX_WORDS_GLOBAL);
         if (lb.n) break;
       }
     if (lb.n) {

@@ -416,7 +416,9 @@ __device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V
                                         double& best, int& besti, V3& hit, bool& hin, double& total, uint32_t& err,
                                         bool xr, int light = -1) {
   const SceneDev& S = p.scene;
-  if (SPH == SPH_BVH_LDSX && !ext && !xr && light >= 0 && p.lds_lbuf >= 0) {   // the light buffer's cell (§3.18)
+  // the light buffer's cell (§3.18): staged in LDS with the sphere records
+  // (SPH_BVH_LDSX), read from global memory beside C4's 16-bit leaves
+  if (SPH == SPH_BVH_LDSX && !ext && !xr && light >= 0 && p.lds_lbuf >= 0) {
     int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
     double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
     const uint16_t* lb = reinterpret_cast<const uint16_t*>(lds + p.lds_lbuf) + (size_t)light * S.lbuf_stride;
@@ -424,6 +426,15 @@ __device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V
                        reinterpret_cast<const Sphere64*>(lds + p.lds_x64),
                        reinterpret_cast<const int32_t*>(lds + p.lds_xobj), cov_i, cov_v, o, d, L, rad, best, besti,
                        hit, hin, total, err))
+      return true;
+  }
+  if (SPH == SPH_BVH_QLDS && !ext && !xr && light >= 0 && p.lv_lbuf && S.lbuf) {
+    int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
+    double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
+    const QLeaf ql = {reinterpret_cast<const uint4*>(lds + p.lds_leaf), S.q_org[0], S.q_org[1], S.q_org[2],
+                      S.q_step[0], S.q_step[1], S.q_step[2], S.q_rstep};
+    if (query_lbuf<BS>(S, S.lbuf + (size_t)light * S.lbuf_stride, ql, S.bvh_sph64, S.bvh_obj, cov_i, cov_v, o, d, L,
+                       rad, best, besti, hit, hin, total, err))
       return true;
   }
   if (SPH == SPH_LIN_LDS) {

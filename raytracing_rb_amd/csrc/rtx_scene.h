@@ -59,6 +59,7 @@ constexpr float CULL_M = 2e-5f;            // pre-test margin (exact 
 constexpr int32_t BVH_NONE = 0x7fffffff;
 constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); more -> ordered re-walk
 constexpr size_t LBUF_MAX_WORDS = 8192;   // light buffer, all lights: at most 16 KB (staged in LDS next to the hit ring)
+constexpr size_t LBUF_MAX_WORDS_GLOBAL = 1 << 18;   // scenes above 512 spheres: at most 512 KB, read from global memory
 struct Bvh4Node {
   float lh[3][4][2];      // [axis][child] = {lo, hi}: both slab planes of an axis in one 8-byte pair
                           // (one packed FP32 FMA, v_pk_fma_f32, gives both slab distances)

@@ -775,6 +775,19 @@ def test_light_buffer_bit_identical(gpu, world, camera, ov):
         assert _same(_renderer(sd, cd, 1, lbuf=0, **opts).render(seed=3), lanes), opts
 
 
+def test_light_buffer_c4_global_table(gpu):
+    """C4-sized scenes read a finer table from global memory beside their 16-bit leaves."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_scenes
+    make_scenes.ensure_c4()
+    sd, cd = _scene("c4_world.yml", "c4_camera.yml", width=160, height=90, pre_sample_times=2, max_sample_times=2)
+    plain = _renderer(sd, cd, 1, lbuf=0).render(seed=6)
+    assert _same(_renderer(sd, cd, 1).render(seed=6), plain)
+    assert _same(_renderer(sd, cd, 1, lv_sort=0).render(seed=6), plain)
+    assert _same(_renderer(sd, cd, 0).render(seed=6), plain)
+
+
 def test_light_buffer_c2_full_frame_and_options(gpu):
     from raytracing_rb_amd.runtime import RtxError
     sd, cd = _scene("c2_world.yml", "c2_camera.yml")

@@ -112,7 +112,7 @@ int main(int argc, char** argv) {
     for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], s.c[a] - s.r), hi[a] = std::max(hi[a], s.c[a] + s.r);
   std::mt19937_64 rng(12345);
   std::uniform_real_distribution<double> U(0.0, 1.0);
-  long targets = 0, covers = 0, misses = 0;
+  long targets = 0, covers = 0, misses = 0, listed = 0;
   for (int li = 0; li < nl; li++) {
     const double* L = &lp[3 * li];
     const uint16_t* blk = lb.words.data() + (size_t)lb.stride * li;
@@ -142,6 +142,7 @@ int main(int argc, char** argv) {
       const int cell = device_cell(-(float)d[0], -(float)d[1], -(float)d[2], n);
       if (cell < 0) continue;                         // (the device walks the hierarchy)
       targets++;
+      listed += blk[cell + 1] - blk[cell];
       for (size_t si = 0; si < s64.size(); si++) {
         if (!(seg_dist(T, L, s64[si].c) <= s64[si].r * (1 + 1e-9))) continue;
         covers++;
@@ -157,6 +158,7 @@ int main(int argc, char** argv) {
   }
   size_t words = 0;
   for (int li = 0; li < nl; li++) words += lb.stride;
-  printf("n %d targets %ld covers %ld misses %ld words %zu\n", n, targets, covers, misses, words);
+  printf("n %d targets %ld covers %ld misses %ld words %zu listed_x100 %ld\n", n, targets, covers, misses, words,
+         targets ? 100 * listed / targets : 0);
   return misses ? 3 : 0;
 }
