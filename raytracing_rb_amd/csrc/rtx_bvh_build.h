@@ -307,6 +307,8 @@ inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const dou
   for (const Bvh4Node& nd : bb.nodes)
     for (int k = 0; k < 4; k++)
       if (nd.child[k] < 0 && nd.child[k] != BVH_NONE) leaves.push_back(nd.child[k]);
+  for (int32_t ref : leaves)
+    if (ref < -32768) return lb;                   // (the lists hold 16-bit references: at most 32,768 leaves)
   const double DELTA = 1e-4, PI = 3.141592653589793;
   const int cells = 6 * n * n;
   const int B = n % 8 == 0 ? n / 8 : (n % 4 == 0 ? n / 4 : 1);   // cells per block side
