@@ -361,12 +361,14 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          neutral on C2), "lv_ray_bytes" (bounce levels: staged ray record, 80 = origin, direction, attenuation,
          {path, root} with the RNG key decoded from the root, 96 = with a 64-bit path and the key stored; 0 [default]
          = 80 whenever (monte_carlo_diffusion_times + 3)^trace_depth <= 2^32, else 96; 80 for a camera whose paths
-         do not fit fails the render with RTX_EINVAL; same bits), "exact_raises" (1: every shadow walk of
+         do not fit fails the render with RTX_EINVAL; same bits), "exact_raises" (1 [default]: every shadow walk of
          local_lights also checks the Math.acos raise of the covers it skips, spheres whose binary cover factor is 0
          (sphere.rb:45-46), so the reference's raise is reported wherever it happens: the check
-         is part of the shadow walk (a kernel variant), which then also visits the boxes the light's cone meets;
-         0 [default]: only the covers the walk evaluates; World#high_lights' lit_area is checked either way; same
-         colours),
+         is part of the shadow walk (a kernel variant); through the light buffer, its cell's leaves get a band
+         test and a per-light raise buffer built at upload lists the rest of the raise region per direction and
+         target distance; without it (or for a target nearer the light than every object surface) the hierarchy
+         walk visits the boxes the light's cone meets; 0: only the covers the walk evaluates; World#high_lights'
+         lit_area is checked either way; same colours),
          "lv_hl_cap" (bounce levels: entries of the batch's list of highlight rays whose lit_area raise is checked
          after the levels (k_hl_raise); 0 [default] = 1/256 of the tree-record capacity, at least 4096; a ray that
          finds it full has its sample re-rendered by the lanes engine; same bits), "lv_sort" (bounce levels, fused
@@ -375,7 +377,8 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          chunks in that order, so a wave's rays start close together and point alike; records and children are
          placed as without it; 0 off, 1 / -1 [default] on; same bits), "lv_sort_from" (the first level binned;
          0 [default] = level 1 above 512 spheres, else the last level only and only in batches of at least 2^22
-         camera samples; the levels before it keep the queue order), "lv_sort_bits" (2^bits origin cells per axis of a bin, 3 or 4; 0 [default] = 4 above 512
+         camera samples; the levels before it keep the queue order; read-only "lv_sort_effective": whether the next
+         whole-frame render bins a level, "lv_sort_last": the levels per batch the last bounce-level render binned), "lv_sort_bits" (2^bits origin cells per axis of a bin, 3 or 4; 0 [default] = 4 above 512
          spheres, else 3), "lbuf" (bounce levels: 1 [default] = the shadow walks of scenes whose sphere records
          are staged in LDS (sphere mode 3) visit only the leaves listed in a per-light cube map of the spheres
          as seen from the light, built at upload, when it fits LDS next to the hit rings; 0 = the hierarchy

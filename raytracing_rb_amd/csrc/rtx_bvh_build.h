@@ -5,6 +5,7 @@
 #pragma once
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <algorithm>
 #include <cmath>
@@ -280,53 +281,31 @@ inline QuantLeaves quantize_leaves(const Bvh4Builder& bb, float sph_scale) {
   return ql;
 }
 
-// Light buffer (DESIGN.md §3.18): for each light, a cube map of 6 x n x n cells
-// around its position; cell c lists the hierarchy's leaves that hold a sphere
-// whose disc, as seen from the light, meets the cell.  A sphere that covers a
-// shadow ray's target T (World#lit_area: it crosses the segment from T to the
-// light L, short of L) meets the ray from L towards T, so its disc holds that
-// direction and its leaf is in the direction's cell: the shadow walk visits
-// those leaves only, with the same leaf tests.  The discs are widened by
-// DELTA radians, far more than the float32 cell lookup's error (the cell of
-// direction v is found on face 2a + (v_a < 0) of its dominant axis a, at
-// i = floor((s + 1) n / 2), s = v_b / |v_a|, b = (a + 1) mod 3, likewise j for
-// c = (a + 2) mod 3); a light inside or on a sphere puts that sphere's leaf in
-// every cell.  Layout per light (uint16 words, `stride` per light): 6 n n + 1
-// offsets into the light's leaf list, then the list (leaf references, int16).
-struct LightBuffer {
-  int n = 0, stride = 0;
-  std::vector<uint16_t> words;
-};
+// The cube map of directions around a light shared by the light buffer and
+// the raise buffer: 6 faces x n x n cells; the cell of direction v is on face
+// 2a + (v_a < 0) of its dominant axis a, at i = floor((s + 1) n / 2),
+// s = v_b / |v_a|, b = (a + 1) mod 3, likewise j for c = (a + 2) mod 3
+// (query_lbuf's float32 lookup).  Each cell (and each block of B x B cells)
+// keeps its center direction and its angular radius (from boundary samples).
+struct CubeCells {
+  int n = 0, cells = 0, B = 1, nb = 0;
+  std::vector<double> cctr, crho, bctr, brho;
+  static constexpr double PI = 3.141592653589793;
 
-inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const double (*lpos)[3], int n_light, int n,
-                                      size_t max_words) {
-  LightBuffer lb;
-  if (n_light <= 0 || root == BVH_NONE || n <= 0) return lb;
-  std::vector<int32_t> leaves;                     // every leaf reference of the hierarchy
-  if (root < 0) leaves.push_back(root);
-  for (const Bvh4Node& nd : bb.nodes)
-    for (int k = 0; k < 4; k++)
-      if (nd.child[k] < 0 && nd.child[k] != BVH_NONE) leaves.push_back(nd.child[k]);
-  for (int32_t ref : leaves)
-    if (ref < -32768) return lb;                   // (the lists hold 16-bit references: at most 32,768 leaves)
-  const double DELTA = 1e-4, PI = 3.141592653589793;
-  const int cells = 6 * n * n;
-  const int B = n % 8 == 0 ? n / 8 : (n % 4 == 0 ? n / 4 : 1);   // cells per block side
-  const int nb = n / B;
-  auto dir = [](int face, double s, double t, double v[3]) {   // the direction of face `face` at (s, t)
+  static void dir(int face, double s, double t, double v[3]) {   // the direction of face `face` at (s, t)
     const int a = face >> 1, b = (a + 1) % 3, c = (a + 2) % 3;
     v[a] = (face & 1) ? -1.0 : 1.0;
     v[b] = s;
     v[c] = t;
     const double r = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
     for (int k = 0; k < 3; k++) v[k] /= r;
-  };
-  auto angle = [](const double u[3], const double v[3]) {
+  }
+  static double angle(const double u[3], const double v[3]) {
     const double d = u[0] * v[0] + u[1] * v[1] + u[2] * v[2];
     return std::acos(std::max(-1.0, std::min(1.0, d)));
-  };
-  // a rectangle of face coordinates: its center direction and angular radius (from boundary samples)
-  auto region = [&](int face, double s0, double s1, double t0, double t1, double ctr[3]) {
+  }
+  // a rectangle of face coordinates: its center direction and angular radius
+  static double region(int face, double s0, double s1, double t0, double t1, double ctr[3]) {
     dir(face, 0.5 * (s0 + s1), 0.5 * (t0 + t1), ctr);
     double rho = 0.0;
     for (int k = 0; k <= 8; k++) {
@@ -340,57 +319,118 @@ inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const dou
       }
     }
     return rho * (1.0 + 1e-6);
-  };
-  std::vector<double> cctr(3 * (size_t)cells), crho(cells), bctr(3 * (size_t)6 * nb * nb), brho(6 * nb * nb);
-  for (int face = 0; face < 6; face++) {
-    for (int i = 0; i < n; i++)
-      for (int j = 0; j < n; j++) {
-        const int cell = (face * n + i) * n + j;
-        crho[cell] = region(face, -1.0 + 2.0 * i / n, -1.0 + 2.0 * (i + 1) / n, -1.0 + 2.0 * j / n,
-                            -1.0 + 2.0 * (j + 1) / n, &cctr[3 * (size_t)cell]);
-      }
-    for (int bi = 0; bi < nb; bi++)
-      for (int bj = 0; bj < nb; bj++) {
-        const int blk = (face * nb + bi) * nb + bj;
-        brho[blk] = region(face, -1.0 + 2.0 * bi * B / n, -1.0 + 2.0 * (bi + 1) * B / n, -1.0 + 2.0 * bj * B / n,
-                           -1.0 + 2.0 * (bj + 1) * B / n, &bctr[3 * (size_t)blk]);
-      }
   }
-  auto within = [&](const double u[3], const double* c, double lim) {   // angle(u, c) <= lim
+  explicit CubeCells(int n_) : n(n_), cells(6 * n_ * n_) {
+    B = n % 8 == 0 ? n / 8 : (n % 4 == 0 ? n / 4 : 1);   // cells per block side
+    nb = n / B;
+    cctr.resize(3 * (size_t)cells), crho.resize(cells), bctr.resize(3 * (size_t)6 * nb * nb), brho.resize(6 * nb * nb);
+    for (int face = 0; face < 6; face++) {
+      for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+          const int cell = (face * n + i) * n + j;
+          crho[cell] = region(face, -1.0 + 2.0 * i / n, -1.0 + 2.0 * (i + 1) / n, -1.0 + 2.0 * j / n,
+                              -1.0 + 2.0 * (j + 1) / n, &cctr[3 * (size_t)cell]);
+        }
+      for (int bi = 0; bi < nb; bi++)
+        for (int bj = 0; bj < nb; bj++) {
+          const int blk = (face * nb + bi) * nb + bj;
+          brho[blk] = region(face, -1.0 + 2.0 * bi * B / n, -1.0 + 2.0 * (bi + 1) * B / n, -1.0 + 2.0 * bj * B / n,
+                             -1.0 + 2.0 * (bj + 1) * B / n, &bctr[3 * (size_t)blk]);
+        }
+    }
+  }
+  static bool within(const double u[3], const double* c, double lim) {   // angle(u, c) <= lim
     if (lim >= PI) return true;
     return u[0] * c[0] + u[1] * c[1] + u[2] * c[2] >= std::cos(lim);
-  };
+  }
+  // every cell whose region comes within `lim` of direction u (blocks first)
+  template <typename F>
+  void visit(const double u[3], double lim, F&& f) const {
+    for (int face = 0; face < 6; face++)
+      for (int bi = 0; bi < nb; bi++)
+        for (int bj = 0; bj < nb; bj++) {
+          const int blk = (face * nb + bi) * nb + bj;
+          if (!within(u, &bctr[3 * (size_t)blk], lim + brho[blk])) continue;
+          for (int i = bi * B; i < (bi + 1) * B; i++)
+            for (int j = bj * B; j < (bj + 1) * B; j++) {
+              const int cell = (face * n + i) * n + j;
+              if (within(u, &cctr[3 * (size_t)cell], lim + crho[cell])) f(cell);
+            }
+        }
+  }
+  // the least angle between u and a direction of `cell` (0 when u is inside)
+  double gap(const double u[3], int cell) const {
+    return std::max(0.0, angle(u, &cctr[3 * (size_t)cell]) - crho[cell]);
+  }
+};
+
+// Every leaf reference of the hierarchy (int16 list entries: at most 8,192
+// leaves, since a reference is ~((leaf << 2) | (count - 1)) >= -32768); empty
+// when some reference does not fit.
+inline std::vector<int32_t> leaf_refs(const Bvh4Builder& bb, int root) {
+  std::vector<int32_t> leaves;
+  if (root < 0 && root != BVH_NONE) leaves.push_back(root);
+  for (const Bvh4Node& nd : bb.nodes)
+    for (int k = 0; k < 4; k++)
+      if (nd.child[k] < 0 && nd.child[k] != BVH_NONE) leaves.push_back(nd.child[k]);
+  for (int32_t ref : leaves)
+    if (ref < -32768) return {};
+  return leaves;
+}
+
+// Light buffer (DESIGN.md §3.18): for each light, a cube map of 6 x n x n cells
+// around its position; cell c lists the hierarchy's leaves that hold a sphere
+// whose disc, as seen from the light, meets the cell.  A sphere that covers a
+// shadow ray's target T (World#lit_area: it crosses the segment from T to the
+// light L, short of L) meets the ray from L towards T, so its disc holds that
+// direction and its leaf is in the direction's cell: the shadow walk visits
+// those leaves only, with the same leaf tests.  The discs are widened by
+// DELTA radians, far more than the float32 cell lookup's error (CubeCells);
+// a light inside or on a sphere puts that sphere's leaf in every cell.
+// Layout per light (uint16 words, `stride` per light): 6 n n + 1 offsets into
+// the light's leaf list, then the list (leaf references, int16).
+struct LightBuffer {
+  int n = 0, stride = 0;
+  std::vector<uint16_t> words;
+};
+
+inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const double (*lpos)[3], int n_light, int n,
+                                      size_t max_words, const double* lrad = nullptr) {
+  LightBuffer lb;
+  if (n_light <= 0 || root == BVH_NONE || n <= 0) return lb;
+  // the offsets alone must fit (skip a resolution before building it)
+  if ((size_t)(6 * n * n + 1) * (size_t)n_light > max_words) return lb;
+  const std::vector<int32_t> leaves = leaf_refs(bb, root);
+  if (leaves.empty()) return lb;
+  const double DELTA = 1e-4;
+  const CubeCells cc(n);
+  const int cells = cc.cells;
   std::vector<std::vector<uint16_t>> per(n_light);
+  size_t total = 0;
   for (int li = 0; li < n_light; li++) {
     const double* L = lpos[li];
+    const double rad_pad = lrad && std::isfinite(lrad[li]) ? std::fabs(lrad[li]) : 0.0;
     std::vector<std::vector<int>> in_cell(cells);   // leaf numbers per cell, ascending
+    std::vector<char> mark(cells, 0);
     for (size_t f = 0; f < leaves.size(); f++) {
       const int v = ~leaves[f], slot0 = (v >> 2) * BVH_LEAF, cnt = (v & 3) + 1;
-      std::vector<char> mark(cells, 0);
+      std::fill(mark.begin(), mark.end(), 0);
       for (int u = 0; u < cnt; u++) {
         const Sphere64& sp = bb.slot64[(size_t)slot0 + u];
         if (!(sp.r >= 0.0)) continue;
         const double w[3] = {sp.c[0] - L[0], sp.c[1] - L[1], sp.c[2] - L[2]};
         const double D = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         const double scale = std::fabs(L[0]) + std::fabs(L[1]) + std::fabs(L[2]) + std::fabs(sp.c[0]) +
-                             std::fabs(sp.c[1]) + std::fabs(sp.c[2]) + sp.r;
-        if (!(D > sp.r * (1.0 + 1e-9) + 1e-12 * scale) || !std::isfinite(D)) {   // the light in or on it
+                             std::fabs(sp.c[1]) + std::fabs(sp.c[2]) + sp.r + rad_pad;
+        if (!(D > sp.r + 1e-6 * scale) || !std::isfinite(D)) {   // the light in, on or next to it
           std::fill(mark.begin(), mark.end(), 1);
           continue;
         }
         const double du[3] = {w[0] / D, w[1] / D, w[2] / D};
-        const double alpha = std::asin(std::min(1.0, sp.r / D)) + 2.0 * DELTA;
-        for (int face = 0; face < 6; face++)
-          for (int bi = 0; bi < nb; bi++)
-            for (int bj = 0; bj < nb; bj++) {
-              const int blk = (face * nb + bi) * nb + bj;
-              if (!within(du, &bctr[3 * (size_t)blk], alpha + brho[blk])) continue;
-              for (int i = bi * B; i < (bi + 1) * B; i++)
-                for (int j = bj * B; j < (bj + 1) * B; j++) {
-                  const int cell = (face * n + i) * n + j;
-                  if (!mark[cell] && within(du, &cctr[3 * (size_t)cell], alpha + crho[cell])) mark[cell] = 1;
-                }
-            }
+        // the disc (sin <= R / D), with the raise buffer's slack 1e-9 S / D: the
+        // cells also serve its regime (A) (build_raise_buffer)
+        const double alpha = std::asin(std::min(1.0, sp.r / D + 1e-9 * scale / D)) + 2.0 * DELTA;
+        cc.visit(du, alpha, [&](int cell) { mark[cell] = 1; });
       }
       for (int cell = 0; cell < cells; cell++)
         if (mark[cell]) in_cell[cell].push_back((int)f);
@@ -405,6 +445,8 @@ inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const dou
     off[cells] = (uint16_t)list.size();
     per[li] = off;
     per[li].insert(per[li].end(), list.begin(), list.end());
+    total += per[li].size();
+    if (total > max_words) return LightBuffer{};   // (stop once the lights so far cannot fit)
   }
   size_t stride = 0;
   for (const auto& v : per) stride = std::max(stride, v.size());
@@ -415,6 +457,220 @@ inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const dou
   lb.words.assign(stride * (size_t)n_light, 0);
   for (int li = 0; li < n_light; li++) std::copy(per[li].begin(), per[li].end(), lb.words.begin() + stride * li);
   return lb;
+}
+
+// Raise buffer: which leaves can hold a sphere whose
+// Sphere#cover_area (sphere.rb:28-57) raises Math::DomainError for a target T
+// and light (L, radius), whatever its binary factor.  The raise needs d within
+// a few ulps of |R - r1| (d: the distance of the center C from the line
+// through T and L; r1 = radius |s_T| / l, the cone's radius at C's projection,
+// s_T its signed distance from T along the line, l = |L - T|).  Let w be the
+// unit direction from L towards T, sigma = (C - L).w = D cos(theta) with
+// D = |C - L| and theta the angle of C - L from w (from -w when sigma < 0),
+// and k = radius / l.  Then d = D sin(theta) and
+//   (A) R > r1: d ~ R - r1 <= R: sin(theta) <= R / D: the line meets the ball;
+//   (B) r1 > R: d ~ r1 - R:
+//     B1, 0 <= sigma <= l: r1 = radius (l - sigma) / l:
+//         sin(theta) + k cos(theta) <= (radius - R) / D,
+//     B2, sigma > l: r1 = radius (sigma - l) / l:
+//         k cos(theta) - sin(theta) >= (radius + R) / D,
+//     BM, sigma < 0 (theta from -w): r1 = radius (l + |sigma|) / l:
+//         sin(theta) - k cos(theta) <= (radius - R) / D.
+// For a cell whose directions all lie at least g from C's direction (theta >=
+// g, theta <= pi / 2), sin + k cos is at least min(sin g + k cos g, 1), k cos
+// - sin at most k cos g - sin g, sin - k cos at least sin g - k cos g.  So,
+// with g a sphere's gap to the cell less 2 DELTA (the lookup's slack, as the
+// light buffer's), its leaf is needed in cell c
+//   for w in c: if sin g <= R / D (A: the light buffer's own cells, which use
+//     this disc), if l >= l1 = radius cos g / ((radius - R) / D - sin g) (B1),
+//     or if l <= l2 = radius cos g / (sin g + (radius + R) / D) (B2);
+//   for -w in c: if sin g <= R / D or l <= lm = radius cos g / (sin g -
+//     (radius - R) / D) (BM).
+// Every bound carries 1e-9 S / D (S: the coordinates' scale: d and r1 are
+// computed to a few ulps of S, a raise needs them within a few ulps of
+// tangency); a light within 1e-6 S of a sphere's surface puts that sphere's
+// leaf in every cell.  Thresholds below `floor` (per light) are cut: a query
+// with l < floor walks the hierarchy instead.
+// Three lists per cell (n cells per face side; the light buffer's n is a
+// multiple, and its cell's parent is looked up): B2 (needed when ql <= q,
+// sorted by q descending), B1 (ql >= q, ascending), M (ql <= q, descending;
+// q = 255: always), with ql = 16 log2(l / floor) and q the ceiling (B2, M) or
+// floor (B1) of the threshold's 16 log2(l* / floor); a query with ql > 254
+// walks the hierarchy.  Layout per light (uint32 words, `stride` per light):
+// word 0 the floor (float, rounded up), word 1 the entry count, 3 (6 n n + 1)
+// offsets (B2's cells, B1's, M's, counting entries from the list start), then
+// the entries: leaf reference (int16) << 16 | q.
+struct RaiseBuffer {
+  int n = 0, stride = 0;
+  std::vector<uint32_t> words;
+};
+
+enum { RB_B2 = 0, RB_B1 = 1, RB_M = 2, RB_LISTS = 3 };
+
+inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const double (*lpos)[3], const double* lrad,
+                                      const double* lfloor, int n_light, int n, size_t max_words,
+                                      std::vector<double>* floors_used = nullptr, bool per_sphere = false) {
+  RaiseBuffer rb;
+  if (n_light <= 0 || root == BVH_NONE || n <= 0) return rb;
+  const int cells = 6 * n * n;
+  const size_t head = 2 + (size_t)RB_LISTS * (cells + 1);
+  if (head * (size_t)n_light > max_words) return rb;
+  const std::vector<int32_t> leaves = leaf_refs(bb, root);
+  if (leaves.empty()) return rb;
+  if (per_sphere && leaves.size() * BVH_LEAF > 65536) return rb;   // (16-bit slot indices)
+  const double DELTA = 1e-4, PI = CubeCells::PI, QMAX = 254.0 / 16.0;
+  const CubeCells cc(n);
+  std::vector<std::vector<uint32_t>> per(n_light);
+  if (floors_used) floors_used->assign(n_light, 0.0);
+  size_t total = 0;
+  auto as = [PI](double x) { return x >= 1.0 ? PI / 2 : (x <= 0.0 ? 0.0 : std::asin(x)); };
+  for (int li = 0; li < n_light; li++) {
+    const double* L = lpos[li];
+    const double rad = lrad[li];
+    double floor_l = std::max(0.0, lfloor[li]);
+    if (!(floor_l > 1e-6 * rad)) floor_l = 1e-6 * rad;
+    std::vector<uint32_t> blk;
+    for (int attempt = 0; attempt < 32; attempt++, floor_l *= 2.0) {
+      blk.clear();
+      if (!(rad > 0.0) || !std::isfinite(rad)) {      // a point light: no cover_area raises (r1 = 0)
+        blk.assign(head, 0);
+        break;
+      }
+      auto q_up = [&](double l2) -> uint32_t {        // ceil(16 log2(l2 / floor)), 255: always
+        if (!(l2 < floor_l * std::exp2(QMAX))) return 255u;
+        const double q = std::ceil(16.0 * std::log2(std::max(l2 * (1.0 + 1e-4) / floor_l, 1.0)));
+        return (uint32_t)std::min(254.0, q);
+      };
+      auto q_dn = [&](double l1) -> uint32_t {        // floor(16 log2(l1 / floor)), 255: never
+        if (!(l1 < floor_l * std::exp2(QMAX))) return 255u;
+        if (!(l1 * (1.0 - 1e-4) > floor_l)) return 0u;
+        return (uint32_t)std::max(0.0, std::floor(16.0 * std::log2(l1 * (1.0 - 1e-4) / floor_l)));
+      };
+      // per cell: the leaf's combined thresholds (B2 and M: the largest, B1: the least)
+      std::vector<std::vector<uint32_t>> lst[RB_LISTS];
+      for (auto& v : lst) v.assign(cells, {});
+      std::vector<double> t2(cells, -1.0), t1(cells, INFINITY), tm(cells, -1.0);
+      std::vector<int> touched;
+      std::vector<char> seen(cells, 0);
+      // entries per sphere (slot index), or per leaf (reference): the device's choice
+      const size_t units = per_sphere ? leaves.size() * BVH_LEAF : leaves.size();
+      for (size_t f = 0; f < units; f++) {
+        const int lf = (int)(per_sphere ? f / BVH_LEAF : f);
+        const int v = ~leaves[lf], slot0 = (v >> 2) * BVH_LEAF, cnt0 = (v & 3) + 1;
+        const int u0 = per_sphere ? (int)(f % BVH_LEAF) : 0, cnt = per_sphere ? (u0 < cnt0 ? u0 + 1 : 0) : cnt0;
+        touched.clear();
+        auto note = [&](int cell, double l2, double l1, double lm) {
+          if (!seen[cell]) seen[cell] = 1, touched.push_back(cell);
+          t2[cell] = std::max(t2[cell], l2);
+          t1[cell] = std::min(t1[cell], l1);
+          tm[cell] = std::max(tm[cell], lm);
+        };
+        for (int u = u0; u < cnt; u++) {
+          const Sphere64& sp = bb.slot64[(size_t)slot0 + u];
+          if (!(sp.r >= 0.0)) continue;
+          const double R = sp.r;
+          const double w[3] = {sp.c[0] - L[0], sp.c[1] - L[1], sp.c[2] - L[2]};
+          const double D = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+          const double scale = std::fabs(L[0]) + std::fabs(L[1]) + std::fabs(L[2]) + std::fabs(sp.c[0]) +
+                               std::fabs(sp.c[1]) + std::fabs(sp.c[2]) + R + rad;
+          if (!(D > R + 1e-6 * scale) || !std::isfinite(D)) {   // the light in, on or next to it: every cell
+            for (int cell = 0; cell < cells; cell++) note(cell, -1.0, INFINITY, INFINITY);
+            continue;                                 // (P: the light buffer lists it in every cell)
+          }
+          const double du[3] = {w[0] / D, w[1] / D, w[2] / D};
+          const double e = 1e-9 * scale / D;
+          const double sA = R / D + e, b1 = (rad - R) / D + e, b2 = (rad + R) / D - e;
+          const double kf = rad / floor_l;               // k at the floor: the widest reach
+          const double reach = std::max({as(sA), as(b1), as(kf), as(b1 + kf)}) + 2.0 * DELTA;
+          cc.visit(du, reach, [&](int cell) {
+            const double g = std::max(0.0, cc.gap(du, cell) - 2.0 * DELTA);
+            if (g >= PI / 2) return;
+            const double sg = std::sin(g), cg = std::cos(g);
+            const double l1 = b1 - sg > 0.0 ? rad * cg / (b1 - sg) : INFINITY;          // B1: l >= l1
+            const double l2 = sg + b2 > 0.0 ? rad * cg / (sg + b2) : INFINITY;          // B2: l <= l2
+            const double lm = sg <= sA ? INFINITY : (sg - b1 > 0.0 ? rad * cg / (sg - b1) : INFINITY);   // A / BM
+            note(cell, l2, l1, lm);
+          });
+        }
+        const uint32_t ref = per_sphere ? (uint32_t)(((~leaves[lf]) >> 2) * BVH_LEAF + (int)(f % BVH_LEAF)) << 16
+                                        : (uint32_t)(uint16_t)(int16_t)leaves[f] << 16;
+        for (int cell : touched) {
+          seen[cell] = 0;
+          if (t2[cell] >= floor_l) lst[RB_B2][cell].push_back(ref | q_up(t2[cell]));
+          const uint32_t q1 = q_dn(t1[cell]);
+          if (q1 != 255u) lst[RB_B1][cell].push_back(ref | q1);
+          if (tm[cell] >= floor_l) lst[RB_M][cell].push_back(ref | q_up(tm[cell]));
+          t2[cell] = -1.0, t1[cell] = INFINITY, tm[cell] = -1.0;
+        }
+      }
+      size_t nent = 0;
+      for (auto& v : lst)
+        for (int cell = 0; cell < cells; cell++) nent += v[cell].size();
+      if (head + nent > max_words) continue;          // too large: raise the floor
+      blk.assign(head + nent, 0);
+      float ff = (float)floor_l;
+      if ((double)ff < floor_l) ff = nextafterf(ff, INFINITY);
+      memcpy(&blk[0], &ff, 4);
+      blk[1] = (uint32_t)nent;
+      uint32_t* off = &blk[2];
+      size_t k = 0;
+      for (int t = 0; t < RB_LISTS; t++) {
+        for (int cell = 0; cell < cells; cell++) {
+          auto& v = lst[t][cell];
+          // (stable: ties keep leaf order)
+          if (t == RB_B1)
+            std::stable_sort(v.begin(), v.end(), [](uint32_t a, uint32_t b) { return (a & 255u) < (b & 255u); });
+          else
+            std::stable_sort(v.begin(), v.end(), [](uint32_t a, uint32_t b) { return (a & 255u) > (b & 255u); });
+          off[t * (cells + 1) + cell] = (uint32_t)k;
+          for (uint32_t ent : v) blk[head + k++] = ent;
+        }
+        off[t * (cells + 1) + cells] = (uint32_t)k;
+      }
+      break;
+    }
+    if (blk.empty()) return RaiseBuffer{};
+    if (floors_used) (*floors_used)[li] = floor_l;
+    total += blk.size();
+    if (total > max_words) return RaiseBuffer{};
+    per[li].swap(blk);
+  }
+  size_t stride = 0;
+  for (const auto& v : per) stride = std::max(stride, v.size());
+  stride = (stride + 3) & ~(size_t)3;               // (16-B aligned blocks)
+  if (stride * (size_t)n_light > max_words) return RaiseBuffer{};
+  rb.n = n;
+  rb.stride = (int)stride;
+  rb.words.assign(stride * (size_t)n_light, 0);
+  for (int li = 0; li < n_light; li++) std::copy(per[li].begin(), per[li].end(), rb.words.begin() + stride * li);
+  return rb;
+}
+
+// The raise buffer's gates: one word per light and raise-buffer cell, the q
+// of the first entry of each list (byte 0: B2's, 0 when empty; byte 1: B1's,
+// 255 when empty; byte 2: M's, 0 when empty).  A query reads the lists only
+// when ql <= byte 0 or ql >= byte 1 (P), or ql <= byte 2 (M): small scenes
+// stage the gates in LDS and rarely touch the lists (ql > 0 always).
+inline std::vector<uint32_t> raise_gates(const RaiseBuffer& rb, int n_light) {
+  std::vector<uint32_t> g;
+  if (!rb.n) return g;
+  const int cells = 6 * rb.n * rb.n;
+  g.assign((size_t)cells * n_light, 0);
+  for (int li = 0; li < n_light; li++) {
+    const uint32_t* blk = rb.words.data() + (size_t)rb.stride * li;
+    const uint32_t* off = blk + 2;
+    const uint32_t* ent = blk + 2 + (size_t)RB_LISTS * (cells + 1);
+    for (int c = 0; c < cells; c++) {
+      uint32_t w = 0;
+      for (int t = 0; t < RB_LISTS; t++) {
+        const uint32_t k0 = off[t * (cells + 1) + c], k1 = off[t * (cells + 1) + c + 1];
+        const uint32_t q = k1 > k0 ? (ent[k0] & 255u) : (t == RB_B1 ? 255u : 0u);
+        w |= q << (8 * t);
+      }
+      g[(size_t)cells * li + c] = w;
+    }
+  }
+  return g;
 }
 
 }  // namespace rtx

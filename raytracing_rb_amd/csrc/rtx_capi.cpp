@@ -90,7 +90,7 @@ struct rtx_context {
   int64_t opt_lv_streams = 2;        // bounce levels: P = the region's tiles in P interleaved parts on P streams at once
   int64_t opt_lv_ray_bytes = 0;      // bounce levels: staged ray record, 0 auto (80 B when every path fits 32 bits), 80, 96
   int64_t opt_lv_hl_cap = 0;         // bounce levels: deferred highlight-check list entries (0 auto)
-  int64_t opt_exact_raises = 0;      // 1: local_lights' shadow walks also check the acos raises of the covers they skip
+  int64_t opt_exact_raises = 1;      // 1 (default): local_lights' shadow walks also check the acos raises of the covers they skip (§2.4)
                                      // (C2 +10 %, C4 +108 %, r09c; so not the default)
   int64_t opt_lv_sort = -1;          // bounce levels: 1 = levels visited bin by bin (direction octant, origin cell), 0 off,
                                      // -1 auto = on
@@ -100,6 +100,7 @@ struct rtx_context {
   int64_t opt_lbuf = 1;              // bounce levels: 1 = shadow walks through the light buffer where it is staged (§3.18)
   int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
+  int64_t last_sort_levels = 0;              // levels per batch the last bounce-level render binned (lv_sort_last)
   uint32_t* d_tile_rays = nullptr;   // rtx_tile_rays: rays per 8x8 tile of the last whole-frame level render
   size_t tile_rays_n = 0;
   int32_t* d_rowtiles = nullptr;     // rtx_render_tile_list_device: the tile list on the device
@@ -248,7 +249,11 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
     *value = c->have_cam && c->have_scene ? (levels_engine(c) ? 1 : 0) : c->opt_engine;
     return RTX_OK;
   }
-  if (!strcmp(key, "lv_sort_effective")) {    // read-only: whether the next bounce-level render bins its levels
+  if (!strcmp(key, "lv_sort_last")) {         // read-only: levels per batch the last bounce-level render binned
+    *value = c->last_sort_levels;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_sort_effective")) {    // read-only: whether the next whole-frame bounce-level render bins its levels
     *value = c->have_cam && lv_sort_from(c, lv_frame_items(c)) > 0 ? 1 : 0;
     return RTX_OK;
   }
@@ -639,12 +644,14 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
 #ifndef RTX_LBUF_GLOBAL_N
 #define RTX_LBUF_GLOBAL_N 160
 #endif
+    std::vector<double> lrad(std::max(1, sd->n_lights), 0.0);
+    for (int i = 0; i < sd->n_lights; i++) lrad[i] = lights[i].radius;
     LightBuffer lb;
     const bool small = sph64.size() <= 512;
     if (sd->n_lights > 0 && !sph64.empty())
       for (int n : small ? std::vector<int>{24, 16, 12, 8} : std::vector<int>{RTX_LBUF_GLOBAL_N, 128, 96, 64, 48, 32, 24}) {
         lb = build_light_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), sd->n_lights, n,
-                                small ? LBUF_MAX_WORDS : LBUF_MAX_WORDS_GLOBAL);
+                                small ? LBUF_MAX_WORDS : LBUF_MAX_WORDS_GLOBAL, lrad.data());
         if (lb.n) break;
       }
     if (lb.n) {
@@ -652,6 +659,59 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
       S.lbuf = (const uint16_t*)ptr;
       S.lbuf_n = lb.n;
       S.lbuf_stride = lb.stride;
+      // the raise buffer (exact_raises): its cells nest in the
+      // light buffer's (small scenes: 8 per face side, gates staged in LDS;
+      // larger: 40 for C4's 160), read from global memory; each light's floor
+      // is 0.99 of the distance to the nearest object surface (targets of
+      // World#local_lights lie on surfaces; nearer ones walk the hierarchy)
+      std::vector<double> lfloor(std::max(1, sd->n_lights), 0.0);
+      for (int li = 0; li < sd->n_lights; li++) {
+        const double* L = lights[li].pos;
+        double fl = HUGE_VAL;
+        for (int k = 0; k < sd->n_objects; k++) {
+          const rtx_object_desc& o = sd->objects[k];
+          auto dist = [&](const double* p) {
+            return std::sqrt((L[0] - p[0]) * (L[0] - p[0]) + (L[1] - p[1]) * (L[1] - p[1]) + (L[2] - p[2]) * (L[2] - p[2]));
+          };
+          auto norm = [](const double* v) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); };
+          if (o.type == RTX_SPHERE) {
+            fl = std::min(fl, dist(o.center) - std::fabs(o.radius));
+          } else if (o.type == RTX_PLANE) {
+            const double fn = norm(o.front);
+            fl = std::min(fl, std::fabs((L[0] - o.point[0]) * o.front[0] + (L[1] - o.point[1]) * o.front[1] +
+                                        (L[2] - o.point[2]) * o.front[2]) / fn);
+          } else {                                    // a box: within this ball of its point (box.rb:15-73)
+            const double rb = 0.5 * (std::fabs(o.width_front) * (1.0 + norm(o.front)) +
+                                     std::fabs(o.width_up) * (1.0 + norm(o.up)) + 2.0 * std::fabs(o.width_left));
+            fl = std::min(fl, dist(o.point) - rb);
+          }
+        }
+        lfloor[li] = std::isfinite(fl) ? std::max(0.0, 0.99 * fl) : 0.0;
+      }
+      RaiseBuffer rb;
+      const int want = small ? 8 : 40;
+      for (int nc = std::min(want, lb.n); nc >= 1 && !rb.n; nc--) {
+        if (lb.n % nc) continue;
+        rb = build_raise_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), lrad.data(),
+                                lfloor.data(), sd->n_lights, nc, RBUF_MAX_WORDS);
+        if (!rb.n && nc <= 8) break;
+      }
+      if (rb.n) {
+        const std::vector<uint32_t> g = raise_gates(rb, sd->n_lights);
+        const int cells = 6 * rb.n * rb.n, gs = (4 + cells + 3) & ~3;
+        std::vector<uint32_t> gw((size_t)gs * sd->n_lights, 0);
+        for (int li = 0; li < sd->n_lights; li++) {
+          gw[(size_t)gs * li] = rb.words[(size_t)rb.stride * li];   // the floor
+          std::copy(g.begin() + (size_t)cells * li, g.begin() + (size_t)cells * (li + 1), gw.begin() + (size_t)gs * li + 4);
+        }
+        HIPCHK(c, up(rb.words.data(), rb.words.size() * sizeof(uint32_t), &ptr));
+        S.rbuf = (const uint32_t*)ptr;
+        HIPCHK(c, up(gw.data(), gw.size() * sizeof(uint32_t), &ptr));
+        S.rgate = (const uint32_t*)ptr;
+        S.rbuf_n = rb.n;
+        S.rbuf_stride = rb.stride;
+        S.rgate_stride = gs;
+      }
     }
   }
   S.max_distance = sd->max_distance;
@@ -833,10 +893,17 @@ static int lv_sort_from(const rtx_context* c, size_t n0) {
   const int from = c->opt_lv_sort_from > 0 ? (int)c->opt_lv_sort_from : large ? 1 : c->cam.depth - 1;
   return from >= 1 && from < c->cam.depth ? from : 0;
 }
-// the samples of a whole-frame render's first batch (lv_sort_effective)
+// the camera samples of a whole-frame render's batch (lv_sort_effective): the
+// arithmetic of render_levels' n0, with the frame's tiles split in lv_streams
+// parts (the default two parts give C2 4,147,200 samples per batch,
+// below the 2^22 of lv_sort_from, so a single C2 frame bins nothing; the
+// bench's frames in flight render one part of 8.3 M)
 static size_t lv_frame_items(const rtx_context* c) {
-  const size_t tiles = (size_t)((c->cam.width + 7) / 8) * (size_t)((c->cam.height + 7) / 8);
-  return std::min<size_t>((size_t)c->opt_lv_batch, tiles * 64 * (size_t)std::max(1, c->cam.pre));
+  const int64_t tiles = (int64_t)((c->cam.width + 7) / 8) * ((c->cam.height + 7) / 8);
+  const int64_t per_tile = 64 * (int64_t)std::max(1, c->cam.pre);
+  const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_streams, tiles));
+  const int64_t batch_tiles = std::max<int64_t>(1, std::min<int64_t>(c->opt_lv_batch / per_tile, (tiles + parts - 1) / parts));
+  return std::max<size_t>((size_t)(batch_tiles * per_tile), (size_t)std::max(0, c->cam.max_samples - c->cam.pre));
 }
 static int lv_sort_bits(const rtx_context* c) {
   return c->opt_lv_sort_bits ? (int)c->opt_lv_sort_bits : c->scene.n_sphere > 512 ? 4 : 3;
@@ -892,6 +959,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // level's bin list, the bin counts and cursors
   const int sort_from = lv_sort_from(c, n0);
   const bool sort = sort_from > 0;
+  c->last_sort_levels = sort ? std::max(0, c->cam.depth - sort_from) : 0;   // (read-only option lv_sort_last)
   const size_t sz_key = sort ? al256(scap * 2) : 0, sz_perm = sort ? al256(scap * 8) : 0,
                sz_bins = sort ? al256((size_t)LV_BINS * 8) : 0;
   // One buffer set per part: with lv_streams = P the region's tiles are
@@ -1502,7 +1570,7 @@ rtx_status rtx_lpt_plan(const int64_t* costs, int32_t n_tiles, int32_t nranks, i
   }
   *per_rank = (int32_t)width;
   if (!plan) return RTX_OK;                     // (a query of the width)
-  if ((size_t)cap < width) return RTX_EINVAL;
+  if (cap < 0 || (size_t)cap < width) return RTX_EINVAL;   // (a negative cap: refused, not a huge size_t)
   for (int k = 0; k < nranks; k++)
     for (size_t j = 0; j < width; j++) plan[(size_t)k * width + j] = j < lists[k].size() ? lists[k][j] : n_tiles;
   return RTX_OK;

@@ -782,25 +782,11 @@ __device__ __forceinline__ void walk_covers(const SceneDev& S, V3 o, V3 d, V3 L,
   }
 }
 
-// World#lit_area's walk through the light buffer (DESIGN.md §3.18, SceneDev::
-// lbuf; lb: this light's block): planes and boxes first, then only the leaves
-// listed in the cell of the direction from the light towards o, each with the
-// hierarchy walk's own leaf test (walk_leaf), then the ordered cover sum.  Every
-// sphere that covers o lies in a listed leaf (the cell holds the direction of
-// its crossing point as seen from the light), and the covers are summed in
-// object order, so the result is the hierarchy walk's.  false: no usable cell
-// (a non-finite or zero ray); the caller walks the hierarchy.
-template <int BS, typename LP, typename XP, typename OP>
-__device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb, LP leaf4, XP x64, OP xobj, int* ci,
-                                           double* cv, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
-                                           V3& bhit, bool& bin, double& total, uint32_t& err) {
-  const SlabRay s = slab_setup(S, o, d);
-  if (!s.fin) return false;
-  // the cube-map cell of v = o - L = -d: face 2a + (v_a < 0) of the dominant
-  // axis a, cell (floor((v_b / |v_a| + 1) n / 2), likewise for c), b = a + 1, c = a + 2 (mod 3)
-  const float vx = -s.dx, vy = -s.dy, vz = -s.dz;
+// The light buffer's cube-map cell of direction v (float32):
+// face 2a + (v_a < 0) of the dominant axis a, cell (floor((v_b / |v_a| + 1) n
+// / 2), likewise for c), b = a + 1, c = a + 2 (mod 3).  -1: no usable cell.
+__device__ __forceinline__ int lbuf_cell(float vx, float vy, float vz, int n, int& face, int& i, int& j) {
   const float ax = fabsf(vx), ay = fabsf(vy), az = fabsf(vz);
-  int face;
   float m, fs, ft;
   if (ax >= ay && ax >= az) {
     face = vx < 0.0f ? 1 : 0, m = ax, fs = vy, ft = vz;
@@ -809,12 +795,123 @@ __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb
   } else {
     face = vz < 0.0f ? 5 : 4, m = az, fs = vx, ft = vy;
   }
-  if (!(m > 0.0f)) return false;
-  const int n = S.lbuf_n;
+  if (!(m > 0.0f)) return -1;
   const float h = 0.5f * (float)n / m;
-  const int i = min(max((int)floorf(__builtin_fmaf(fs, h, 0.5f * (float)n)), 0), n - 1);
-  const int j = min(max((int)floorf(__builtin_fmaf(ft, h, 0.5f * (float)n)), 0), n - 1);
-  const int cell = (face * n + i) * n + j;
+  i = min(max((int)floorf(__builtin_fmaf(fs, h, 0.5f * (float)n)), 0), n - 1);
+  j = min(max((int)floorf(__builtin_fmaf(ft, h, 0.5f * (float)n)), 0), n - 1);
+  return (face * n + i) * n + j;
+}
+
+// exact_raises through the raise buffer: the band test
+// (xr_band) of every sphere of one leaf, whatever its factor, and the binary64
+// test (penumbra_raises) of those it keeps.
+template <typename LP, typename XP>
+__device__ __forceinline__ void leaf_raises(int lf, LP leaf4, XP x64, const SlabRay& s, const XrRay& xrr, V3 o, V3 d,
+                                            double radius, uint32_t& err) {
+  const int v = ~lf;
+  const int slot0 = (v >> 2) * BVH_LEAF;
+  const int cnt = (v & 3) + 1;
+  float4 cx, cy, cz, cw;
+  leaf_records(leaf4, v, cx, cy, cz, cw);
+  const F2 po = {s.ox, s.ox}, poy = {s.oy, s.oy}, poz = {s.oz, s.oz};
+  const F2 pdx = {s.dx, s.dx}, pdy = {s.dy, s.dy}, pdz = {s.dz, s.dz}, pdd = {s.dd, s.dd};
+  uint32_t xkeep = 0;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const F2 X = h ? F2{cx.z, cx.w} : F2{cx.x, cx.y}, Y = h ? F2{cy.z, cy.w} : F2{cy.x, cy.y};
+    const F2 Z = h ? F2{cz.z, cz.w} : F2{cz.x, cz.y}, Wr = h ? F2{cw.z, cw.w} : F2{cw.x, cw.y};
+    const F2 ocx = X - po, ocy = Y - poy, ocz = Z - poz;
+    const F2 sq = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
+    const F2 q = __builtin_elementwise_fma(ocx, pdx, __builtin_elementwise_fma(ocy, pdy, ocz * pdz));
+    const F2 l = __builtin_elementwise_fma(sq, pdd, -(q * q));
+    xkeep |= (xr_band(xrr, s.dd, l.x, q.x, sq.x, __builtin_amdgcn_sqrtf(Wr.x)) ? 1u << (2 * h) : 0u) |
+             (xr_band(xrr, s.dd, l.y, q.y, sq.y, __builtin_amdgcn_sqrtf(Wr.y)) ? 2u << (2 * h) : 0u);
+  }
+  xkeep &= (1u << cnt) - 1u;
+  while (xkeep && !(err & 0xffu)) {
+    const int u = __builtin_ctz(xkeep);
+    xkeep &= xkeep - 1;
+    const Sphere64 sp64 = x64[slot0 + u];
+    if (penumbra_raises(v3(sp64.c[0], sp64.c[1], sp64.c[2]), sp64.r, o, d, radius)) seterr(err, ERR_DOMAIN);
+  }
+}
+
+// The raise buffer's reach for a shadow ray of light `light` (o = T, d = L -
+// T, s its float32 set-up): ql = 16 log2(l / floor), false when l lies below
+// the light's floor (or ql above 254): the caller walks the hierarchy.
+// gates: this light's gate block (floor, 3 words of padding, one word per
+// raise-buffer cell), in LDS or global memory.
+__device__ __forceinline__ bool raise_ql(const uint32_t* gates, const SlabRay& s, float& ql) {
+  const float fl = __uint_as_float(gates[0]);
+  const float ell = __builtin_amdgcn_sqrtf(s.dd);
+  ql = 16.0f * __log2f(ell * __builtin_amdgcn_rcpf(fl));
+  // (ell >= fl (1 + 1e-4) with the hardware reciprocal's 1 ulp inside the margin)
+  return ell >= fl * (1.0f + 1e-4f) && ql <= 254.0f;
+}
+
+// The raise buffer's lists (rtx_bvh_build.h build_raise_buffer): B2 and B1 at
+// the parent (raise-buffer) cell of the light buffer's cell (face, i, j) of
+// -d, M at the parent of the light buffer's cell of d, each read while its
+// entries' thresholds admit ql and only when the cell's gate opens; each
+// listed leaf gets leaf_raises.  (The light buffer's own cell, walked with
+// walk_leaf's band test, holds regime A.)
+template <typename LP, typename XP>
+__device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const uint32_t* gates, LP leaf4, XP x64,
+                                            const SlabRay& s, const XrRay& xrr, V3 o, V3 d, double radius, int face,
+                                            int i, int j, float ql, uint32_t& err) {
+  const int nu = S.lbuf_n, nc = S.rbuf_n, m = nu / nc, cells = 6 * nc * nc;
+  int mf, mi, mj;
+  if (lbuf_cell(s.dx, s.dy, s.dz, nu, mf, mi, mj) < 0) return;   // (d finite and nonzero: never)
+  const int pc = (face * nc + i / m) * nc + j / m, mc = (mf * nc + mi / m) * nc + mj / m;
+  const uint32_t gp = gates[4 + pc], gm = gates[4 + mc];
+  const bool o2 = ql <= (float)(gp & 255u), o1 = ql >= (float)((gp >> 8) & 255u), om = ql <= (float)((gm >> 16) & 255u);
+  if (!(o2 || o1 || om)) return;
+  const uint32_t* blk = S.rbuf + (size_t)light * S.rbuf_stride;
+  const uint32_t* off = blk + 2;
+  const uint32_t* ent = blk + 2 + (size_t)3 * (cells + 1);
+#pragma unroll 1
+  for (int t = 0; t < 3; t++) {
+    if (!(t == 0 ? o2 : t == 1 ? o1 : om)) continue;
+    const int c = t < 2 ? pc : mc;
+    const uint32_t k0 = off[t * (cells + 1) + c], k1 = off[t * (cells + 1) + c + 1];
+    for (uint32_t k = k0; k < k1 && !(err & 0xffu); k++) {
+      const uint32_t e = ent[k];
+      const float q = (float)(e & 255u);
+      if (t == 1 ? q > ql : q < ql) break;
+      leaf_raises((int)(int16_t)(e >> 16), leaf4, x64, s, xrr, o, d, radius, err);
+    }
+  }
+}
+
+// World#lit_area's walk through the light buffer (DESIGN.md §3.18, SceneDev::
+// lbuf; lb: this light's block): planes and boxes first, then only the leaves
+// listed in the cell of the direction from the light towards o, each with the
+// hierarchy walk's own leaf test (walk_leaf), then the ordered cover sum.  Every
+// sphere that covers o lies in a listed leaf (the cell holds the direction of
+// its crossing point as seen from the light), and the covers are summed in
+// object order, so the result is the hierarchy walk's.  With xr (exact_raises)
+// the listed leaves also get the raise band test, and the raise buffer's lists
+// the rest of World#lit_area's raise region (raise_lists; gates: this light's
+// gate block).  false: no usable cell (a non-finite or zero
+// ray), or (xr) a target nearer the light than the raise buffer's floor; the
+// caller walks the hierarchy.
+template <int BS, typename LP, typename XP, typename OP>
+__device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb, LP leaf4, XP x64, OP xobj, int* ci,
+                                           double* cv, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
+                                           V3& bhit, bool& bin, double& total, uint32_t& err, bool xr = false,
+                                           int light = 0, const uint32_t* gates = nullptr) {
+  const SlabRay s = slab_setup(S, o, d);
+  if (!s.fin) return false;
+  // the cube-map cell of v = o - L = -d
+  const int n = S.lbuf_n;
+  int face, i, j;
+  const int cell = lbuf_cell(-s.dx, -s.dy, -s.dz, n, face, i, j);
+  if (cell < 0) return false;
+  // exact_raises: a light of radius 0 never raises (r1 = 0); without the raise
+  // buffer, or below its floor, the hierarchy walk checks the cone
+  xr = xr && radius > 0.0;
+  float ql = 0.0f;
+  if (xr && !(S.rbuf && gates && raise_ql(gates, s, ql))) return false;
   const int k0 = lb[cell], k1 = lb[cell + 1];
   const uint16_t* ent = lb + 6 * n * n + 1;
   const double r = vr(d);
@@ -824,11 +921,16 @@ __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb
   float thi = 1.0f + 1e-5f + s.mS / (float)r;
   int ncov = 0;
   bool ovf = false;
+  constexpr bool Q16 = std::is_same<LP, QLeaf>::value;   // 16-bit leaf records: their decoding error
+  const float qerr = Q16 ? S.q_err : 0.0f;
   walk_planes_boxes<BS>(S, false, o, d, L, r, best, besti, bhit, bin, thi, ci, cv, ncov, ovf);
   for (int k = k0; k < k1; k++)
     walk_leaf<BS>((int)(int16_t)ent[k], leaf4, x64, xobj, s, false, o, d, dn, r, r2, L, radius, best, besti, bhit,
-                  bin, thi, err, ci, cv, ncov, ovf, false, 0.0f);
-  walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, false);
+                  bin, thi, err, ci, cv, ncov, ovf, xr, qerr);
+  if (xr) raise_lists(S, light, gates, leaf4, x64, s, xr_ray(s.Sx, s.dd, radius, qerr), o, d, radius, face, i, j, ql,
+                      err);
+  // (an overflowing cover list repeats the ordered linear walk, which checks the raises itself)
+  walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, xr);
   return true;
 }
 
@@ -1516,7 +1618,7 @@ inline size_t lds_layout(KParams& p, int mode, int bs) {
   const SceneDev& S = p.scene;
   size_t off = 0;
   if (mode == SPH_LIN_LDS) off = (size_t)(S.n_sphere + 4) * 16;
-  p.lds_x64 = p.lds_xobj = p.lds_mat = p.lds_sphr = p.lds_lbuf = -1;
+  p.lds_x64 = p.lds_xobj = p.lds_mat = p.lds_sphr = p.lds_lbuf = p.lds_rgate = -1;
   if (mode == SPH_BVH_LDS || mode == SPH_BVH_MIX || mode == SPH_BVH_LDSX || mode == SPH_BVH_QLDS) {
     off = (size_t)S.n_nodes * sizeof(Bvh4Node);
     p.lds_leaf = (int32_t)off;

@@ -64,6 +64,7 @@ struct KParams {
   int32_t lds_leaf, lds_stack, lds_cov, lds_items;
   int32_t lds_x64, lds_xobj;       // SPH_BVH_LDSX: staged Sphere64 records / object indices per leaf slot
   int32_t lds_lbuf;                // the light buffer staged in LDS (byte offset), or -1: shadow walks use the hierarchy
+  int32_t lds_rgate;               // the raise buffer's gates staged in LDS (byte offset), or -1: read from global memory
   int32_t lds_mat, lds_sphr;       // SPH_BVH_LDSX: staged materials (per object) / Sphere64 records (per sphere)
   int32_t stk_slots;               // ray-stack entries per lane kept in LDS (set by the launcher)
   int32_t stk_slots_max;           // cap (option "lds_stack"; the stack bucket by default)

@@ -403,6 +403,11 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
         const int nw = S.lbuf_stride * S.n_light / 8;
         for (int i = threadIdx.x; i < nw; i += BS) lb[i] = reinterpret_cast<const uint4*>(S.lbuf)[i];
       }
+      if (p.lds_rgate >= 0) {                 // the raise buffer's gates (rgate_stride words per light, a multiple of 4)
+        uint4* g = reinterpret_cast<uint4*>(lds + p.lds_rgate);
+        const int nw = S.rgate_stride * S.n_light / 4;
+        for (int i = threadIdx.x; i < nw; i += BS) g[i] = reinterpret_cast<const uint4*>(S.rgate)[i];
+      }
     }
     __syncthreads();
   }
@@ -418,23 +423,28 @@ __device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V
   const SceneDev& S = p.scene;
   // the light buffer's cell (§3.18): staged in LDS with the sphere records
   // (SPH_BVH_LDSX), read from global memory beside C4's 16-bit leaves
-  if (SPH == SPH_BVH_LDSX && !ext && !xr && light >= 0 && p.lds_lbuf >= 0) {
+  // exact_raises (xr): the raise buffer's gates, staged in LDS beside the light buffer or global
+  const uint32_t* gates = xr && S.rgate && light >= 0
+                              ? (p.lds_rgate >= 0 ? reinterpret_cast<const uint32_t*>(lds + p.lds_rgate)
+                                                  : S.rgate) + (size_t)light * S.rgate_stride
+                              : nullptr;
+  if (SPH == SPH_BVH_LDSX && !ext && light >= 0 && p.lds_lbuf >= 0) {
     int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
     double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
     const uint16_t* lb = reinterpret_cast<const uint16_t*>(lds + p.lds_lbuf) + (size_t)light * S.lbuf_stride;
     if (query_lbuf<BS>(S, lb, reinterpret_cast<const float4*>(lds + p.lds_leaf),
                        reinterpret_cast<const Sphere64*>(lds + p.lds_x64),
                        reinterpret_cast<const int32_t*>(lds + p.lds_xobj), cov_i, cov_v, o, d, L, rad, best, besti,
-                       hit, hin, total, err))
+                       hit, hin, total, err, xr, light, gates))
       return true;
   }
-  if (SPH == SPH_BVH_QLDS && !ext && !xr && light >= 0 && p.lv_lbuf && S.lbuf) {
+  if (SPH == SPH_BVH_QLDS && !ext && light >= 0 && p.lv_lbuf && S.lbuf) {
     int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
     double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
     const QLeaf ql = {reinterpret_cast<const uint4*>(lds + p.lds_leaf), S.q_org[0], S.q_org[1], S.q_org[2],
                       S.q_step[0], S.q_step[1], S.q_step[2], S.q_rstep};
     if (query_lbuf<BS>(S, S.lbuf + (size_t)light * S.lbuf_stride, ql, S.bvh_sph64, S.bvh_obj, cov_i, cov_v, o, d, L,
-                       rad, best, besti, hit, hin, total, err))
+                       rad, best, besti, hit, hin, total, err, xr, light, gates))
       return true;
   }
   if (SPH == SPH_LIN_LDS) {
@@ -1849,6 +1859,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   q.stk_slots_max = 0;                         // no ray stack in this engine
   size_t lds = lds_layout(q, SPH, BS);
   // exact_raises (the default) compiles the shadow walks' raise check in (k_level / k_level_c <..., XR>)
+  // (the kernels without it serve exact_raises = 0)
   const bool xr = q.exact_raises != 0;
   auto kern = kind == 0 ? (xr ? k_level<SPH, BS, true> : k_level<SPH, BS, false>)
               : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
@@ -1869,12 +1880,20 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
       kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, xr, q.lv_sort && level + 1 >= q.lv_sort);
     }
   }
-  // the light buffer (§3.18) after the rings, when it fits: the shadow walks read their cell's leaves
+  // the light buffer (§3.18) after the rings, when it fits: the shadow walks read their cell's leaves;
+  // with exact_raises the raise buffer's gates after it (§2.4), when they fit too
   if constexpr (SPH == SPH_BVH_LDSX) if (kind == 0 && q.lv_lbuf && q.scene.lbuf) {
     const size_t at = (lds + 15) & ~(size_t)15, bytes = (size_t)q.scene.lbuf_stride * q.scene.n_light * 2;
     if (at + bytes <= LDS_TOTAL_BYTES) {
       q.lds_lbuf = (int32_t)at;
       lds = at + bytes;
+      if (xr && q.scene.rgate) {
+        const size_t ga = (lds + 15) & ~(size_t)15, gb = (size_t)q.scene.rgate_stride * q.scene.n_light * 4;
+        if (ga + gb <= LDS_TOTAL_BYTES) {
+          q.lds_rgate = (int32_t)ga;
+          lds = ga + gb;
+        }
+      }
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)

@@ -722,6 +722,12 @@ def test_binned_levels_batches_overflow_schedule(gpu, opts):
         assert r.level_stats()["redo"] > 0
 
 
+def plain_r_last(sd, cd):
+    r = _renderer(sd, cd, 1, lv_sort=0)
+    r.render()
+    return r.get_option("lv_sort_last")
+
+
 def test_binned_levels_c4_and_c2_full_frame(gpu):
     """Binning on the C4 hierarchy (16-bit leaves, compact ring) and on C2 at
     full size: the same frame as without it."""
@@ -735,15 +741,21 @@ def test_binned_levels_c4_and_c2_full_frame(gpu):
     plain = _renderer(sd, cd, 1, lv_sort=0)
     assert plain.get_option("lv_sort_effective") == 0
     plain = plain.render(seed=4)
-    assert _same(auto.render(seed=4), plain)
+    assert _same(auto.render(seed=4), plain) and auto.get_option("lv_sort_last") == cd.trace_depth - 1
     assert _same(_renderer(sd, cd, 1, lv_sort=1, lv_compact=0).render(seed=4), plain)
     sd, cd = _scene("c2_world.yml", "c2_camera.yml")
     plain = _renderer(sd, cd, 1, lv_sort=0)
     assert plain.get_option("lv_sort_effective") == 0
     plain = plain.render()
-    r = _renderer(sd, cd, 1)                      # 64 spheres: the last level binned, 8^3 cells
+    assert plain_r_last(sd, cd) == 0
+    # 64 spheres: the last level binned (8^3 cells) in batches of >= 2^22 samples: one part per frame
+    # (the bench's frames in flight); the default two parts give 4,147,200 samples each, not binned
+    r = _renderer(sd, cd, 1)
+    assert r.get_option("lv_sort_effective") == 0
+    assert _same(r.render(), plain) and r.get_option("lv_sort_last") == 0
+    r = _renderer(sd, cd, 1, lv_streams=1)
     assert r.get_option("lv_sort_effective") == 1
-    assert _same(r.render(), plain)
+    assert _same(r.render(), plain) and r.get_option("lv_sort_last") == 1   # the binning ran
     r = _renderer(sd, cd, 1, lv_sort=1, lv_sort_from=1, lv_sort_bits=4)
     assert _same(r.render(), plain)
     st = r.level_stats()

@@ -7,9 +7,9 @@ calls of the reference:
   oracles and both engines.
 * World#local_lights' lit_area (world.rb:76) over spheres whose binary cover
   factor is 0 (behind the target, inside the cone off the line, beyond the
-  light): with option exact_raises = 1 the shadow walks check them (fused into
-  the walk); the default 0 reports only the covers they
-  evaluate (the departure DESIGN.md §2.3 states).
+  light): option exact_raises = 1, the default, checks them (the light buffer's
+  cell and the raise buffer's lists, or the widened hierarchy walk, DESIGN.md
+  §2.4); exact_raises = 0 reports only the covers the walks evaluate.
 
 The raising spheres are found by tools/raise_search.py (committed in
 tests/golden/raise_scenes.json): a sphere placed within a few ulps of the
@@ -322,8 +322,9 @@ def test_gpu_highlight_raise_through_trace_and_path_trace(gpu, tmp_path):
 @pytest.mark.parametrize("case", ["shadow_A", "shadow_B"])
 @pytest.mark.parametrize("fillers", [0, 40, 300])
 def test_gpu_local_lights_factor0_raise(gpu, tmp_path, case, fillers):
-    """rtx_trace (the lanes engine, every sphere walk): exact_raises = 1 reports
-    the raise of the factor-0 cover; the default returns the colour."""
+    """rtx_trace (the lanes engine, every sphere walk): the default
+    (exact_raises = 1) reports the raise of the factor-0 cover, as the oracle
+    does; exact_raises = 0 returns the colour."""
     from oracle.c_oracle import Oracle
     from raytracing_rb_amd.runtime import RtxError
     sd, cd, rays, keys = _shadow_trace(tmp_path, case, fillers=fillers)
@@ -331,9 +332,9 @@ def test_gpu_local_lights_factor0_raise(gpu, tmp_path, case, fillers):
     assert rc == 3
     for engine, opts in ENGINES:
         with pytest.raises(RtxError) as e:
-            _renderer(sd, cd, engine, exact_raises=1, **opts).trace(rays, keys)
+            _renderer(sd, cd, engine, **opts).trace(rays, keys)
         assert e.value.kind == "domain", (engine, opts)
-        fb = _renderer(sd, cd, engine, **opts).trace(rays, keys)
+        fb = _renderer(sd, cd, engine, exact_raises=0, **opts).trace(rays, keys)
         assert np.isfinite(fb).all()
 
 
@@ -342,28 +343,31 @@ def test_gpu_local_lights_factor0_raise(gpu, tmp_path, case, fillers):
 @pytest.mark.parametrize("fillers", [0, 40, 300])
 def test_gpu_local_lights_factor0_raise_in_a_render(gpu, tmp_path, case, fillers):
     """A whole render through every engine / walk / ring / split / sphere mode
-    with exact_raises = 1 (the level kernels' fused shadow-walk check,
-    DESIGN.md §2.4): the same Math::DomainError at the same first pixel as the
-    oracle; the default renders (no raise reported) and every other pixel
-    equals the oracle's frame without the raising sphere's raise."""
+    with the default exact_raises = 1 (the light buffer's cell and the raise
+    buffer's lists, or the widened hierarchy walk): the same
+    Math::DomainError at the same first pixel as the oracle.  With
+    exact_raises = 0 the frame renders, and every pixel the oracle does not
+    raise at equals the oracle's."""
     from oracle.c_oracle import Oracle
     from raytracing_rb_amd.runtime import RtxError
     sd, cd = _pixel_scene(tmp_path, case, fillers=fillers)
-    _, status, rc = Oracle(sd, cd).render()
+    out, status, rc = Oracle(sd, cd).render()
     assert rc == 3
     x, y = _first_pixel(status, 3)
+    ok = status == 0
     for engine, opts in ENGINES:
         with pytest.raises(RtxError) as e:
-            _renderer(sd, cd, engine, exact_raises=1, **opts).render()
+            _renderer(sd, cd, engine, **opts).render()
         assert e.value.kind == "domain", (engine, opts, str(e.value))
         m = re.search(r"at pixel \((\d+),(\d+)\)", str(e.value))
         assert m and (int(m.group(1)), int(m.group(2))) == (x, y), (engine, opts, str(e.value), (x, y))
-        fb = _renderer(sd, cd, engine, **opts).render()
+        fb = _renderer(sd, cd, engine, exact_raises=0, **opts).render()
         assert np.isfinite(fb).all(), (engine, opts)
+        assert np.abs(fb - out)[ok].max() <= 1e-12, (engine, opts)
     # control: without the sphere the frame renders and equals the oracle's, with the check on
     sd2, cd2 = _pixel_scene(tmp_path, case, fillers=fillers, sphere=False)
     ref, st2, rc2 = Oracle(sd2, cd2).render()
     assert rc2 == 0
     for engine, opts in ENGINES:
-        fb = _renderer(sd2, cd2, engine, exact_raises=1, **opts).render()
+        fb = _renderer(sd2, cd2, engine, **opts).render()
         assert np.abs(fb - ref).max() <= 1e-12, (engine, opts)

@@ -1,0 +1,93 @@
+// Host restatement of the device's light-buffer and raise-buffer lookups
+// (rtx_device.h query_lbuf / raise_lbuf, float32 operations), shared by
+// tools/lbuf_check.cpp (conservativeness checks) and tools/walk_sim.cpp (cost
+// predictions).  Analysis code: not product code, not the oracle.
+#pragma once
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../raytracing_rb_amd/csrc/rtx_bvh_build.h"
+
+namespace lbuf_host {
+
+// query_lbuf's cell of direction v (float32); -1: no usable cell
+inline int device_cell(float vx, float vy, float vz, int n) {
+  const float ax = fabsf(vx), ay = fabsf(vy), az = fabsf(vz);
+  int face;
+  float m, fs, ft;
+  if (ax >= ay && ax >= az) {
+    face = vx < 0.0f ? 1 : 0, m = ax, fs = vy, ft = vz;
+  } else if (ay >= az) {
+    face = vy < 0.0f ? 3 : 2, m = ay, fs = vz, ft = vx;
+  } else {
+    face = vz < 0.0f ? 5 : 4, m = az, fs = vx, ft = vy;
+  }
+  if (!(m > 0.0f)) return -1;
+  const float h = 0.5f * (float)n / m;
+  const int i = std::min(std::max((int)floorf(fmaf(fs, h, 0.5f * (float)n)), 0), n - 1);
+  const int j = std::min(std::max((int)floorf(fmaf(ft, h, 0.5f * (float)n)), 0), n - 1);
+  return (face * n + i) * n + j;
+}
+
+// The device's shadow-walk lists for a target T and light L (d = L - T in
+// binary64, as the device holds it): the light buffer's cell of -d (covers,
+// and the raise check of regime A),
+// then the raise buffer's B2 and B1 lists at that cell's parent and its M list
+// at the parent of the cell of d, each read until its early exit (B2, M: q <
+// ql; B1: q > ql; ql = 16 log2(l / floor)) and only when its gate opens.  fallback: the device walks the hierarchy instead
+// (no usable cell, l below the floor or ql above 254).
+struct Lists {
+  bool fallback = false;
+  std::vector<int32_t> cover, b2, b1, m;
+  int scanned = 0;                                  // raise-buffer entries read
+};
+
+inline Lists shadow_lists(const uint16_t* lblk, int nu, const uint32_t* rblk, const uint32_t* gates, int nc,
+                          const double d[3]) {
+  Lists r;
+  const float dx = (float)d[0], dy = (float)d[1], dz = (float)d[2];
+  const int cu = device_cell(-dx, -dy, -dz, nu), cmu = device_cell(dx, dy, dz, nu);
+  if (cu < 0 || cmu < 0) {
+    r.fallback = true;
+    return r;
+  }
+  const uint16_t* ent = lblk + 6 * nu * nu + 1;
+  for (int k = lblk[cu]; k < lblk[cu + 1]; k++) r.cover.push_back((int32_t)(int16_t)ent[k]);
+  if (!rblk) return r;
+  const float dd = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+  const float ell = sqrtf(dd);
+  float fl;
+  memcpy(&fl, &rblk[0], 4);
+  const float ql = 16.0f * log2f(ell / fl);
+  if (!(ell >= fl * (1.0f + 1e-4f)) || !(ql <= 254.0f)) {
+    r.fallback = true;
+    return r;
+  }
+  const int m = nu / nc, cells = 6 * nc * nc;
+  auto parent = [&](int c) {
+    const int face = c / (nu * nu), i = c / nu % nu, j = c % nu;
+    return (face * nc + i / m) * nc + j / m;
+  };
+  const uint32_t* off = rblk + 2;
+  const uint32_t* re = rblk + 2 + (size_t)3 * (cells + 1);
+  const int pc = parent(cu), mc = parent(cmu);
+  const uint32_t gp = gates[pc], gm = gates[mc];
+  const bool open[3] = {ql <= (float)(gp & 255u), ql >= (float)(gp >> 8 & 255u), ql <= (float)(gm >> 16 & 255u)};
+  for (int t = 0; t < 3; t++) {
+    if (!open[t]) continue;
+    const int c = t < 2 ? pc : mc;
+    for (uint32_t k = off[t * (cells + 1) + c]; k < off[t * (cells + 1) + c + 1]; k++) {
+      const uint32_t e = re[k];
+      r.scanned++;
+      const float q = (float)(e & 255u);
+      if (t == 1 ? q > ql : q < ql) break;
+      (t == 0 ? r.b2 : t == 1 ? r.b1 : r.m).push_back((int32_t)(int16_t)(e >> 16));
+    }
+  }
+  return r;
+}
+
+}  // namespace lbuf_host

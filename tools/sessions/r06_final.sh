@@ -5,4 +5,4 @@ TAG=$1
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
-bash tools/r06_shares.sh $TAG
+bash tools/sessions/r06_shares.sh $TAG

@@ -1,6 +1,6 @@
 # Round-4 GPU session: tests, smoke, variant A/B (tools/variants.py: every
 # library under _variants/), C2 bench, single-frame kernel-trace summary,
-# C4 variants.     bash tools/r07_session.sh TAG [exact]
+# C4 variants.     bash tools/sessions/r07_session.sh TAG [exact]
 #   (exact: also time option exact_raises on C2 / C4)
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 evidence session (one build, one sha):
-#   bash tools/r08_final.sh TAG a   tests, smoke, option A/B (refill), C2 PMC passes + bench + kernel traces
-#   bash tools/r08_final.sh TAG b   C4 PMC passes + bench line + single-frame kernel trace
+#   bash tools/sessions/r08_final.sh TAG a   tests, smoke, option A/B (refill), C2 PMC passes + bench + kernel traces
+#   bash tools/sessions/r08_final.sh TAG b   C4 PMC passes + bench line + single-frame kernel trace
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -2,7 +2,7 @@
 # Round-4 GPU session (C4 quantized leaves): GPU tests, C4 A/B of the sphere
 # modes (auto = SPH_BVH_QLDS vs sphere_src 2 = nodes in LDS, leaves global),
 # then the C4 PMC passes + bench line + single-frame kernel trace.
-#     bash tools/r08_session.sh TAG [nopmc]
+#     bash tools/sessions/r08_session.sh TAG [nopmc]
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

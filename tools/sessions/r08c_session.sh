@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU session (refill): the refill tests first, then every GPU test,
-# then the C2 / C4 A/B of option lv_refill (drain / save).   bash tools/r08c_session.sh TAG [notests]
+# then the C2 / C4 A/B of option lv_refill (drain / save).   bash tools/sessions/r08c_session.sh TAG [notests]
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

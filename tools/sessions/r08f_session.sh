@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 A/B of compile-time variants (tools/variants.py: every library under
-# _variants/), rounds interleaved: C2 and C4 frames alone.   bash tools/r08f_session.sh TAG
+# _variants/), rounds interleaved: C2 and C4 frames alone.   bash tools/sessions/r08f_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

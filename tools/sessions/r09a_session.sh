@@ -2,7 +2,7 @@
 # Round 5, session a: the pruned build (no refill / LDS-gathered reduction, lanes-engine stack depth as a
 # launch parameter): every GPU test, smoke, the bench line (fixture parity fields), then C2 / C4 timing of
 # the round-4 library against this one on one box (tools/variants.py: interleaved rounds, one process each).
-#   bash tools/r09a_session.sh TAG
+#   bash tools/sessions/r09a_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -3,7 +3,7 @@
 # test (the raise tests first), smoke, the bench line, then on one box: the round-4 library, the pruned
 # build without the fused check (cur) and this one (xr) on C2 and C4 (tools/variants.py), and this build
 # with exact_raises 0 / 1 (tools/timing.py, same process).
-#   bash tools/r09b_session.sh TAG
+#   bash tools/sessions/r09b_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

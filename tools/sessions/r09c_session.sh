@@ -2,7 +2,7 @@
 # Round 5, session c: the fused raise check as a compile-time kernel variant (k_level_c<..., XR>), band
 # half-width 32 float32 ulps, per-nappe cone bounds.  Raise tests, every GPU test, then C2 / C4 timing
 # with exact_raises on (default) and off in one process, and the round-4 library beside this one.
-#   bash tools/r09c_session.sh TAG
+#   bash tools/sessions/r09c_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

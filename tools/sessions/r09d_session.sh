@@ -2,7 +2,7 @@
 # Round 5, session d: exact_raises off by default (its fused check a kernel variant), rtx_render_multi_plan /
 # rtx_tile_probe / rtx_lpt_plan, the CLI's LPT split.  Every GPU test, smoke, the bench line, then C2 / C4
 # with exact_raises 0 (default) / 1 in one process, and the round-4 library beside this one on C2.
-#   bash tools/r09d_session.sh TAG
+#   bash tools/sessions/r09d_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -2,7 +2,7 @@
 # Round 5, session e: World#high_lights' lit_area raise checked inline in the level kernels with the fused
 # walk (RTX_HL_INLINE, no k_hl_raise), the walk's slab constants kept const (no scratch).  Every GPU test,
 # then C2 / C4 on one box: this build (new), the deferred k_hl_raise build (hl0) and round 4 (r4).
-#   bash tools/r09e_session.sh TAG
+#   bash tools/sessions/r09e_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

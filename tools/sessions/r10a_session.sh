@@ -3,7 +3,7 @@
 # pass per level; the wave emulator tools/wave_sim.cpp ranked it first).  The binning tests, C2 / C4
 # timing with and without it on one box, the walks' lane counters (RTX_WALKSTATS build) with and
 # without it, and a kernel trace of the binned C2 frame.
-#   bash tools/r10a_session.sh TAG
+#   bash tools/sessions/r10a_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

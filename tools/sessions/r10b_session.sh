@@ -2,7 +2,7 @@
 # Round 5, session r10b: where ray binning's time goes (r10a: C2 4.62 -> 7.72 ms although the walks'
 # wave iterations fell 18-21 %).  One part per frame (no second stream to overlap or to block the
 # binning kernels), kernel traces with and without binning, C2 and C4.
-#   bash tools/r10b_session.sh TAG
+#   bash tools/sessions/r10b_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

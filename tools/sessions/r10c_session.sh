@@ -2,7 +2,7 @@
 # Round 5, session r10c: ray binning with per-workgroup LDS histograms (r10b: the per-wave global atomics
 # took 0.5 ms per C2 level; the binned level kernels themselves were 5.6 % (C2) and 9.3 % (C4) faster).
 # Binning tests, C2 / C4 timing with and without it (default two parts), kernel traces of one part.
-#   bash tools/r10c_session.sh TAG
+#   bash tools/sessions/r10c_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

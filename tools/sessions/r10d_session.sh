@@ -2,7 +2,7 @@
 # Round 5, session r10d: ray binning, keys written by the producing level, one contiguous range of chunks per
 # binning workgroup (r10c: counting from the staged rays cost 0.1 ms per C2 level).
 # Binning tests, C2 / C4 timing with and without it (default two parts), kernel traces of one part.
-#   bash tools/r10c_session.sh TAG
+#   bash tools/sessions/r10c_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

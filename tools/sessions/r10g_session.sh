@@ -2,7 +2,7 @@
 # Round 5, session r10g: ray-bin resolution, 8^3 (cb3: 4,096 bins) against 16^3 origin cells (cb4: 32,768
 # bins, the new default; the emulator: C4 walk time 0.822 -> 0.788 of the unbinned order), same box,
 # interleaved rounds; then the binning tests on the in-tree (cb4) build.
-#   bash tools/r10g_session.sh TAG
+#   bash tools/sessions/r10g_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

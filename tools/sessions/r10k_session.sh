@@ -2,7 +2,7 @@
 # Round 5, session r10k: C2 with binning of the deep levels only (option lv_sort_from: r10b showed the
 # binned level kernels gain most on the last level, -10 %, and nothing on level 1), 32,768 bins (in-tree)
 # and 4,096 bins (_variants/librtx_cb3.so), then the binning tests.
-#   bash tools/r10k_session.sh TAG
+#   bash tools/sessions/r10k_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -2,7 +2,7 @@
 # Round 5, session r10l: binning by default everywhere (auto: C4-sized scenes every level >= 1 with 16^3
 # origin cells, small scenes the last level only with 8^3; r10k: C2 4.60 -> 4.57 ms).  Every GPU test,
 # then C2 / C4 timing of the auto policy against binning off and against the other resolution.
-#   bash tools/r10l_session.sh TAG
+#   bash tools/sessions/r10l_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

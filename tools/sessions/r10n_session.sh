@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, session r10n: the final bench line (frame latency now as one frame renders by default),
 # C4's PMC passes, bench line and single-frame kernel trace for this build.
-#   bash tools/r10n_session.sh TAG
+#   bash tools/sessions/r10n_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, session r10p: last-level binning on small shares (C2 1/8, 1/4, 1/2 of the frame, one part each as
 # the in-flight bench renders them): default (binned) against lv_sort 0, two interleaved pairs.
-#   bash tools/r10p_session.sh TAG
+#   bash tools/sessions/r10p_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -2,7 +2,7 @@
 # Round 5, session r10r: the light buffer (option lbuf, DESIGN.md §3.18: C2's shadow walks visit only the
 # leaves listed in their cube-map cell as seen from the light).  The level / raise / parity GPU tests,
 # then C2 timing with and without it (two interleaved pairs) and a single-frame kernel trace.
-#   bash tools/r10r_session.sh TAG
+#   bash tools/sessions/r10r_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, session r10s2: C4 runtime-option sweep on the final build (no rebuild): ray-bin grid,
 # static chunk share, streams, batch, light-buffer on/off.
-#   bash tools/r10s2_session.sh TAG
+#   bash tools/sessions/r10s2_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -2,7 +2,7 @@
 # Round 5, session r10s: the light buffer for C4-sized scenes (a 96 x 96-per-face table read from global
 # memory beside the 16-bit leaves; C2 keeps its LDS table).  The level / raise / parity GPU tests, then C4
 # and C2 timing with and without it.
-#   bash tools/r10s_session.sh TAG
+#   bash tools/sessions/r10s_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, session r10t: C4's global light-buffer resolution, 96 / 128 / 160 cells per face side
 # (lbuf_check: 2.0 / 1.6 / 1.4 leaves per lookup), interleaved rounds on one box.
-#   bash tools/r10t_session.sh TAG
+#   bash tools/sessions/r10t_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, session r10v: C4's PMC passes, bench line and single-frame trace for the final build, then
 # BASELINE.md's table.
-#   bash tools/r10v_session.sh TAG
+#   bash tools/sessions/r10v_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

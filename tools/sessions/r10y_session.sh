@@ -2,7 +2,7 @@
 # Round 5, session r10y: the LDS prefetch of queue-order chunks (option lv_prefetch): its parity
 # tests, then C2 whole-frame and 1/8-share timings with it off and on (interleaved).
 # (The option existed only in the build this session measured; it was reverted)
-#   bash tools/r10y_session.sh TAG
+#   bash tools/sessions/r10y_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

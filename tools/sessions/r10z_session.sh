@@ -2,7 +2,7 @@
 # Round 5, session r10z: kernel traces of the C2 frame with the LDS prefetch off and on (per-level
 # k_level_c durations), run twice each in alternation.
 # (The option existed only in the build this session measured; it was reverted)
-#   bash tools/r10z_session.sh TAG
+#   bash tools/sessions/r10z_session.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1

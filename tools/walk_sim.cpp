@@ -33,6 +33,7 @@
 #include "../raytracing_rb_amd/cli/scene_load.hpp"
 #include "../raytracing_rb_amd/csrc/rtx_bvh_build.h"
 #include "../raytracing_rb_amd/csrc/rtx_vec3.h"
+#include "lbuf_lookup.h"
 
 using namespace rtx;
 
@@ -380,6 +381,41 @@ int main(int argc, char** argv) {
   S.build(true);
   printf("scene: %zu spheres, %zu nodes, %zu slots, stack %d, q16 %d, q_err %.3g, sph_scale %.3g\n", S.sph64.size(),
          S.bb->nodes.size(), S.bb->slot_obj.size(), S.bb->stack + 1, (int)S.q16, S.q_err, S.sph_scale);
+  // the light buffer and the raise buffer (RAISE_N cells per face side, default 16)
+  const int nl = (int)S.lights.size();
+  std::vector<double> lp, lr, lf;
+  for (const rtx_light_desc& L : S.lights) {
+    lp.insert(lp.end(), {L.position[0], L.position[1], L.position[2]});
+    lr.push_back(L.radius);
+    double fl = INFINITY;                          // the nearest object surface (rtx_capi.cpp raise_floor)
+    for (const rtx_object_desc& o : S.obj) {
+      if (o.type == RTX_SPHERE) {
+        const double w[3] = {o.center[0] - L.position[0], o.center[1] - L.position[1], o.center[2] - L.position[2]};
+        fl = std::min(fl, sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) - o.radius);
+      } else if (o.type == RTX_PLANE) {
+        const double fn = sqrt(o.front[0] * o.front[0] + o.front[1] * o.front[1] + o.front[2] * o.front[2]);
+        fl = std::min(fl, fabs((L.position[0] - o.point[0]) * o.front[0] + (L.position[1] - o.point[1]) * o.front[1] +
+                               (L.position[2] - o.point[2]) * o.front[2]) / fn);
+      } else {
+        fl = 0.0;
+      }
+    }
+    lf.push_back(std::max(0.0, 0.99 * fl));
+  }
+  const int cover_n = getenv("COVER_N") ? atoi(getenv("COVER_N")) : (S.sph64.size() <= 512 ? 24 : 160);
+  const int raise_n = getenv("RAISE_N") ? atoi(getenv("RAISE_N")) : (S.sph64.size() <= 512 ? 24 : 32);
+  LightBuffer lbc = build_light_buffer(*S.bb, S.root, reinterpret_cast<const double(*)[3]>(lp.data()), nl, cover_n,
+                                       1u << 30, lr.data());
+  std::vector<double> floors;
+  RaiseBuffer rbf = build_raise_buffer(*S.bb, S.root, reinterpret_cast<const double(*)[3]>(lp.data()), lr.data(),
+                                       lf.data(), nl, raise_n, (size_t)1 << 30, &floors, getenv("PER_SPHERE") != nullptr);
+  const std::vector<uint32_t> gates = raise_gates(rbf, nl);
+  const bool flags = true;
+  printf("light buffer n %d: %d words per light; raise buffer n %d: %d words per light, floor %.4g (nearest surface "
+         "%.4g), flags %d\n",
+         lbc.n, lbc.stride, rbf.n, rbf.stride, floors.empty() ? 0.0 : floors[0], lf.empty() ? 0.0 : lf[0] / 0.99,
+         (int)flags);
+  double rs_walks = 0, rs_cover = 0, rs_p = 0, rs_m = 0, rs_fb = 0, rs_union = 0, rs_band = 0, rs_scan = 0, rs_lookups = 0;
   // camera rays (pinhole through the pixel centers of every stride-th pixel; lens jitter ignored)
   const V3 pos = v3p(cam.position), front = v3p(cam.front), up = v3p(cam.up);
   uint32_t e = 0;
@@ -427,6 +463,36 @@ int main(int argc, char** argv) {
       for (const rtx_light_desc& L : S.lights) {
         const V3 lt = vsub(v3p(L.position), T);
         for (int rr = 0; rr < NRULE; rr++) sh[rr].add(shadow_walk(S, T, lt, L.radius, (Rule)rr));
+        {                                            // light buffer / raise buffer lookups
+          const int li = (int)(&L - S.lights.data());
+          const double dl[3] = {lt.x, lt.y, lt.z};
+          rs_walks++;
+          if (lbc.n && rbf.n) {
+            const lbuf_host::Lists ls = lbuf_host::shadow_lists(lbc.words.data() + (size_t)lbc.stride * li, lbc.n,
+                                                                rbf.words.data() + (size_t)rbf.stride * li,
+                                                                gates.data() + (size_t)6 * rbf.n * rbf.n * li, rbf.n, dl);
+            if (ls.fallback) {
+              rs_fb++;
+            } else {
+              rs_cover += ls.cover.size();
+              rs_p += ls.b2.size() + ls.b1.size();
+              rs_m += ls.m.size();
+              rs_scan += ls.scanned;
+              std::vector<int32_t> un = ls.cover;
+              for (const auto* v : {&ls.b2, &ls.b1, &ls.m}) un.insert(un.end(), v->begin(), v->end());
+              if (getenv("PER_SPHERE")) {
+                for (int32_t r : ls.cover) rs_band += ((~r) & 3) + 1;
+                rs_band += ls.b2.size() + ls.b1.size() + ls.m.size();
+                un = ls.cover;
+              } else {
+                for (int32_t r : un) rs_band += ((~r) & 3) + 1;
+              }
+              std::sort(un.begin(), un.end());
+              rs_union += std::unique(un.begin(), un.end()) - un.begin();
+              rs_lookups += (ls.scanned > 0);
+            }
+          }
+        }
         // lit unless a sphere or plane crosses the segment (approximate local_lights)
         bool blocked = false;
         for (size_t i = 0; i < S.obj.size() && !blocked; i++) {
@@ -489,6 +555,10 @@ int main(int argc, char** argv) {
            tot_sh[rr].leaves / tot_sh[rr].walks, tot_sh[rr].spheres / tot_sh[rr].walks,
            tot_sh[rr].band / tot_sh[rr].walks, tot_sh[rr].band2 / tot_sh[rr].walks, tot_sh[rr].band3 / tot_sh[rr].walks,
            tot_sh[rr].leaves / tot_sh[SEG].leaves);
+  printf("light/raise buffers per shadow walk: cover leaves %.3f, raise B2+B1 %.3f, raise M %.3f, distinct leaves %.3f, "
+         "band spheres %.3f, raise entries read %.3f (walks with an open gate %.3f), hierarchy fallbacks %.5f\n",
+         rs_cover / rs_walks, rs_p / rs_walks, rs_m / rs_walks, rs_union / rs_walks, rs_band / rs_walks, rs_scan / rs_walks,
+         rs_lookups / rs_walks, rs_fb / rs_walks);
   return 0;
 }
 #endif  // WALK_SIM_NO_MAIN
