@@ -711,6 +711,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
         S.rbuf_n = rb.n;
         S.rbuf_stride = rb.stride;
         S.rgate_stride = gs;
+        S.rbuf_inv_m = (float)rb.n / (float)lb.n;   // (exact enough: (i + 0.5) m' stays 0.5 / m from an integer)
       }
     }
   }

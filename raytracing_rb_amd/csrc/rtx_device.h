@@ -859,26 +859,50 @@ template <typename LP, typename XP>
 __device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const uint32_t* gates, LP leaf4, XP x64,
                                             const SlabRay& s, const XrRay& xrr, V3 o, V3 d, double radius, int face,
                                             int i, int j, float ql, uint32_t& err) {
-  const int nu = S.lbuf_n, nc = S.rbuf_n, m = nu / nc, cells = 6 * nc * nc;
+  const int nu = S.lbuf_n, nc = S.rbuf_n, cells = 6 * nc * nc;
   int mf, mi, mj;
   if (lbuf_cell(s.dx, s.dy, s.dz, nu, mf, mi, mj) < 0) return;   // (d finite and nonzero: never)
-  const int pc = (face * nc + i / m) * nc + j / m, mc = (mf * nc + mi / m) * nc + mj / m;
+  // parent cells: i / m as (int)((i + 0.5) / m) in float32 (no integer division: i, m < 2^12, so
+  // (i + 0.5) / m lies at least 0.5 / m from an integer, far beyond the rounding)
+  const float im = S.rbuf_inv_m;
+  auto up = [im](int k) { return (int)(((float)k + 0.5f) * im); };
+  const int pc = (face * nc + up(i)) * nc + up(j), mc = (mf * nc + up(mi)) * nc + up(mj);
   const uint32_t gp = gates[4 + pc], gm = gates[4 + mc];
   const bool o2 = ql <= (float)(gp & 255u), o1 = ql >= (float)((gp >> 8) & 255u), om = ql <= (float)((gm >> 16) & 255u);
   if (!(o2 || o1 || om)) return;
   const uint32_t* blk = S.rbuf + (size_t)light * S.rbuf_stride;
   const uint32_t* off = blk + 2;
   const uint32_t* ent = blk + 2 + (size_t)3 * (cells + 1);
+  // the open lists' ranges, loaded together; then their entries four at a
+  // time (global memory: one round trip per four entries, not per entry)
+  uint32_t ka[3], kb[3];
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    const bool on = t == 0 ? o2 : t == 1 ? o1 : om;
+    const uint32_t* oc = off + t * (cells + 1) + (t < 2 ? pc : mc);
+    ka[t] = on ? oc[0] : 0u;
+    kb[t] = on ? oc[1] : 0u;
+  }
 #pragma unroll 1
   for (int t = 0; t < 3; t++) {
-    if (!(t == 0 ? o2 : t == 1 ? o1 : om)) continue;
-    const int c = t < 2 ? pc : mc;
-    const uint32_t k0 = off[t * (cells + 1) + c], k1 = off[t * (cells + 1) + c + 1];
-    for (uint32_t k = k0; k < k1 && !(err & 0xffu); k++) {
-      const uint32_t e = ent[k];
-      const float q = (float)(e & 255u);
-      if (t == 1 ? q > ql : q < ql) break;
-      leaf_raises((int)(int16_t)(e >> 16), leaf4, x64, s, xrr, o, d, radius, err);
+    uint32_t k = ka[t];
+    const uint32_t k1 = kb[t];
+    bool go = true;
+    while (go && k < k1 && !(err & 0xffu)) {
+      uint32_t e0 = ent[k], e1 = k + 1 < k1 ? ent[k + 1] : 0u, e2 = k + 2 < k1 ? ent[k + 2] : 0u,
+               e3 = k + 3 < k1 ? ent[k + 3] : 0u;
+      const uint32_t n = k1 - k < 4u ? k1 - k : 4u;
+      for (uint32_t u = 0; u < n; u++) {
+        const uint32_t e = e0;
+        e0 = e1, e1 = e2, e2 = e3;
+        const float q = (float)(e & 255u);
+        if (t == 1 ? q > ql : q < ql) {         // (sorted: the rest of the list is not needed either)
+          go = false;
+          break;
+        }
+        leaf_raises((int)(int16_t)(e >> 16), leaf4, x64, s, xrr, o, d, radius, err);
+      }
+      k += 4;
     }
   }
 }
@@ -923,15 +947,50 @@ __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb
   bool ovf = false;
   constexpr bool Q16 = std::is_same<LP, QLeaf>::value;   // 16-bit leaf records: their decoding error
   const float qerr = Q16 ? S.q_err : 0.0f;
+#ifndef RTX_DIAG_XR_NOBAND
+#define RTX_DIAG_XR_NOBAND 0       // diagnostic builds only (wrong results on raise inputs)
+#endif
+#ifndef RTX_DIAG_XR_NOLISTS
+#define RTX_DIAG_XR_NOLISTS 0      // diagnostic builds only (wrong results on raise inputs)
+#endif
   walk_planes_boxes<BS>(S, false, o, d, L, r, best, besti, bhit, bin, thi, ci, cv, ncov, ovf);
   for (int k = k0; k < k1; k++)
     walk_leaf<BS>((int)(int16_t)ent[k], leaf4, x64, xobj, s, false, o, d, dn, r, r2, L, radius, best, besti, bhit,
-                  bin, thi, err, ci, cv, ncov, ovf, xr, qerr);
-  if (xr) raise_lists(S, light, gates, leaf4, x64, s, xr_ray(s.Sx, s.dd, radius, qerr), o, d, radius, face, i, j, ql,
-                      err);
+                  bin, thi, err, ci, cv, ncov, ovf, xr && !RTX_DIAG_XR_NOBAND, qerr);
+  if (xr && !RTX_DIAG_XR_NOLISTS)
+    raise_lists(S, light, gates, leaf4, x64, s, xr_ray(s.Sx, s.dd, radius, qerr), o, d, radius, face, i, j, ql, err);
   // (an overflowing cover list repeats the ordered linear walk, which checks the raises itself)
   walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, xr);
   return true;
+}
+
+// Does World#lit_area(T, L, radius) raise (Math.acos in a cover_area,
+// DESIGN.md §2.4)?  Through the light buffer's cell of T - L (its leaves' band
+// test: regime A) and the raise buffer's lists, global memory, float32 leaf
+// records (S.bvh_sph32): the highlight check of k_hl_raise on large scenes.
+// -1: the buffers cannot serve this target (below the floor, a degenerate
+// ray): the caller walks the hierarchy (lit_area_raises).
+__device__ __forceinline__ int lit_area_raises_lbuf(const SceneDev& S, int light, V3 T, V3 L, double radius) {
+  if (!(radius > 0.0) || S.n_sphere == 0) return 0;   // as lit_area_raises
+  const V3 d = vsub(L, T);
+  const SlabRay s = slab_setup(S, T, d);
+  if (!s.fin) return -1;
+  int face, i, j;
+  const int n = S.lbuf_n;
+  const int cell = lbuf_cell(-s.dx, -s.dy, -s.dz, n, face, i, j);
+  if (cell < 0) return -1;
+  const uint32_t* gates = S.rgate + (size_t)light * S.rgate_stride;
+  float ql;
+  if (!raise_ql(gates, s, ql)) return -1;
+  const uint16_t* lb = S.lbuf + (size_t)light * S.lbuf_stride;
+  const int k0 = lb[cell], k1 = lb[cell + 1];
+  const uint16_t* ent = lb + 6 * n * n + 1;
+  const float4* leaf4 = reinterpret_cast<const float4*>(S.bvh_sph32);
+  const XrRay xrr = xr_ray(s.Sx, s.dd, radius, 0.0f);
+  uint32_t err = 0;
+  for (int k = k0; k < k1 && !err; k++) leaf_raises((int)(int16_t)ent[k], leaf4, S.bvh_sph64, s, xrr, T, d, radius, err);
+  if (!err) raise_lists(S, light, gates, leaf4, S.bvh_sph64, s, xrr, T, d, radius, face, i, j, ql, err);
+  return err ? 1 : 0;
 }
 
 // Resumable: a lane whose walk is still running when fewer than `postpone`
@@ -1516,7 +1575,7 @@ __device__ __forceinline__ bool highlight_leaves_att(const SceneDev& S, const Ra
     if (fire) {
       fired |= 1u << l;
       nfired++;
-      if (RTX_HL_RAISES && !(err & 0xffu) && raises(it.ray.o, v3(L.pos[0], L.pos[1], L.pos[2]), L.radius))
+      if (RTX_HL_RAISES && !(err & 0xffu) && raises(it.ray.o, v3(L.pos[0], L.pos[1], L.pos[2]), L.radius, l))
         seterr(err, ERR_DOMAIN);
     }
   }

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(BS, WPS) void k_render(KParams p) {
           cnt[C_HIGHLIGHT_TESTS] += S.n_light;
         }
         if (highlights(S, cur, sum, err,
-                       [&](V3 T, V3 L, double rad) { return raises_walk<SPH, BS>(p, lds, T, L, rad); }))
+                       [&](V3 T, V3 L, double rad, int) { return raises_walk<SPH, BS>(p, lds, T, L, rad); }))
           continue;
         mode = M_EXTEND;
         qo = cur.ray.o;
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void k_path_trace(KParams p) {
   uint32_t err = 0;
   V3 sum = v3(0.0, 0.0, 0.0);
   if (it.depth > 0 && !(vr(it.att) < 0.0001) &&
-      !highlights<false>(S, it, sum, err, [&](V3 T, V3 L, double rad) {
+      !highlights<false>(S, it, sum, err, [&](V3 T, V3 L, double rad, int) {
         return lit_area_raises(S, nullptr, nullptr, nullptr, (int*)nullptr, 0, T, L, rad);   // (ordered linear walk)
       })) {
     double best = S.max_distance, total = 0.0;

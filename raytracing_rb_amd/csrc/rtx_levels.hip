@@ -414,21 +414,27 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
 }
 
 // One walk (EXTEND or SHADOW) through the launch's sphere mode.
-// xr: a SHADOW walk of local_lights also checks the covers' acos raises
-// (option exact_raises, rtx_device.h xr_band).
+// xrm (option exact_raises): a SHADOW walk of local_lights
+// also checks the covers' acos raises: XR_BUF through the light buffer's cell
+// and the raise buffer's lists (a target below the floor: the ordered linear
+// walk), XR_WALK with the hierarchy walk widened to the light's cone; XR_NONE
+// not.  A kernel variant each (the launcher picks XR_BUF where both buffers
+// are in place): the widened walk's registers would cost XR_BUF's kernels.
+enum { XR_NONE = 0, XR_BUF = 1, XR_WALK = 2 };
 template <int SPH, int BS>
 __device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V3 o, V3 d, V3 L, double rad,
                                         double& best, int& besti, V3& hit, bool& hin, double& total, uint32_t& err,
-                                        bool xr, int light = -1) {
+                                        int xrm, int light = -1) {
   const SceneDev& S = p.scene;
+  const bool xr = xrm != XR_NONE && !ext;
   // the light buffer's cell (§3.18): staged in LDS with the sphere records
-  // (SPH_BVH_LDSX), read from global memory beside C4's 16-bit leaves
-  // exact_raises (xr): the raise buffer's gates, staged in LDS beside the light buffer or global
-  const uint32_t* gates = xr && S.rgate && light >= 0
+  // (SPH_BVH_LDSX), read from global memory beside C4's 16-bit leaves;
+  // exact_raises: the raise buffer's gates, staged in LDS beside the light buffer or global
+  const uint32_t* gates = xrm == XR_BUF && S.rgate && light >= 0
                               ? (p.lds_rgate >= 0 ? reinterpret_cast<const uint32_t*>(lds + p.lds_rgate)
                                                   : S.rgate) + (size_t)light * S.rgate_stride
                               : nullptr;
-  if (SPH == SPH_BVH_LDSX && !ext && light >= 0 && p.lds_lbuf >= 0) {
+  if (SPH == SPH_BVH_LDSX && !ext && xrm != XR_WALK && light >= 0 && p.lds_lbuf >= 0) {
     int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
     double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
     const uint16_t* lb = reinterpret_cast<const uint16_t*>(lds + p.lds_lbuf) + (size_t)light * S.lbuf_stride;
@@ -438,7 +444,7 @@ __device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V
                        hit, hin, total, err, xr, light, gates))
       return true;
   }
-  if (SPH == SPH_BVH_QLDS && !ext && light >= 0 && p.lv_lbuf && S.lbuf) {
+  if (SPH == SPH_BVH_QLDS && !ext && xrm != XR_WALK && light >= 0 && p.lv_lbuf && S.lbuf) {
     int* cov_i = reinterpret_cast<int*>(lds + p.lds_cov) + threadIdx.x;
     double* cov_v = reinterpret_cast<double*>(lds + p.lds_cov + COVER_K * BS * 4) + threadIdx.x;
     const QLeaf ql = {reinterpret_cast<const uint4*>(lds + p.lds_leaf), S.q_org[0], S.q_org[1], S.q_org[2],
@@ -446,6 +452,13 @@ __device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V
     if (query_lbuf<BS>(S, S.lbuf + (size_t)light * S.lbuf_stride, ql, S.bvh_sph64, S.bvh_obj, cov_i, cov_v, o, d, L,
                        rad, best, besti, hit, hin, total, err, xr, light, gates))
       return true;
+  }
+  if ((SPH == SPH_BVH_LDSX || SPH == SPH_BVH_QLDS) && xrm == XR_BUF && !ext) {
+    // XR_BUF whose buffers could not serve this target (below the raise
+    // buffer's floor, a degenerate ray): the ordered linear walk, raises checked
+    total = 1.0;
+    query<false>(S, cptr(S.sph32), false, o, d, L, rad, best, besti, hit, hin, total, err, nullptr, true);
+    return true;
   }
   if (SPH == SPH_LIN_LDS) {
     query<false>(S, reinterpret_cast<const float*>(lds), ext, o, d, L, rad, best, besti, hit, hin, total, err,
@@ -677,7 +690,7 @@ __device__ __forceinline__ void lv_finish(const KParams& p, int level, int slice
 
 // Level `level` (0 .. trace_depth-1) of one batch in one launch (option
 // lv_split = 0).  Persistent, static chunk schedule.
-template <int SPH, int BS, bool XR>
+template <int SPH, int BS, int XR>
 __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
   const SceneDev& S = p.scene;
   extern __shared__ float4 lds_sph[];
@@ -736,7 +749,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
         leafp[3 * nleaf + 1] = c.y;
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
-      }, errA, [&](V3, V3, double) {              // lit_area's raise: deferred to k_hl_raise
+      }, errA, [&](V3, V3, double, int) {         // lit_area's raise: deferred to k_hl_raise
         hl_defer = true;
         return false;
       });
@@ -748,7 +761,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
     int besti = -1;
     V3 hit = v3(0.0, 0.0, 0.0);
     bool hin = true;
-    if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL, false);
+    if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL, XR_NONE);
     const bool shade = ext && besti >= 0;
     if (RTX_STAMPS) {
       nA += __popcll(__ballot(active));
@@ -811,7 +824,7 @@ __device__ __forceinline__ void k_level_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS, bool XR>
+template <int SPH, int BS, int XR>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level(KParams p, int level) {
   k_level_body<SPH, BS, XR>(p, level);
   lv_level_done(p, level + 1);
@@ -847,7 +860,7 @@ constexpr int LV_RING_FIELDS_SMALL = 5;
 constexpr size_t LV_RING_WAVE_BYTES = (size_t)LV_RING * LV_RING_FIELDS * 8;
 constexpr size_t LV_RING_WAVE_BYTES_SMALL = (size_t)LV_RING * LV_RING_FIELDS_SMALL * 8;
 
-template <int SPH, int BS, int RF, bool LAST, bool XR, bool SORT>
+template <int SPH, int BS, int RF, bool LAST, int XR, bool SORT>
 __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   static_assert(RF == LV_RING_FIELDS || RF == LV_RING_FIELDS_SMALL, "ring layout");
   constexpr int FI = RF == LV_RING_FIELDS ? 9 : 3;   // ring field of {dense index, queue slot}
@@ -926,7 +939,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
             leafp[3 * nleaf + 1] = c.y;
             leafp[3 * nleaf + 2] = c.z;
             nleaf++;
-          }, errA, [&](V3, V3, double) {              // lit_area's raise: deferred to k_hl_raise
+          }, errA, [&](V3, V3, double, int) {         // lit_area's raise: deferred to k_hl_raise
         hl_defer = true;
         return false;
       });
@@ -937,7 +950,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         int besti = -1;
         V3 hit = v3(0.0, 0.0, 0.0);
         bool hin = true;
-        if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL, false);
+        if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL, XR_NONE);
         const bool shade = ext && besti >= 0;
         if (RTX_STAMPS) {
           nA += __popcll(__ballot(active));
@@ -1088,7 +1101,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
   }
 }
 
-template <int SPH, int BS, int RF, bool LAST, bool XR, bool SORT>
+template <int SPH, int BS, int RF, bool LAST, int XR, bool SORT>
 __global__ __launch_bounds__(BS, RTX_LVL_WPS) void k_level_c(KParams p, int level) {
   k_level_c_body<SPH, BS, RF, LAST, XR, SORT>(p, level);
   lv_level_done(p, level + 1);
@@ -1162,7 +1175,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
         leafp[3 * nleaf + 1] = c.y;
         leafp[3 * nleaf + 2] = c.z;
         nleaf++;
-      }, errA, [&](V3, V3, double) {              // lit_area's raise: deferred to k_hl_raise
+      }, errA, [&](V3, V3, double, int) {         // lit_area's raise: deferred to k_hl_raise
         hl_defer = true;
         return false;
       });
@@ -1172,7 +1185,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_trace(KParams p, int
     int besti = -1;
     V3 hit = v3(0.0, 0.0, 0.0);
     bool hin = true;
-    if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL, false);
+    if (ext) lv_walk<SPH, BS>(p, lds, true, cur.ray.o, cur.ray.d, hit, 0.0, best, besti, hit, hin, total, errL, XR_NONE);
     bool shade = ext && besti >= 0;
     V3 delta = hit, nrm = hit;
     if (shade) hit_info(S, besti, cur.ray, hit, delta, nrm, hin);
@@ -1226,7 +1239,7 @@ __global__ __launch_bounds__(BS, RTX_LV_WALK_WPS) void k_lv_shadow(KParams p, in
       bool in2 = true;
       uint32_t err = 0;
       lv_walk<SPH, BS>(p, lds, false, qo, vsub(qL, qo), qL, L.radius, b2, bi2, h2, in2, tot, err,
-                       p.exact_raises != 0);   // (split phases: the check's flag at run time)
+                       p.exact_raises != 0 ? XR_WALK : XR_NONE);   // (split phases: the widened walk, at run time)
       reinterpret_cast<double2*>(p.lv_area)[(size_t)hs * nL + li] =
           make_double2(tot, __builtin_bit_cast(double, (uint64_t)err));
     }
@@ -1590,7 +1603,7 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
       const uint32_t rec = (uint32_t)__builtin_bit_cast(uint64_t, d.x);
       uint32_t err = 0;
       highlight_leaves_att(S, r, [] { return v3(0.0, 0.0, 0.0); }, [](V3) {}, err,
-                           [&](V3 T, V3 L, double rad) { return lit_area_raises_wave(S, T, L, rad); });
+                           [&](V3 T, V3 L, double rad, int) { return lit_area_raises_wave(S, T, L, rad); });
       if (__lane_id() == 0) {
         uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)rec * p.lv_rec_bytes);
         *h = (*h & ~0xffu) | (err & 0xffu);
@@ -1602,7 +1615,7 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
   const Bvh4Node* nodes = S.bvh_root != BVH_NONE ? S.bvh : nullptr;
   const float4* leaf4 = reinterpret_cast<const float4*>(S.bvh_sph32);
   int* stk = lds_hl + threadIdx.x;
-  if (stage && nodes) {
+  if (stage == 1 && nodes) {
     float4* l = reinterpret_cast<float4*>(lds_hl);
     const int nn = S.n_nodes * (int)(sizeof(Bvh4Node) / 16);
     for (int k = threadIdx.x; k < nn; k += 256) l[k] = reinterpret_cast<const float4*>(S.bvh)[k];
@@ -1620,7 +1633,12 @@ __global__ __launch_bounds__(256) void k_hl_raise(KParams p, int stage) {
     r.d = v3(b.y, c.x, c.y);
     const uint32_t rec = (uint32_t)__builtin_bit_cast(uint64_t, d.x);
     uint32_t err = 0;
-    highlight_leaves_att(S, r, [] { return v3(0.0, 0.0, 0.0); }, [](V3) {}, err, [&](V3 T, V3 L, double rad) {
+    highlight_leaves_att(S, r, [] { return v3(0.0, 0.0, 0.0); }, [](V3) {}, err, [&](V3 T, V3 L, double rad, int li) {
+      // the light and raise buffers when built, else / below their floor the walk
+      if (stage == 3) {
+        const int b = lit_area_raises_lbuf(S, li, T, L, rad);
+        if (b >= 0) return b != 0;
+      }
       return lit_area_raises(S, nodes, leaf4, S.bvh_sph64, stk, 256, T, L, rad);
     });
     uint32_t* h = reinterpret_cast<uint32_t*>(p.lv_rec + (size_t)rec * p.lv_rec_bytes);
@@ -1633,8 +1651,11 @@ static hipError_t launch_hl_raise(const KParams& q, hipStream_t s) {
   // up to 256 spheres: a wave per entry over the spheres (C2); else the walk, the
   // hierarchy staged in LDS when small (every workgroup with entries copies it)
   const size_t hier = (size_t)q.scene.n_nodes * sizeof(Bvh4Node) + (size_t)q.scene.n_slots * 16;
-  const int stage = q.scene.n_sphere <= 256 ? 2 : q.scene.bvh_root != BVH_NONE && hier <= 16 * 1024 ? 1 : 0;
-  const size_t lds = stage == 2 ? 0 : (stage ? hier : 0) + (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
+  // (stage 3: larger scenes with the light and raise buffers: their lists, the global hierarchy as fallback)
+  const int stage = q.scene.n_sphere <= 256                  ? 2
+                    : q.scene.lbuf && q.scene.rbuf           ? 3
+                    : q.scene.bvh_root != BVH_NONE && hier <= 16 * 1024 ? 1 : 0;
+  const size_t lds = stage == 2 ? 0 : (stage == 1 ? hier : 0) + (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
   int cus = 0, per_cu = 0;
   hipError_t e = launch_fit(reinterpret_cast<const void*>(k_hl_raise), 256, lds, cus, per_cu);
   if (e != hipSuccess) return e;
@@ -1837,11 +1858,20 @@ static hipError_t launch_timed(K kern, long blocks, int bs, size_t lds, hipStrea
 // k_level_c for a level: the batch's last level compiled apart; with ray
 // binning (lv_sort) the other levels write their children's bins (SORT: a
 // kernel of its own, the key's registers would cost the default one spills).
+// xrm: XR_NONE / XR_BUF / XR_WALK (lv_walk); XR_BUF is instantiated only for
+// the sphere modes with a light buffer (the others take XR_WALK).
+template <int SPH, int BS, int RF, bool LAST, bool SORT>
+static void (*level_c_xr(int xrm))(KParams, int) {
+  constexpr bool BUF = SPH == SPH_BVH_LDSX || SPH == SPH_BVH_QLDS;
+  if (xrm == XR_NONE) return k_level_c<SPH, BS, RF, LAST, XR_NONE, SORT>;
+  if constexpr (BUF) if (xrm == XR_BUF) return k_level_c<SPH, BS, RF, LAST, XR_BUF, SORT>;
+  return k_level_c<SPH, BS, RF, LAST, XR_WALK, SORT>;
+}
 template <int SPH, int BS, int RF>
-static void (*level_c_kernel(bool last, bool xr, bool sort))(KParams, int) {
-  if (last) return xr ? k_level_c<SPH, BS, RF, true, true, false> : k_level_c<SPH, BS, RF, true, false, false>;
-  if (sort) return xr ? k_level_c<SPH, BS, RF, false, true, true> : k_level_c<SPH, BS, RF, false, false, true>;
-  return xr ? k_level_c<SPH, BS, RF, false, true, false> : k_level_c<SPH, BS, RF, false, false, false>;
+static void (*level_c_kernel(bool last, int xrm, bool sort))(KParams, int) {
+  if (last) return level_c_xr<SPH, BS, RF, true, false>(xrm);
+  if (sort) return level_c_xr<SPH, BS, RF, false, true>(xrm);
+  return level_c_xr<SPH, BS, RF, false, false>(xrm);
 }
 
 #ifndef RTX_LV_FUSED_BS
@@ -1858,13 +1888,18 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
   KParams q = p;
   q.stk_slots_max = 0;                         // no ray stack in this engine
   size_t lds = lds_layout(q, SPH, BS);
-  // exact_raises (the default) compiles the shadow walks' raise check in (k_level / k_level_c <..., XR>)
-  // (the kernels without it serve exact_raises = 0)
+  // exact_raises (the default) compiles the shadow walks' raise check in (k_level / k_level_c <..., XR>):
+  // XR_BUF through the light and raise buffers where both serve this launch (the LDS-staged light
+  // buffer of SPH_BVH_LDSX, the global one of SPH_BVH_QLDS), else XR_WALK; exact_raises = 0: XR_NONE
   const bool xr = q.exact_raises != 0;
-  auto kern = kind == 0 ? (xr ? k_level<SPH, BS, true> : k_level<SPH, BS, false>)
+  bool bufs = false;                           // (SPH_BVH_LDSX: settled below, once the rings are placed)
+  if constexpr (SPH == SPH_BVH_QLDS) bufs = q.lv_lbuf && q.scene.lbuf && q.scene.rbuf;
+  int xrm = !xr ? XR_NONE : bufs ? XR_BUF : XR_WALK;
+  auto kern = kind == 0 ? (xrm == XR_NONE ? k_level<SPH, BS, XR_NONE> : k_level<SPH, BS, XR_WALK>)
               : kind == 1 ? k_lv_trace<SPH, BS> : k_lv_shadow<SPH, BS>;
   // hit compaction when the rings fit next to the walk's LDS (k_level_c is
   // instantiated for the fused kernel's block size only)
+  int ring_fields = 0;
   if constexpr (BS == fused_bs<SPH>()) if (kind == 0 && q.lv_compact != 0) {
     constexpr bool BVH = sph_is_bvh(SPH);
     const size_t ring = (lds + 15) & ~(size_t)15, budget = BVH ? LDS_TOTAL_BYTES : LDS_LIN_BLOCK_BYTES;
@@ -1873,27 +1908,38 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
     if (need <= budget && q.lv_compact != 2) { // the full ring
       q.lds_ring = (int32_t)ring;
       lds = need;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(level == q.lv_last_level, xr, q.lv_sort && level + 1 >= q.lv_sort);
+      ring_fields = LV_RING_FIELDS;
     } else if (BVH && need_small <= budget) {  // the compact ring (C4-sized hierarchies)
       q.lds_ring = (int32_t)ring;
       lds = need_small;
-      kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(level == q.lv_last_level, xr, q.lv_sort && level + 1 >= q.lv_sort);
+      ring_fields = LV_RING_FIELDS_SMALL;
     }
   }
   // the light buffer (§3.18) after the rings, when it fits: the shadow walks read their cell's leaves;
-  // with exact_raises the raise buffer's gates after it (§2.4), when they fit too
+  // with exact_raises the raise buffer's gates after it (§2.4), in LDS when they fit too
   if constexpr (SPH == SPH_BVH_LDSX) if (kind == 0 && q.lv_lbuf && q.scene.lbuf) {
     const size_t at = (lds + 15) & ~(size_t)15, bytes = (size_t)q.scene.lbuf_stride * q.scene.n_light * 2;
     if (at + bytes <= LDS_TOTAL_BYTES) {
       q.lds_lbuf = (int32_t)at;
       lds = at + bytes;
-      if (xr && q.scene.rgate) {
+      if (xr && q.scene.rbuf) {
+        xrm = XR_BUF;
         const size_t ga = (lds + 15) & ~(size_t)15, gb = (size_t)q.scene.rgate_stride * q.scene.n_light * 4;
         if (ga + gb <= LDS_TOTAL_BYTES) {
           q.lds_rgate = (int32_t)ga;
           lds = ga + gb;
         }
       }
+    }
+  }
+  if constexpr (BS == fused_bs<SPH>()) {
+    const bool last = level == q.lv_last_level, sort = q.lv_sort && level + 1 >= q.lv_sort;
+    if (ring_fields == LV_RING_FIELDS) kern = level_c_kernel<SPH, BS, LV_RING_FIELDS>(last, xrm, sort);
+    else if (ring_fields == LV_RING_FIELDS_SMALL) kern = level_c_kernel<SPH, BS, LV_RING_FIELDS_SMALL>(last, xrm, sort);
+    else if (kind == 0 && xrm == XR_BUF) {     // (no ring: k_level, which walks the widened hierarchy)
+      xrm = XR_WALK;
+      q.lds_lbuf = q.lds_rgate = -1;
+      kern = k_level<SPH, BS, XR_WALK>;
     }
   }
   int cus = 0, per_cu = 0;                     // (also raises the kernel's dynamic-LDS limit once)

@@ -145,6 +145,7 @@ struct SceneDev {
   const uint32_t* rbuf;
   const uint32_t* rgate;
   int32_t rbuf_n, rbuf_stride, rgate_stride;
+  float rbuf_inv_m;       // rbuf_n / lbuf_n: a light-buffer cell index i has its parent at (int)((i + 0.5) * this)
 };
 
 struct CameraDev {

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 6, session r11b (r11a repeated on the XR_BUF / XR_WALK kernel split): exact_raises through the light buffer + raise buffer
+# (DESIGN.md §2.4), now the default.  GPU tests, then C2 and C4 frames alone
+# with exact_raises 0 and 1 in alternation (tools/timing.py checks both render
+# the same bits).
+#   bash tools/sessions/r11a_session.sh TAG
+set -o pipefail
+export TMPDIR=/tmp
+TAG=$1
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > $OUT/pytest_gpu.log 2>&1 &&
+timeout -k 10 240 python3 tools/timing.py --scene c2 --reps 9 '{"exact_raises": 0}' '{"exact_raises": 1}' \
+  '{"exact_raises": 0}' '{"exact_raises": 1}' > $OUT/timing_c2.log 2>&1 &&
+timeout -k 10 300 python3 tools/timing.py --scene c4 --reps 3 '{"exact_raises": 0}' '{"exact_raises": 1}' \
+  '{"exact_raises": 0}' '{"exact_raises": 1}' > $OUT/timing_c4.log 2>&1
+rc=$?
+tail -3 $OUT/pytest_gpu.log
+cat $OUT/timing_c2.log $OUT/timing_c4.log 2>/dev/null | tail -20
+echo "session $TAG rc=$rc"
+exit $rc

@@ -430,6 +430,7 @@ int main(int argc, char** argv) {
     }
   std::mt19937_64 rng(1);
   Stats tot_sh[NRULE], tot_ext;
+  double child_hist[8] = {0};                     // parents (hits above the last level) by children
   for (int lev = 0; lev < cam.trace_depth && !level.empty(); lev++) {
     if (level.size() > cap) {                   // a uniform subsample of the level
       std::vector<Ray> sub;
@@ -509,6 +510,13 @@ int main(int argc, char** argv) {
         if (!blocked) nl++;
       }
       if (ray.depth - 1 <= 0) continue;
+      const size_t nch0 = next.size();
+      struct ChildCount {
+        std::vector<Ray>& nx;
+        size_t n0;
+        double* h;
+        ~ChildCount() { h[std::min<size_t>(nx.size() - n0, 7)]++; }   // (the parent's child block size)
+      } cc_{next, nch0, child_hist};
       const V3 nn = vnorm(n, e);
       const V3 dn = vnorm(ray.d, e);
       const V3 ra = vmul(ray.att, v3p(ob.reflective_attenuation));
@@ -555,6 +563,21 @@ int main(int argc, char** argv) {
            tot_sh[rr].leaves / tot_sh[rr].walks, tot_sh[rr].spheres / tot_sh[rr].walks,
            tot_sh[rr].band / tot_sh[rr].walks, tot_sh[rr].band2 / tot_sh[rr].walks, tot_sh[rr].band3 / tot_sh[rr].walks,
            tot_sh[rr].leaves / tot_sh[SEG].leaves);
+  {
+    // k_tree_finalize's reads: 32-B tree records, a parent's
+    // children contiguous; 64-B segments its child block touches, at a random
+    // 32-B alignment (today) and with each block 64-B aligned
+    double parents = 0, kids = 0, seg_now = 0, seg_al = 0;
+    for (int k = 1; k < 8; k++) {
+      parents += child_hist[k], kids += k * child_hist[k];
+      seg_now += child_hist[k] * (k + 1) / 2.0;   // (k + 1) / 2 on average over both parities
+      seg_al += child_hist[k] * ((k + 1) / 2);
+    }
+    printf("tree records: parents by children:");
+    for (int k = 0; k < 8; k++) printf(" %d:%.0f", k, child_hist[k]);
+    printf("\n  child blocks %.0f, records %.0f, 64-B segments %.0f now, %.0f aligned (%.1f %% fewer)\n", parents, kids,
+           seg_now, seg_al, 100.0 * (1.0 - seg_al / std::max(1.0, seg_now)));
+  }
   printf("light/raise buffers per shadow walk: cover leaves %.3f, raise B2+B1 %.3f, raise M %.3f, distinct leaves %.3f, "
          "band spheres %.3f, raise entries read %.3f (walks with an open gate %.3f), hierarchy fallbacks %.5f\n",
          rs_cover / rs_walks, rs_p / rs_walks, rs_m / rs_walks, rs_union / rs_walks, rs_band / rs_walks, rs_scan / rs_walks,
