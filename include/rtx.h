@@ -379,7 +379,9 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          0 [default] = level 1 above 512 spheres, else the last level only and only in batches of at least 2^22
          camera samples; the levels before it keep the queue order; read-only "lv_sort_effective": whether the next
          whole-frame render bins a level, "lv_sort_last": the levels per batch the last bounce-level render binned), "lv_sort_bits" (2^bits origin cells per axis of a bin, 3 or 4; 0 [default] = 4 above 512
-         spheres, else 3), "lbuf" (bounce levels: 1 [default] = the shadow walks of scenes whose sphere records
+         spheres, else 3), "lv_sort_copy" (1: the binning pass also moves the level's ray records into bin
+         order, so the level reads them in runs instead of gathering them; 0 [default]: the gathers cost less
+         than the copy, C4 296 -> 342 ms per frame with it; same bits), "lbuf" (bounce levels: 1 [default] = the shadow walks of scenes whose sphere records
          are staged in LDS (sphere mode 3) visit only the leaves listed in a per-light cube map of the spheres
          as seen from the light, built at upload, when it fits LDS next to the hit rings; 0 = the hierarchy
          walk; same bits). */

@@ -646,13 +646,43 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
   return rb;
 }
 
-// The raise buffer's gates: one word per light and raise-buffer cell, the q
-// of the first entry of each list (byte 0: B2's, 0 when empty; byte 1: B1's,
-// 255 when empty; byte 2: M's, 0 when empty).  A query reads the lists only
-// when ql <= byte 0 or ql >= byte 1 (P), or ql <= byte 2 (M): small scenes
-// stage the gates in LDS and rarely touch the lists (ql > 0 always).
-inline std::vector<uint32_t> raise_gates(const RaiseBuffer& rb, int n_light) {
-  std::vector<uint32_t> g;
+// The raise buffer's gates: one 16-bit word per light and raise-buffer cell
+// summarising the q of the first entry of each list in 5-bit fields of
+// GATE_UNIT q units (an eighth of an octave of l): bits 0-4 g2 = ceil(q /
+// unit) of B2's (0 when empty), bits 5-9 g1 = floor(q / unit) of B1's (31 when
+// empty), bits 10-14 gm = ceil(q / unit) of M's (0 when empty), each clamped
+// to 31.  A query reads the lists only when ql <= unit g2 or ql >= unit g1
+// (P), or ql <= unit gm (M), a field of 31 in g2 / gm opening always (a
+// threshold beyond 2^3.9 floors): small scenes stage the gates in LDS and
+// rarely touch the lists (ql > 0 always).
+inline uint16_t gate_word(uint32_t q2, uint32_t q1, uint32_t qm) {
+  auto up = [](uint32_t q) { return std::min<uint32_t>(31u, (q + GATE_UNIT - 1) / GATE_UNIT); };
+  return (uint16_t)(up(q2) | (std::min<uint32_t>(31u, q1 / GATE_UNIT) << 5) | (up(qm) << 10));
+}
+inline bool gate_open(uint16_t g, int t, float ql) {   // (the device's test, rtx_device.h raise_lists)
+  const uint32_t f = (g >> (5 * t)) & 31u;
+  return t == 1 ? ql >= (float)(GATE_UNIT * f) : (f == 31u || ql <= (float)(GATE_UNIT * f));
+}
+
+// A light's floor^2 rounded up and log2 floor^2 (the gate block's header;
+// rtx_device.h raise_qa / raise_rq).  ql = 8 (log2 |d|^2 - log2 floor^2) is
+// 16 log2(l / floor) to float rounding, far inside the 1e-4 slack of the q's.
+inline float raise_floor2(const RaiseBuffer& rb, int li) {
+  float fl;
+  memcpy(&fl, &rb.words[(size_t)rb.stride * li], 4);
+  const double f2 = (double)fl * (double)fl;
+  float r = (float)f2;
+  if ((double)r < f2) r = nextafterf(r, INFINITY);
+  return r;
+}
+inline float raise_lf2(const RaiseBuffer& rb, int li) {
+  float fl;
+  memcpy(&fl, &rb.words[(size_t)rb.stride * li], 4);
+  return (float)(2.0 * std::log2((double)fl));
+}
+
+inline std::vector<uint16_t> raise_gates(const RaiseBuffer& rb, int n_light) {
+  std::vector<uint16_t> g;
   if (!rb.n) return g;
   const int cells = 6 * rb.n * rb.n;
   g.assign((size_t)cells * n_light, 0);
@@ -661,13 +691,12 @@ inline std::vector<uint32_t> raise_gates(const RaiseBuffer& rb, int n_light) {
     const uint32_t* off = blk + 2;
     const uint32_t* ent = blk + 2 + (size_t)RB_LISTS * (cells + 1);
     for (int c = 0; c < cells; c++) {
-      uint32_t w = 0;
+      uint32_t q[RB_LISTS];
       for (int t = 0; t < RB_LISTS; t++) {
         const uint32_t k0 = off[t * (cells + 1) + c], k1 = off[t * (cells + 1) + c + 1];
-        const uint32_t q = k1 > k0 ? (ent[k0] & 255u) : (t == RB_B1 ? 255u : 0u);
-        w |= q << (8 * t);
+        q[t] = k1 > k0 ? (ent[k0] & 255u) : (t == RB_B1 ? 255u : 0u);
       }
-      g[(size_t)cells * li + c] = w;
+      g[(size_t)cells * li + c] = gate_word(q[RB_B2], q[RB_B1], q[RB_M]);
     }
   }
   return g;

@@ -97,6 +97,7 @@ struct rtx_context {
   int64_t opt_lv_sort_from = 0;      // bounce levels: the first level binned; 0 auto: level 1 above 512 spheres (C4 354 ->
                                      // 307 ms), else the last level only (C2 4.60 -> 4.57 ms; all levels 4.65 -> 4.88, r10d/r10k)
   int64_t opt_lv_sort_bits = 0;      // bounce levels: 2^bits origin cells per axis (3 or 4); 0 auto: 4 above 512 spheres, else 3
+  int64_t opt_lv_sort_copy = 0;      // bounce levels: 1 = binning copies the rays' records into bin order (r11i: C4 296 -> 342 ms, off)
   int64_t opt_lbuf = 1;              // bounce levels: 1 = shadow walks through the light buffer where it is staged (§3.18)
   int n_cus = 0;                     // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   unsigned long long* d_lvstats = nullptr;   // rtx_level_stats of the last bounce-level render call
@@ -280,7 +281,8 @@ rtx_status rtx_get_option(rtx_context* c, const char* key, int64_t* value) {
       {"lv_redo_blocks", c->opt_lv_redo_blocks},
       {"lv_fin_grid", c->opt_lv_fin_grid}, {"lv_ray_bytes", c->opt_lv_ray_bytes},
       {"exact_raises", c->opt_exact_raises}, {"lv_hl_cap", c->opt_lv_hl_cap}, {"lv_sort", c->opt_lv_sort},
-      {"lv_sort_from", c->opt_lv_sort_from}, {"lv_sort_bits", c->opt_lv_sort_bits}, {"lbuf", c->opt_lbuf}};
+      {"lv_sort_from", c->opt_lv_sort_from}, {"lv_sort_bits", c->opt_lv_sort_bits}, {"lbuf", c->opt_lbuf},
+      {"lv_sort_copy", c->opt_lv_sort_copy}};
   for (const auto& t : tab)
     if (!strcmp(key, t.k)) {
       *value = t.v;
@@ -382,6 +384,11 @@ rtx_status rtx_set_option(rtx_context* c, const char* key, int64_t value) {
   if (!strcmp(key, "lv_sort_from")) {      // bounce levels: the first level binned (with lv_sort), 0 auto
     if (value < 0 || value > LV_MAXL) return fail(c, RTX_EINVAL, "lv_sort_from must be in [0, %d]", LV_MAXL);
     c->opt_lv_sort_from = value;
+    return RTX_OK;
+  }
+  if (!strcmp(key, "lv_sort_copy")) {      // bounce levels: binning moves the records into bin order (same bits)
+    if (value < 0 || value > 1) return fail(c, RTX_EINVAL, "lv_sort_copy must be 0 or 1");
+    c->opt_lv_sort_copy = value;
     return RTX_OK;
   }
   if (!strcmp(key, "lv_sort_bits")) {      // bounce levels: 2^bits origin cells per axis of a ray bin, 0 auto
@@ -689,7 +696,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
         lfloor[li] = std::isfinite(fl) ? std::max(0.0, 0.99 * fl) : 0.0;
       }
       RaiseBuffer rb;
-      const int want = small ? 8 : 40;
+      const int want = small ? 12 : 40;
       for (int nc = std::min(want, lb.n); nc >= 1 && !rb.n; nc--) {
         if (lb.n % nc) continue;
         rb = build_raise_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), lrad.data(),
@@ -697,17 +704,20 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
         if (!rb.n && nc <= 8) break;
       }
       if (rb.n) {
-        const std::vector<uint32_t> g = raise_gates(rb, sd->n_lights);
-        const int cells = 6 * rb.n * rb.n, gs = (4 + cells + 3) & ~3;
-        std::vector<uint32_t> gw((size_t)gs * sd->n_lights, 0);
+        // per light: floor^2 (rounded up) and log2 floor^2 (float bits, 2 words each), 4 words of
+        // padding, a gate word per cell (rtx_device.h raise_qa)
+        const std::vector<uint16_t> g = raise_gates(rb, sd->n_lights);
+        const int cells = 6 * rb.n * rb.n, gs = (8 + cells + 7) & ~7;
+        std::vector<uint16_t> gw((size_t)gs * sd->n_lights, 0);
         for (int li = 0; li < sd->n_lights; li++) {
-          gw[(size_t)gs * li] = rb.words[(size_t)rb.stride * li];   // the floor
-          std::copy(g.begin() + (size_t)cells * li, g.begin() + (size_t)cells * (li + 1), gw.begin() + (size_t)gs * li + 4);
+          const float hw[2] = {raise_floor2(rb, li), raise_lf2(rb, li)};
+          memcpy(&gw[(size_t)gs * li], hw, 8);
+          std::copy(g.begin() + (size_t)cells * li, g.begin() + (size_t)cells * (li + 1), gw.begin() + (size_t)gs * li + 8);
         }
         HIPCHK(c, up(rb.words.data(), rb.words.size() * sizeof(uint32_t), &ptr));
         S.rbuf = (const uint32_t*)ptr;
-        HIPCHK(c, up(gw.data(), gw.size() * sizeof(uint32_t), &ptr));
-        S.rgate = (const uint32_t*)ptr;
+        HIPCHK(c, up(gw.data(), gw.size() * sizeof(uint16_t), &ptr));
+        S.rgate = (const uint16_t*)ptr;
         S.rbuf_n = rb.n;
         S.rbuf_stride = rb.stride;
         S.rgate_stride = gs;
@@ -969,8 +979,11 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
   // others' levels).  The extra-sample list and the statistics are shared
   // (appended / added atomically); each part has its own level buffers, its
   // own lanes-engine work counter and ray stacks for its overflow re-render.
+  // (lv_sort_copy: the binned level's records in bin order, a third staging buffer)
+  const bool sort_copy = sort && c->opt_lv_sort_copy == 1;
+  const size_t sz_sorted = sort_copy ? sz_stage : 0;
   const size_t set = sz_ctl + 2 * sz_redo + sz_smp + 2 * sz_stage + sz_rec + sz_hit + sz_area + sz_hlq + sz_key +
-                     sz_perm + sz_bins;
+                     sz_perm + sz_bins + sz_sorted;
   const size_t total = parts * set + sz_extra;
   if (!c->d_lvstats) HIPCHK(c, hipMalloc(&c->d_lvstats, sizeof(unsigned long long) * (LV_MAXL + 3)));
   char* buf = nullptr;
@@ -990,6 +1003,7 @@ static rtx_status render_levels(rtx_context* c, KParams& p, int maxs, hipStream_
     k.lv_key = sort ? (uint16_t*)q : nullptr;      q += sz_key;
     k.lv_perm = sort ? (uint2*)q : nullptr;        q += sz_perm;
     k.lv_bins = sort ? (uint32_t*)q : nullptr;     q += sz_bins;
+    k.lv_sorted = sort_copy ? (double*)q : nullptr; q += sz_sorted;
     k.lv_sort = sort_from;
     k.lv_cell_bits = lv_sort_bits(c);
     k.lv_lbuf = (int32_t)c->opt_lbuf;

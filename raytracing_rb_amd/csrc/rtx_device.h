@@ -836,40 +836,54 @@ __device__ __forceinline__ void leaf_raises(int lf, LP leaf4, XP x64, const Slab
   }
 }
 
-// The raise buffer's reach for a shadow ray of light `light` (o = T, d = L -
-// T, s its float32 set-up): ql = 16 log2(l / floor), false when l lies below
-// the light's floor (or ql above 254): the caller walks the hierarchy.
-// gates: this light's gate block (floor, 3 words of padding, one word per
+// The raise buffer's reach for a shadow ray (o = T, d = L - T, s its float32
+// set-up): ql = 16 log2(l / floor) = 8 (log2 |d|^2 - log2 floor^2), first as
+// a cheap lower bound qa from the bits of |d|^2 (a float's bits / 2^23 - 127
+// is log2 x less the mantissa's log2(1 + f) - f, which lies in [0, 0.0861]:
+// qa <= ql <= qa + QA_SLACK); the exact value (raise_rq) only when a gate
+// opens.  false when l lies below the light's floor or ql may exceed 254: the
+// caller walks the hierarchy.  gates: this light's gate block (16-bit words:
+// floor^2 and log2 floor^2 as float bits, 4 of padding, a gate per
 // raise-buffer cell), in LDS or global memory.
-__device__ __forceinline__ bool raise_ql(const uint32_t* gates, const SlabRay& s, float& ql) {
-  const float fl = __uint_as_float(gates[0]);
-  const float ell = __builtin_amdgcn_sqrtf(s.dd);
-  ql = 16.0f * __log2f(ell * __builtin_amdgcn_rcpf(fl));
-  // (ell >= fl (1 + 1e-4) with the hardware reciprocal's 1 ulp inside the margin)
-  return ell >= fl * (1.0f + 1e-4f) && ql <= 254.0f;
+constexpr float QA_SLACK = 0.7f;             // 8 x 0.0861 + the int-to-float rounding of the bits
+__device__ __forceinline__ float gate_f(const uint16_t* g, int k) {
+  return __uint_as_float((uint32_t)g[k] | (uint32_t)g[k + 1] << 16);
+}
+__device__ __forceinline__ bool raise_qa(const uint16_t* gates, const SlabRay& s, float& qa) {
+  qa = 8.0f * (__builtin_fmaf((float)__float_as_int(s.dd), 1.0f / 8388608.0f, -127.0f) - gate_f(gates, 2));
+  // l >= floor (1 + 1e-4): |d|^2 >= floor^2 (1 + 2.1e-4), floor^2 rounded up
+  return s.dd >= gate_f(gates, 0) * (1.0f + 2.1e-4f) && qa + QA_SLACK <= 254.0f;
+}
+__device__ __forceinline__ float raise_rq(const uint16_t* gates, const SlabRay& s) {
+  return 8.0f * (__log2f(s.dd) - gate_f(gates, 2));
 }
 
 // The raise buffer's lists (rtx_bvh_build.h build_raise_buffer): B2 and B1 at
 // the parent (raise-buffer) cell of the light buffer's cell (face, i, j) of
-// -d, M at the parent of the light buffer's cell of d, each read while its
-// entries' thresholds admit ql and only when the cell's gate opens; each
-// listed leaf gets leaf_raises.  (The light buffer's own cell, walked with
-// walk_leaf's band test, holds regime A.)
+// -d, M at the parent of its opposite cell (face ^ 1, n - 1 - i, n - 1 - j:
+// the cell of d, or a neighbour sharing the boundary d lies on, which the
+// cells' slack covers), each read while its entries' thresholds admit ql and
+// only when the cell's gate opens; each listed leaf gets leaf_raises.  (The
+// light buffer's own cell, walked with walk_leaf's band test, holds regime A.)
 template <typename LP, typename XP>
-__device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const uint32_t* gates, LP leaf4, XP x64,
+__device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const uint16_t* gates, LP leaf4, XP x64,
                                             const SlabRay& s, const XrRay& xrr, V3 o, V3 d, double radius, int face,
-                                            int i, int j, float ql, uint32_t& err) {
+                                            int i, int j, float qa, uint32_t& err) {
   const int nu = S.lbuf_n, nc = S.rbuf_n, cells = 6 * nc * nc;
-  int mf, mi, mj;
-  if (lbuf_cell(s.dx, s.dy, s.dz, nu, mf, mi, mj) < 0) return;   // (d finite and nonzero: never)
   // parent cells: i / m as (int)((i + 0.5) / m) in float32 (no integer division: i, m < 2^12, so
   // (i + 0.5) / m lies at least 0.5 / m from an integer, far beyond the rounding)
   const float im = S.rbuf_inv_m;
   auto up = [im](int k) { return (int)(((float)k + 0.5f) * im); };
-  const int pc = (face * nc + up(i)) * nc + up(j), mc = (mf * nc + up(mi)) * nc + up(mj);
-  const uint32_t gp = gates[4 + pc], gm = gates[4 + mc];
-  const bool o2 = ql <= (float)(gp & 255u), o1 = ql >= (float)((gp >> 8) & 255u), om = ql <= (float)((gm >> 16) & 255u);
+  const int pc = (face * nc + up(i)) * nc + up(j), mc = ((face ^ 1) * nc + up(nu - 1 - i)) * nc + up(nu - 1 - j);
+  // the gates (rtx_bvh_build.h gate_word: 5-bit fields in GATE_UNIT q units; 31 in g2 / gm: always open),
+  // tested with ql's bounds [qa, qa + QA_SLACK]
+  const uint32_t gp = gates[8 + pc], gm = gates[8 + mc];
+  const uint32_t g2 = gp & 31u, g1 = (gp >> 5) & 31u, gmm = (gm >> 10) & 31u;
+  constexpr float U = (float)GATE_UNIT;
+  const bool o2 = g2 == 31u || qa <= U * (float)g2, o1 = qa + QA_SLACK >= U * (float)g1,
+             om = gmm == 31u || qa <= U * (float)gmm;
   if (!(o2 || o1 || om)) return;
+  const float ql = raise_rq(gates, s);
   const uint32_t* blk = S.rbuf + (size_t)light * S.rbuf_stride;
   const uint32_t* off = blk + 2;
   const uint32_t* ent = blk + 2 + (size_t)3 * (cells + 1);
@@ -923,7 +937,7 @@ template <int BS, typename LP, typename XP, typename OP>
 __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb, LP leaf4, XP x64, OP xobj, int* ci,
                                            double* cv, V3 o, V3 d, V3 L, double radius, double& best, int& besti,
                                            V3& bhit, bool& bin, double& total, uint32_t& err, bool xr = false,
-                                           int light = 0, const uint32_t* gates = nullptr) {
+                                           int light = 0, const uint16_t* gates = nullptr) {
   const SlabRay s = slab_setup(S, o, d);
   if (!s.fin) return false;
   // the cube-map cell of v = o - L = -d
@@ -934,8 +948,8 @@ __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb
   // exact_raises: a light of radius 0 never raises (r1 = 0); without the raise
   // buffer, or below its floor, the hierarchy walk checks the cone
   xr = xr && radius > 0.0;
-  float ql = 0.0f;
-  if (xr && !(S.rbuf && gates && raise_ql(gates, s, ql))) return false;
+  float qa = 0.0f;
+  if (xr && !(S.rbuf && gates && raise_qa(gates, s, qa))) return false;
   const int k0 = lb[cell], k1 = lb[cell + 1];
   const uint16_t* ent = lb + 6 * n * n + 1;
   const double r = vr(d);
@@ -958,7 +972,7 @@ __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb
     walk_leaf<BS>((int)(int16_t)ent[k], leaf4, x64, xobj, s, false, o, d, dn, r, r2, L, radius, best, besti, bhit,
                   bin, thi, err, ci, cv, ncov, ovf, xr && !RTX_DIAG_XR_NOBAND, qerr);
   if (xr && !RTX_DIAG_XR_NOLISTS)
-    raise_lists(S, light, gates, leaf4, x64, s, xr_ray(s.Sx, s.dd, radius, qerr), o, d, radius, face, i, j, ql, err);
+    raise_lists(S, light, gates, leaf4, x64, s, xr_ray(s.Sx, s.dd, radius, qerr), o, d, radius, face, i, j, qa, err);
   // (an overflowing cover list repeats the ordered linear walk, which checks the raises itself)
   walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, xr);
   return true;
@@ -979,9 +993,9 @@ __device__ __forceinline__ int lit_area_raises_lbuf(const SceneDev& S, int light
   const int n = S.lbuf_n;
   const int cell = lbuf_cell(-s.dx, -s.dy, -s.dz, n, face, i, j);
   if (cell < 0) return -1;
-  const uint32_t* gates = S.rgate + (size_t)light * S.rgate_stride;
-  float ql;
-  if (!raise_ql(gates, s, ql)) return -1;
+  const uint16_t* gates = S.rgate + (size_t)light * S.rgate_stride;
+  float qa;
+  if (!raise_qa(gates, s, qa)) return -1;
   const uint16_t* lb = S.lbuf + (size_t)light * S.lbuf_stride;
   const int k0 = lb[cell], k1 = lb[cell + 1];
   const uint16_t* ent = lb + 6 * n * n + 1;
@@ -989,7 +1003,7 @@ __device__ __forceinline__ int lit_area_raises_lbuf(const SceneDev& S, int light
   const XrRay xrr = xr_ray(s.Sx, s.dd, radius, 0.0f);
   uint32_t err = 0;
   for (int k = k0; k < k1 && !err; k++) leaf_raises((int)(int16_t)ent[k], leaf4, S.bvh_sph64, s, xrr, T, d, radius, err);
-  if (!err) raise_lists(S, light, gates, leaf4, S.bvh_sph64, s, xrr, T, d, radius, face, i, j, ql, err);
+  if (!err) raise_lists(S, light, gates, leaf4, S.bvh_sph64, s, xrr, T, d, radius, face, i, j, qa, err);
   return err ? 1 : 0;
 }
 

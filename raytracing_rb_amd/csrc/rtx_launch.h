@@ -124,6 +124,7 @@ struct KParams {
   int32_t lv_lbuf;                 // 1: the fused level kernels' shadow walks use the light buffer when staged (option lbuf)
   uint16_t* lv_key;                // bin of each staged ray of the level being binned, by queue slot (k_lv_bin)
   uint2* lv_perm;                  // the level's rays in bin order: {queue slot, dense index}
+  double* lv_sorted;               // lv_sort_copy: the binned level's ray records in bin order (k_lv_bin), or null
   uint32_t* lv_bins;               // LV_BINS counts, LV_BINS cursors (the first 8 << 3 lv_cell_bits used)
 };
 

@@ -252,11 +252,18 @@ __device__ __forceinline__ uint32_t lv_ray_bin(const SceneDev& S, const Ray& r, 
 }
 static_assert(LV_BINS <= 65536, "bins are 16-bit keys");
 
+__device__ __forceinline__ const double* lv_src(const KParams& p, int level) {
+  return p.lv_sorted && p.lv_sort && level >= p.lv_sort ? p.lv_sorted : p.lv_stage[level & 1];
+}
+
 // The level's chunks, and chunk c's ray for this lane: its queue slot and
 // dense index (binned: from the bin list; else the slices).  All lanes call it.
 __device__ __forceinline__ uint32_t lv_chunks(const KParams& p, const LvQueue& in, int level) {
   return p.lv_sort && level >= p.lv_sort ? (in.total + 63u) >> 6 : in.chunks;
 }
+// With lv_sort_copy the binning pass also moved the records into bin order
+// (lv_sorted): the ray's "slot" is then its place k in that order, and
+// lv_src gives the array the level's records are read from.
 __device__ __forceinline__ bool lv_chunk_item(const KParams& p, const LvQueue& in, int level, uint32_t c,
                                               uint32_t& slot, uint32_t& i) {
   if (p.lv_sort && level >= p.lv_sort) {
@@ -264,7 +271,7 @@ __device__ __forceinline__ bool lv_chunk_item(const KParams& p, const LvQueue& i
     slot = i = 0;
     if (k >= in.total) return false;
     const uint2 e = p.lv_perm[k];
-    slot = e.x;
+    slot = p.lv_sorted ? k : e.x;
     i = e.y;
     return true;
   }
@@ -403,9 +410,9 @@ __device__ __forceinline__ void lv_stage_scene(const KParams& p, float4* lds_sph
         const int nw = S.lbuf_stride * S.n_light / 8;
         for (int i = threadIdx.x; i < nw; i += BS) lb[i] = reinterpret_cast<const uint4*>(S.lbuf)[i];
       }
-      if (p.lds_rgate >= 0) {                 // the raise buffer's gates (rgate_stride words per light, a multiple of 4)
+      if (p.lds_rgate >= 0) {                 // the raise buffer's gates (rgate_stride 16-bit words per light, a multiple of 8)
         uint4* g = reinterpret_cast<uint4*>(lds + p.lds_rgate);
-        const int nw = S.rgate_stride * S.n_light / 4;
+        const int nw = S.rgate_stride * S.n_light / 8;
         for (int i = threadIdx.x; i < nw; i += BS) g[i] = reinterpret_cast<const uint4*>(S.rgate)[i];
       }
     }
@@ -430,8 +437,8 @@ __device__ __forceinline__ bool lv_walk(const KParams& p, char* lds, bool ext, V
   // the light buffer's cell (§3.18): staged in LDS with the sphere records
   // (SPH_BVH_LDSX), read from global memory beside C4's 16-bit leaves;
   // exact_raises: the raise buffer's gates, staged in LDS beside the light buffer or global
-  const uint32_t* gates = xrm == XR_BUF && S.rgate && light >= 0
-                              ? (p.lds_rgate >= 0 ? reinterpret_cast<const uint32_t*>(lds + p.lds_rgate)
+  const uint16_t* gates = xrm == XR_BUF && S.rgate && light >= 0
+                              ? (p.lds_rgate >= 0 ? reinterpret_cast<const uint16_t*>(lds + p.lds_rgate)
                                                   : S.rgate) + (size_t)light * S.rgate_stride
                               : nullptr;
   if (SPH == SPH_BVH_LDSX && !ext && xrm != XR_WALK && light >= 0 && p.lds_lbuf >= 0) {
@@ -519,7 +526,7 @@ __device__ __forceinline__ void lv_ray(const KParams& p, int level, uint32_t idx
     }
     return;
   }
-  const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)idx * p.lv_ray_dbl);
+  const double2* q = reinterpret_cast<const double2*>(lv_src(p, level) + (size_t)idx * p.lv_ray_dbl);
   const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
   cur.ray.o = v3(a.x, a.y, b.x);
   cur.ray.d = v3(b.y, c.x, c.y);
@@ -903,7 +910,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
         // attenuation is read if a highlight fires, the root if the ray
         // overflows the record arena (the second half reloads the rest), so
         // the walk does not carry them.
-        const double2* qs = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
+        const double2* qs = reinterpret_cast<const double2*>(lv_src(p, level) + (size_t)slot * p.lv_ray_dbl);
         Item cur;
         int root = 0, x = 0, y = 0, sample = 0;
         bool alive = false;
@@ -1025,7 +1032,7 @@ __device__ __forceinline__ void k_level_c_body(const KParams& p, int level) {
           cur.ray = lens_ray(cam, lens_target(cam, x, y), x, y, sample, p.seed);
         }
       } else {                                // the staged child at its queue slot (lv_ray)
-        const double2* q = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)(is >> 32) * p.lv_ray_dbl);
+        const double2* q = reinterpret_cast<const double2*>(lv_src(p, level) + (size_t)(is >> 32) * p.lv_ray_dbl);
         if (RF != LV_RING_FIELDS) {
           const double2 a = q[0], b = q[1], c = q[2];
           cur.ray.o = v3(a.x, a.y, b.x);
@@ -1764,7 +1771,17 @@ __global__ __launch_bounds__(BIN_BS) void k_lv_bin(KParams p, int level) {
   }
   if (!SCATTER) return;
   __syncthreads();
-  sweep([&](uint32_t b, uint32_t slot, uint32_t i) { p.lv_perm[atomicAdd(&hist[b], 1u)] = make_uint2(slot, i); });
+  // (lv_sort_copy: each record moves to its place too, read in queue order, written in bin order)
+  double* dst = p.lv_sorted;
+  sweep([&](uint32_t b, uint32_t slot, uint32_t i) {
+    const uint32_t at = atomicAdd(&hist[b], 1u);
+    p.lv_perm[at] = make_uint2(slot, i);
+    if (dst) {
+      const double2* s2 = reinterpret_cast<const double2*>(p.lv_stage[level & 1] + (size_t)slot * p.lv_ray_dbl);
+      double2* d2 = reinterpret_cast<double2*>(p.lv_sorted + (size_t)at * p.lv_ray_dbl);
+      for (int w = 0; w < p.lv_ray_dbl / 2; w++) d2[w] = s2[w];
+    }
+  });
 }
 
 // The bins' exclusive prefix into the cursors; the counts zeroed for the next
@@ -1924,7 +1941,7 @@ static hipError_t launch_level_bs(const KParams& p, int kind, int level, long ca
       lds = at + bytes;
       if (xr && q.scene.rbuf) {
         xrm = XR_BUF;
-        const size_t ga = (lds + 15) & ~(size_t)15, gb = (size_t)q.scene.rgate_stride * q.scene.n_light * 4;
+        const size_t ga = (lds + 15) & ~(size_t)15, gb = (size_t)q.scene.rgate_stride * q.scene.n_light * 2;
         if (ga + gb <= LDS_TOTAL_BYTES) {
           q.lds_rgate = (int32_t)ga;
           lds = ga + gb;

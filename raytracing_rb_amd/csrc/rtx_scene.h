@@ -61,6 +61,7 @@ constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); m
 constexpr size_t LBUF_MAX_WORDS = 8192;   // light buffer, all lights: at most 16 KB (staged in LDS next to the hit ring)
 constexpr size_t LBUF_MAX_WORDS_GLOBAL = 1 << 18;   // scenes above 512 spheres: at most 512 KB, read from global memory
 constexpr size_t RBUF_MAX_WORDS = 1 << 20;          // raise buffer, all lights: at most 4 MB (global memory, L2)
+constexpr uint32_t GATE_UNIT = 2;                    // raise-buffer gates: q units per 5-bit field (rtx_bvh_build.h gate_word)
 struct Bvh4Node {
   float lh[3][4][2];      // [axis][child] = {lo, hi}: both slab planes of an axis in one 8-byte pair
                           // (one packed FP32 FMA, v_pk_fma_f32, gives both slab distances)
@@ -139,11 +140,11 @@ struct SceneDev {
   int32_t lbuf_n, lbuf_stride;
   // raise buffer (rtx_bvh_build.h build_raise_buffer; null when
   // not built): per light rbuf_stride words (floor, count, 3 (6 rbuf_n^2 + 1)
-  // offsets, entries); per light rgate_stride gate words: the floor (float
-  // bits), 3 words of padding, one word per raise-buffer cell (raise_gates);
-  // lbuf_n is a multiple of rbuf_n
+  // offsets, entries); per light rgate_stride 16-bit gate words: the floor
+  // (float bits), 6 words of padding, one word per raise-buffer cell
+  // (raise_gates); lbuf_n is a multiple of rbuf_n
   const uint32_t* rbuf;
-  const uint32_t* rgate;
+  const uint16_t* rgate;
   int32_t rbuf_n, rbuf_stride, rgate_stride;
   float rbuf_inv_m;       // rbuf_n / lbuf_n: a light-buffer cell index i has its parent at (int)((i + 0.5) * this)
 };

@@ -697,7 +697,8 @@ def test_grid_stride_reduction_changes_no_bit(gpu, world, camera, ov):
 def test_binned_levels_bit_identical(gpu, world, camera, ov):
     sd, cd = _scene(world, camera, **ov)
     lanes = _renderer(sd, cd, 0).render(seed=3)
-    for opts in (dict(), dict(lv_compact=0), dict(lv_compact=2), dict(lv_streams=1)):
+    for opts in (dict(), dict(lv_compact=0), dict(lv_compact=2), dict(lv_streams=1), dict(lv_sort_copy=1),
+                 dict(lv_sort_copy=1, lv_compact=2), dict(lv_sort_copy=1, lv_compact=0)):
         r = _renderer(sd, cd, 1, lv_sort=1, **opts)
         assert r.get_option("lv_sort") == 1
         assert _same(r.render(seed=3), lanes), opts
@@ -712,6 +713,7 @@ def test_binned_levels_bit_identical(gpu, world, camera, ov):
     dict(lv_sort_from=2), dict(lv_sort_from=4),          # the first levels in queue order
     dict(lv_sort_from=9),                                # past the last level: nothing binned
     dict(lv_sort_bits=3, lv_sort_from=1), dict(lv_sort_bits=4, lv_sort_from=1),
+    dict(lv_sort_copy=1, lv_sort_from=1), dict(lv_sort_copy=1, lv_stage_pct=5, lv_floor=0),   # records moved to bin order
 ])
 def test_binned_levels_batches_overflow_schedule(gpu, opts):
     sd, cd = _scene("c2_world.yml", "c2_camera.yml", width=120, height=70)
@@ -743,6 +745,7 @@ def test_binned_levels_c4_and_c2_full_frame(gpu):
     plain = plain.render(seed=4)
     assert _same(auto.render(seed=4), plain) and auto.get_option("lv_sort_last") == cd.trace_depth - 1
     assert _same(_renderer(sd, cd, 1, lv_sort=1, lv_compact=0).render(seed=4), plain)
+    assert _same(_renderer(sd, cd, 1, lv_sort_copy=1).render(seed=4), plain)   # records moved to bin order
     sd, cd = _scene("c2_world.yml", "c2_camera.yml")
     plain = _renderer(sd, cd, 1, lv_sort=0)
     assert plain.get_option("lv_sort_effective") == 0

@@ -189,7 +189,7 @@ int raise_main(int n, int per_light, int nc, const std::vector<double>& lp, cons
     printf("no buffers\n");
     return 1;
   }
-  const std::vector<uint32_t> gates = raise_gates(rb, nl);
+  const std::vector<uint16_t> gates = raise_gates(rb, nl);
   std::mt19937_64 rng(777);
   std::uniform_real_distribution<double> U(0.0, 1.0);
   long tested = 0, fallback = 0, misses = 0, listed = 0;
@@ -246,7 +246,8 @@ int raise_main(int n, int per_light, int nc, const std::vector<double>& lp, cons
       tested++;
       const lbuf_host::Lists ls = lbuf_host::shadow_lists(lb.words.data() + (size_t)lb.stride * li, lb.n,
                                                           rb.words.data() + (size_t)rb.stride * li,
-                                                          gates.data() + (size_t)6 * rb.n * rb.n * li, rb.n, lt);
+                                                          gates.data() + (size_t)6 * rb.n * rb.n * li, rb.n, lt,
+                                                          raise_floor2(rb, li), raise_lf2(rb, li));
       if (ls.fallback) {
         fallback++;
         continue;

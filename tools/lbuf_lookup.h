@@ -45,37 +45,38 @@ struct Lists {
   int scanned = 0;                                  // raise-buffer entries read
 };
 
-inline Lists shadow_lists(const uint16_t* lblk, int nu, const uint32_t* rblk, const uint32_t* gates, int nc,
-                          const double d[3]) {
+inline Lists shadow_lists(const uint16_t* lblk, int nu, const uint32_t* rblk, const uint16_t* gates, int nc,
+                          const double d[3], float floor2 = 0.0f, float lf2 = 0.0f) {
   Lists r;
   const float dx = (float)d[0], dy = (float)d[1], dz = (float)d[2];
-  const int cu = device_cell(-dx, -dy, -dz, nu), cmu = device_cell(dx, dy, dz, nu);
-  if (cu < 0 || cmu < 0) {
+  const int cu = device_cell(-dx, -dy, -dz, nu);
+  if (cu < 0) {
     r.fallback = true;
     return r;
   }
   const uint16_t* ent = lblk + 6 * nu * nu + 1;
   for (int k = lblk[cu]; k < lblk[cu + 1]; k++) r.cover.push_back((int32_t)(int16_t)ent[k]);
   if (!rblk) return r;
+  // rtx_device.h raise_qa: the bit-pattern bound of ql, then (gates open) the exact one
   const float dd = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-  const float ell = sqrtf(dd);
-  float fl;
-  memcpy(&fl, &rblk[0], 4);
-  const float ql = 16.0f * log2f(ell / fl);
-  if (!(ell >= fl * (1.0f + 1e-4f)) || !(ql <= 254.0f)) {
+  int32_t bits;
+  memcpy(&bits, &dd, 4);
+  const float qa = 8.0f * (fmaf((float)bits, 1.0f / 8388608.0f, -127.0f) - lf2);
+  if (!(dd >= floor2 * (1.0f + 2.1e-4f)) || !(qa + 0.7f <= 254.0f)) {
     r.fallback = true;
     return r;
   }
   const int m = nu / nc, cells = 6 * nc * nc;
-  auto parent = [&](int c) {
-    const int face = c / (nu * nu), i = c / nu % nu, j = c % nu;
-    return (face * nc + i / m) * nc + j / m;
-  };
+  const int face = cu / (nu * nu), i = cu / nu % nu, j = cu % nu;
+  const int pc = (face * nc + i / m) * nc + j / m, mc = ((face ^ 1) * nc + (nu - 1 - i) / m) * nc + (nu - 1 - j) / m;
   const uint32_t* off = rblk + 2;
   const uint32_t* re = rblk + 2 + (size_t)3 * (cells + 1);
-  const int pc = parent(cu), mc = parent(cmu);
   const uint32_t gp = gates[pc], gm = gates[mc];
-  const bool open[3] = {ql <= (float)(gp & 255u), ql >= (float)(gp >> 8 & 255u), ql <= (float)(gm >> 16 & 255u)};
+  const uint32_t g2 = gp & 31u, g1 = (gp >> 5) & 31u, gmm = (gm >> 10) & 31u;
+  const float U = (float)rtx::GATE_UNIT;
+  const bool open[3] = {g2 == 31u || qa <= U * (float)g2, qa + 0.7f >= U * (float)g1, gmm == 31u || qa <= U * (float)gmm};
+  if (!(open[0] || open[1] || open[2])) return r;
+  const float ql = 8.0f * (log2f(dd) - lf2);
   for (int t = 0; t < 3; t++) {
     if (!open[t]) continue;
     const int c = t < 2 ? pc : mc;

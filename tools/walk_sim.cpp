@@ -409,7 +409,7 @@ int main(int argc, char** argv) {
   std::vector<double> floors;
   RaiseBuffer rbf = build_raise_buffer(*S.bb, S.root, reinterpret_cast<const double(*)[3]>(lp.data()), lr.data(),
                                        lf.data(), nl, raise_n, (size_t)1 << 30, &floors, getenv("PER_SPHERE") != nullptr);
-  const std::vector<uint32_t> gates = raise_gates(rbf, nl);
+  const std::vector<uint16_t> gates = raise_gates(rbf, nl);
   const bool flags = true;
   printf("light buffer n %d: %d words per light; raise buffer n %d: %d words per light, floor %.4g (nearest surface "
          "%.4g), flags %d\n",
@@ -471,7 +471,8 @@ int main(int argc, char** argv) {
           if (lbc.n && rbf.n) {
             const lbuf_host::Lists ls = lbuf_host::shadow_lists(lbc.words.data() + (size_t)lbc.stride * li, lbc.n,
                                                                 rbf.words.data() + (size_t)rbf.stride * li,
-                                                                gates.data() + (size_t)6 * rbf.n * rbf.n * li, rbf.n, dl);
+                                                                gates.data() + (size_t)6 * rbf.n * rbf.n * li, rbf.n, dl,
+                                                          raise_floor2(rbf, li), raise_lf2(rbf, li));
             if (ls.fallback) {
               rs_fb++;
             } else {
