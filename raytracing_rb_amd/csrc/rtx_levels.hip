@@ -2,6 +2,8 @@
 // RayTracer#trace_sync (src/ray_tracer.rb:16-46) breadth-first, one launch per
 // ray-tree level (or three: trace / shadow / shade), and Camera#render_at's
 // reduction over the stored trees.
+#include <vector>
+
 #include "rtx_device.h"
 
 namespace rtx {
@@ -2055,30 +2057,58 @@ static hipError_t launch_finalize(const KParams& q, int nlev, int n, hipStream_t
 // samples (exits at once when there are none), the tree reduction.  A level's
 // launches size their grids for its capacity (level 0: the batch's items;
 // deeper levels: LV_SLICES full slices).
+// One batch as a sequence of launch steps (step 0: k_level_begin; 1..nlev:
+// the levels, each with its binning passes or split phases; then the deferred
+// highlight checks, the lanes-engine re-render and the tree reduction), so
+// that launch_levels can issue the steps of several parts' batches in turn
+// (the host's launch cost otherwise delays part 1 by all of part 0's
+// launches: 55 us of a 0.83 ms C2 1/8 share, r11j).
+struct LevelBatch {
+  KParams q;
+  int mode, maxs, nlev, n0_max, fin_threads;
+  hipStream_t s;
+  KernelEvents* kev;
+  bool first;
+  hipEvent_t after_begin;
+  int step = 0;
+  bool done() const { return step > nlev + 1; }
+  hipError_t next() {
+    hipError_t e = hipSuccess;
+    if (step == 0) {
+      const int words = std::min(nlev + 1, LV_MAXL + 1) * LV_SLICES * 32;
+      hipLaunchKernelGGL(k_level_begin, dim3((unsigned)std::min(64, (words + 255) / 256)), dim3(256), 0, s, q, n0_max,
+                         first ? 1 : 0, nlev);
+      e = hipGetLastError();
+      if (e == hipSuccess && after_begin) e = hipEventRecord(after_begin, s);
+    } else if (step <= nlev) {
+      const int d = step - 1;
+      const long scap = (long)LV_SLICES << q.lv_slice_log2, hcap = (long)LV_SLICES << q.lv_hslice_log2;
+      const long cap = d == 0 ? (long)n0_max : scap;
+      if (!q.lv_split) {
+        if (q.lv_sort && d >= q.lv_sort) e = launch_bins(q, d, cap, s);
+        if (e == hipSuccess) e = launch_level_mode(q, mode, 0, d, cap, s, kev);
+      } else {
+        const long hits = std::min(cap, hcap);
+        e = launch_level_mode(q, mode, 1, d, cap, s, kev);
+        if (e == hipSuccess && q.scene.n_light > 0)
+          e = launch_level_mode(q, mode, 2, d, hits * q.scene.n_light, s, kev);
+        if (e == hipSuccess) e = launch_shade(q, d, hits, s, kev);
+      }
+    } else {
+      e = launch_hl_raise(q, s);
+      if (e == hipSuccess) e = launch_redo(q, mode, maxs, n0_max, s);
+      if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
+    }
+    step++;
+    return e;
+  }
+};
+
 static hipError_t level_batch(KParams q, int mode, int maxs, int nlev, int n0_max, int fin_threads, hipStream_t s,
                               KernelEvents* kev, bool first, hipEvent_t after_begin = nullptr) {
-  const int words = std::min(nlev + 1, LV_MAXL + 1) * LV_SLICES * 32;
-  hipLaunchKernelGGL(k_level_begin, dim3((unsigned)std::min(64, (words + 255) / 256)), dim3(256), 0, s, q, n0_max,
-                     first ? 1 : 0, nlev);
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess && after_begin) e = hipEventRecord(after_begin, s);
-  const long scap = (long)LV_SLICES << q.lv_slice_log2, hcap = (long)LV_SLICES << q.lv_hslice_log2;
-  for (int d = 0; d < nlev && e == hipSuccess; d++) {
-    const long cap = d == 0 ? (long)n0_max : scap;
-    if (!q.lv_split) {
-      if (q.lv_sort && d >= q.lv_sort) e = launch_bins(q, d, cap, s);
-      if (e == hipSuccess) e = launch_level_mode(q, mode, 0, d, cap, s, kev);
-      continue;
-    }
-    const long hits = std::min(cap, hcap);
-    e = launch_level_mode(q, mode, 1, d, cap, s, kev);
-    if (e == hipSuccess && q.scene.n_light > 0)
-      e = launch_level_mode(q, mode, 2, d, hits * q.scene.n_light, s, kev);
-    if (e == hipSuccess) e = launch_shade(q, d, hits, s, kev);
-  }
-  if (e == hipSuccess) e = launch_hl_raise(q, s);
-  if (e == hipSuccess) e = launch_redo(q, mode, maxs, n0_max, s);
-  if (e == hipSuccess && fin_threads > 0) e = launch_finalize(q, nlev, fin_threads, s);
+  LevelBatch b{q, mode, maxs, nlev, n0_max, fin_threads, s, kev, first, after_begin};
+  hipError_t e = hipSuccess;
+  while (!b.done() && e == hipSuccess) e = b.next();
   return e;
 }
 
@@ -2096,26 +2126,41 @@ hipError_t launch_levels(KParams p, int mode, int maxs, int nlev, int batch_tile
   // others' work.
   const int stride = aux ? aux->parts : 1;
   hipError_t e = hipSuccess;                   // (the first batch's k_level_begin zeroes the extra count)
-  // batches of the tiles phase + stride * k (k < n) with the buffers of `base` on stream `st`
-  auto run = [&](const KParams& base, int phase, int n, hipStream_t st, hipEvent_t after_first_begin) {
-    for (int k0 = 0; k0 < n && e == hipSuccess; k0 += batch_tiles) {
+  // part j: the batches of the tiles j + stride * k (k < n_j) with the buffers of
+  // its KParams on its stream; the parts' launch steps are issued in turn (one
+  // step of each part, then the next), each part's in its own order
+  const int parts = aux ? aux->parts : 1;
+  std::vector<std::vector<LevelBatch>> seq(parts);
+  for (int j = 0; j < parts; j++) {
+    const KParams& base = j == 0 ? p : aux->pb[j - 1];
+    const hipStream_t st = j == 0 ? s : aux->s2[j - 1];
+    const int n = (tiles - j + stride - 1) / stride;
+    for (int k0 = 0; k0 < n; k0 += batch_tiles) {
       KParams q = base;
       q.lv_pass = 0;
-      q.lv_t0 = phase + stride * k0;
+      q.lv_t0 = j + stride * k0;
       q.lv_tstride = stride;
       q.lv_tiles = std::min(batch_tiles, n - k0);
       q.lv_e0 = q.lv_entries = 0;
-      const bool first = phase == 0 && k0 == 0;
-      e = level_batch(q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles, st, kev, first,
-                      first ? after_first_begin : nullptr);
+      const bool first = j == 0 && k0 == 0;
+      seq[j].push_back(LevelBatch{q, mode, maxs, nlev, q.lv_tiles * per_tile, q.lv_tiles, st, kev, first,
+                                  first && aux ? aux->ev_first : nullptr});
     }
-  };
-  run(p, 0, (tiles + stride - 1) / stride, s, aux ? aux->ev_first : nullptr);
-  for (int j = 1; aux && j < aux->parts && e == hipSuccess; j++) {
-    e = hipStreamWaitEvent(aux->s2[j - 1], aux->ev_first, 0);    // after the shared totals are zeroed
-    run(aux->pb[j - 1], j, (tiles - j + stride - 1) / stride, aux->s2[j - 1], nullptr);
-    if (e == hipSuccess) e = hipEventRecord(aux->ev_done[j - 1], aux->s2[j - 1]);
   }
+  std::vector<size_t> at(parts, 0);
+  for (bool more = true; more && e == hipSuccess;) {
+    more = false;
+    for (int j = 0; j < parts && e == hipSuccess; j++) {
+      if (at[j] >= seq[j].size()) continue;
+      LevelBatch& b = seq[j][at[j]];
+      // part j >= 1 starts after part 0's first k_level_begin has zeroed the shared totals
+      if (j > 0 && at[j] == 0 && b.step == 0) e = hipStreamWaitEvent(aux->s2[j - 1], aux->ev_first, 0);
+      if (e == hipSuccess) e = b.next();
+      if (b.done()) at[j]++;
+      more = more || at[j] < seq[j].size();
+    }
+  }
+  for (int j = 1; aux && j < aux->parts && e == hipSuccess; j++) e = hipEventRecord(aux->ev_done[j - 1], aux->s2[j - 1]);
   for (int j = 1; aux && j < aux->parts && e == hipSuccess; j++) e = hipStreamWaitEvent(s, aux->ev_done[j - 1], 0);
   if (e != hipSuccess || p.max_samples <= p.pre) return e;
   // extra samples of the pixels the variance test listed (count on the device)
