@@ -362,6 +362,10 @@ struct CubeCells {
   double gap(const double u[3], int cell) const {
     return std::max(0.0, angle(u, &cctr[3 * (size_t)cell]) - crho[cell]);
   }
+  // the largest
+  double gapmax(const double u[3], int cell) const {
+    return std::min(PI, angle(u, &cctr[3 * (size_t)cell]) + crho[cell]);
+  }
 };
 
 // Every leaf reference of the hierarchy (int16 list entries: at most 8,192
@@ -459,47 +463,49 @@ inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const dou
   return lb;
 }
 
-// Raise buffer: which leaves can hold a sphere whose
-// Sphere#cover_area (sphere.rb:28-57) raises Math::DomainError for a target T
-// and light (L, radius), whatever its binary factor.  The raise needs d within
-// a few ulps of |R - r1| (d: the distance of the center C from the line
-// through T and L; r1 = radius |s_T| / l, the cone's radius at C's projection,
-// s_T its signed distance from T along the line, l = |L - T|).  Let w be the
-// unit direction from L towards T, sigma = (C - L).w = D cos(theta) with
-// D = |C - L| and theta the angle of C - L from w (from -w when sigma < 0),
-// and k = radius / l.  Then d = D sin(theta) and
-//   (A) R > r1: d ~ R - r1 <= R: sin(theta) <= R / D: the line meets the ball;
-//   (B) r1 > R: d ~ r1 - R:
-//     B1, 0 <= sigma <= l: r1 = radius (l - sigma) / l:
-//         sin(theta) + k cos(theta) <= (radius - R) / D,
-//     B2, sigma > l: r1 = radius (sigma - l) / l:
-//         k cos(theta) - sin(theta) >= (radius + R) / D,
-//     BM, sigma < 0 (theta from -w): r1 = radius (l + |sigma|) / l:
-//         sin(theta) - k cos(theta) <= (radius - R) / D.
-// For a cell whose directions all lie at least g from C's direction (theta >=
-// g, theta <= pi / 2), sin + k cos is at least min(sin g + k cos g, 1), k cos
-// - sin at most k cos g - sin g, sin - k cos at least sin g - k cos g.  So,
-// with g a sphere's gap to the cell less 2 DELTA (the lookup's slack, as the
-// light buffer's), its leaf is needed in cell c
-//   for w in c: if sin g <= R / D (A: the light buffer's own cells, which use
-//     this disc), if l >= l1 = radius cos g / ((radius - R) / D - sin g) (B1),
-//     or if l <= l2 = radius cos g / (sin g + (radius + R) / D) (B2);
-//   for -w in c: if sin g <= R / D or l <= lm = radius cos g / (sin g -
-//     (radius - R) / D) (BM).
-// Every bound carries 1e-9 S / D (S: the coordinates' scale: d and r1 are
-// computed to a few ulps of S, a raise needs them within a few ulps of
-// tangency); a light within 1e-6 S of a sphere's surface puts that sphere's
-// leaf in every cell.  Thresholds below `floor` (per light) are cut: a query
-// with l < floor walks the hierarchy instead.
+// Raise buffer: which spheres (per-sphere lists, larger
+// scenes) or leaves can hold a sphere whose Sphere#cover_area (sphere.rb:28-57)
+// raises Math::DomainError for a target T and light (L, radius), whatever its
+// binary factor.  The raise needs d within a few ulps of |R - r1| (d: the
+// distance of the center C from the line through T and L; r1 = radius |s_T| /
+// l, the cone's radius at C's projection, s_T its signed distance from T along
+// the line, l = |L - T|).  Let w be the unit direction from L towards T,
+// sigma = (C - L).w = D cos(theta) with D = |C - L| and theta the angle of
+// C - L from w (from -w when sigma < 0), so d = D sin(theta):
+//   (A) R > r1, d ~ R - r1 <= R: the line meets the ball (the light buffer's
+//       cells, whose discs include this slack, for sigma > 0; list M, always,
+//       for sigma < 0);
+//   (B) r1 > R, d ~ r1 - R, i.e. h(theta, l) = d - r1 + R ~ 0 with
+//     B2, sigma > l:  h2 = D sin + R + radius - radius D cos / l (increasing in
+//         theta and in l),
+//     B1, 0 <= sigma <= l:  h1 = D sin + R - radius + radius D cos / l
+//         (concave in theta, decreasing in l),
+//     BM, sigma < 0:  hm = D sin + R - radius - radius D cos / l (increasing
+//         in theta and in l).
+// Over a cell's directions theta ranges over [ta, tb] (the sphere direction's
+// least and largest angle to the cell, widened by 2 DELTA: the lookup's slack,
+// as the light buffer's), so some theta has |h| <= ep only for l in an
+// interval: B2 [radius D cos tb / (D sin tb + R + radius + ep), radius D cos ta
+// / (D sin ta + R + radius - ep)]; B1 from the least of radius D cos t / (radius
+// - R - D sin t + ep) over t = ta, tb (h1's minimum is at an end) up to radius
+// D cos ta / (radius - R - D sin tb - ep) (its maximum is below D sin tb +
+// radius D cos ta / l - radius + R); BM [radius D cos tb / (D sin tb - radius +
+// R + ep), radius D cos ta / (D sin ta - radius + R - ep)], each bound open
+// where its denominator has no sign.  ep = 1e-9 S (S: the coordinates' scale:
+// d and r1 are computed to a few ulps of S, a raise needs them within a few
+// ulps of tangency); a light within 1e-6 S of a sphere's surface puts that
+// sphere in every cell.  Bounds below `floor` (per light) are cut: a query with
+// l < floor walks the hierarchy instead.
 // Three lists per cell (n cells per face side; the light buffer's n is a
-// multiple, and its cell's parent is looked up): B2 (needed when ql <= q,
-// sorted by q descending), B1 (ql >= q, ascending), M (ql <= q, descending;
-// q = 255: always), with ql = 16 log2(l / floor) and q the ceiling (B2, M) or
-// floor (B1) of the threshold's 16 log2(l* / floor); a query with ql > 254
-// walks the hierarchy.  Layout per light (uint32 words, `stride` per light):
-// word 0 the floor (float, rounded up), word 1 the entry count, 3 (6 n n + 1)
-// offsets (B2's cells, B1's, M's, counting entries from the list start), then
-// the entries: leaf reference (int16) << 16 | q.
+// multiple, and its cell's parent is looked up): B2 and M sorted by their upper
+// bound, descending, B1 by its lower bound, ascending (a query reads a list
+// until its key leaves ql, and skips an entry whose other bound excludes ql),
+// with ql = 16 log2(l / floor), upper bounds rounded up (255: unbounded) and
+// lower ones down (0: the floor); a query with ql > 254 walks the hierarchy.
+// Layout per light (uint32 words, `stride` per light): word 0 the floor (float,
+// rounded up), word 1 the entry count, 3 (6 n n + 1) offsets (B2's cells, B1's,
+// M's, counting entries from the list start), then the entries: sphere slot or
+// leaf reference (16 bits) << 16 | the other bound << 8 | the sort key.
 struct RaiseBuffer {
   int n = 0, stride = 0;
   std::vector<uint32_t> words;
@@ -509,7 +515,8 @@ enum { RB_B2 = 0, RB_B1 = 1, RB_M = 2, RB_LISTS = 3 };
 
 inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const double (*lpos)[3], const double* lrad,
                                       const double* lfloor, int n_light, int n, size_t max_words,
-                                      std::vector<double>* floors_used = nullptr, bool per_sphere = false) {
+                                      std::vector<double>* floors_used = nullptr, bool per_sphere = false,
+                                      int max_doublings = 31) {
   RaiseBuffer rb;
   if (n_light <= 0 || root == BVH_NONE || n <= 0) return rb;
   const int cells = 6 * n * n;
@@ -530,7 +537,7 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
     double floor_l = std::max(0.0, lfloor[li]);
     if (!(floor_l > 1e-6 * rad)) floor_l = 1e-6 * rad;
     std::vector<uint32_t> blk;
-    for (int attempt = 0; attempt < 32; attempt++, floor_l *= 2.0) {
+    for (int attempt = 0; attempt <= max_doublings; attempt++, floor_l *= 2.0) {
       blk.clear();
       if (!(rad > 0.0) || !std::isfinite(rad)) {      // a point light: no cover_area raises (r1 = 0)
         blk.assign(head, 0);
@@ -541,15 +548,16 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
         const double q = std::ceil(16.0 * std::log2(std::max(l2 * (1.0 + 1e-4) / floor_l, 1.0)));
         return (uint32_t)std::min(254.0, q);
       };
-      auto q_dn = [&](double l1) -> uint32_t {        // floor(16 log2(l1 / floor)), 255: never
+      auto q_lo = [&](double l1) -> uint32_t {        // floor(16 log2(l1 / floor)), 0 at or below it, 255: never
         if (!(l1 < floor_l * std::exp2(QMAX))) return 255u;
         if (!(l1 * (1.0 - 1e-4) > floor_l)) return 0u;
         return (uint32_t)std::max(0.0, std::floor(16.0 * std::log2(l1 * (1.0 - 1e-4) / floor_l)));
       };
-      // per cell: the leaf's combined thresholds (B2 and M: the largest, B1: the least)
+      // per cell: the unit's combined l-intervals per list (the hull of its spheres')
       std::vector<std::vector<uint32_t>> lst[RB_LISTS];
       for (auto& v : lst) v.assign(cells, {});
-      std::vector<double> t2(cells, -1.0), t1(cells, INFINITY), tm(cells, -1.0);
+      std::vector<double> ilo[RB_LISTS], ihi[RB_LISTS];
+      for (int t = 0; t < RB_LISTS; t++) ilo[t].assign(cells, INFINITY), ihi[t].assign(cells, -1.0);
       std::vector<int> touched;
       std::vector<char> seen(cells, 0);
       // entries per sphere (slot index), or per leaf (reference): the device's choice
@@ -559,11 +567,11 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
         const int v = ~leaves[lf], slot0 = (v >> 2) * BVH_LEAF, cnt0 = (v & 3) + 1;
         const int u0 = per_sphere ? (int)(f % BVH_LEAF) : 0, cnt = per_sphere ? (u0 < cnt0 ? u0 + 1 : 0) : cnt0;
         touched.clear();
-        auto note = [&](int cell, double l2, double l1, double lm) {
+        auto note = [&](int cell, int t, double lo, double hi) {   // needed for l in [lo, hi]
+          if (!(lo <= hi) || !(hi >= floor_l)) return;
           if (!seen[cell]) seen[cell] = 1, touched.push_back(cell);
-          t2[cell] = std::max(t2[cell], l2);
-          t1[cell] = std::min(t1[cell], l1);
-          tm[cell] = std::max(tm[cell], lm);
+          ilo[t][cell] = std::min(ilo[t][cell], lo);
+          ihi[t][cell] = std::max(ihi[t][cell], hi);
         };
         for (int u = u0; u < cnt; u++) {
           const Sphere64& sp = bb.slot64[(size_t)slot0 + u];
@@ -574,33 +582,63 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
           const double scale = std::fabs(L[0]) + std::fabs(L[1]) + std::fabs(L[2]) + std::fabs(sp.c[0]) +
                                std::fabs(sp.c[1]) + std::fabs(sp.c[2]) + R + rad;
           if (!(D > R + 1e-6 * scale) || !std::isfinite(D)) {   // the light in, on or next to it: every cell
-            for (int cell = 0; cell < cells; cell++) note(cell, -1.0, INFINITY, INFINITY);
+            for (int cell = 0; cell < cells; cell++) note(cell, RB_M, 0.0, INFINITY);
             continue;                                 // (P: the light buffer lists it in every cell)
           }
           const double du[3] = {w[0] / D, w[1] / D, w[2] / D};
-          const double e = 1e-9 * scale / D;
-          const double sA = R / D + e, b1 = (rad - R) / D + e, b2 = (rad + R) / D - e;
-          const double kf = rad / floor_l;               // k at the floor: the widest reach
-          const double reach = std::max({as(sA), as(b1), as(kf), as(b1 + kf)}) + 2.0 * DELTA;
+          const double ep = 1e-9 * scale;             // d and r1's tolerance (distance)
+          const double kf = rad / floor_l;            // k at the floor: the widest reach
+          const double reach = std::max({as((R + ep) / D), as((rad - R + ep) / D), as(kf), as((rad - R + ep) / D + kf)}) +
+                               2.0 * DELTA;
           cc.visit(du, reach, [&](int cell) {
-            const double g = std::max(0.0, cc.gap(du, cell) - 2.0 * DELTA);
-            if (g >= PI / 2) return;
-            const double sg = std::sin(g), cg = std::cos(g);
-            const double l1 = b1 - sg > 0.0 ? rad * cg / (b1 - sg) : INFINITY;          // B1: l >= l1
-            const double l2 = sg + b2 > 0.0 ? rad * cg / (sg + b2) : INFINITY;          // B2: l <= l2
-            const double lm = sg <= sA ? INFINITY : (sg - b1 > 0.0 ? rad * cg / (sg - b1) : INFINITY);   // A / BM
-            note(cell, l2, l1, lm);
+            // theta, the angle of C - L from the axis direction (w for P's cells, -w for M's),
+            // ranges over [ta, tb] for the cell's directions (with the lookup's slack)
+            const double ta = std::max(0.0, cc.gap(du, cell) - 2.0 * DELTA);
+            if (ta >= PI / 2) return;
+            const double tb = std::min(PI / 2, cc.gapmax(du, cell) + 2.0 * DELTA);
+            const double sa = std::sin(ta), ca = std::cos(ta), sb = std::sin(tb), cb = std::cos(tb);
+            const double k1 = rad * D;                // (radius D cos(theta) / l: the cone's share of h)
+            // B2: h2 = D sin - k1 cos / l + radius + R, increasing in theta and l
+            {
+              const double a = D * sa + rad + R - ep, b = D * sb + rad + R + ep;
+              note(cell, RB_B2, k1 * cb / b, a <= 0.0 ? INFINITY : k1 * ca / a);
+            }
+            // B1: h1 = D sin + k1 cos / l - radius + R, concave in theta, decreasing in l
+            {
+              auto lower = [&](double st, double ct) {   // h1(theta, l) <= ep from this l on
+                const double r = rad - R - D * st + ep;
+                return r < 0.0 ? INFINITY : (ct <= 0.0 ? 0.0 : (r == 0.0 ? INFINITY : k1 * ct / r));
+              };
+              const double lo = std::min(lower(sa, ca), lower(sb, cb));
+              const double r = rad - R - D * sb - ep;   // max h1 <= D sin(tb) + k1 cos(ta) / l - radius + R
+              note(cell, RB_B1, lo, r <= 0.0 ? INFINITY : k1 * ca / r);
+            }
+            // M: regime A (the line through the ball beyond the light) always; BM: hm = D sin -
+            // k1 cos / l - radius + R, increasing in theta and l
+            if (D * sa <= R + ep) {
+              note(cell, RB_M, 0.0, INFINITY);
+            } else {
+              const double a = D * sa - rad + R - ep, b = D * sb - rad + R + ep;
+              if (b >= 0.0) note(cell, RB_M, cb <= 0.0 ? 0.0 : (b == 0.0 ? INFINITY : k1 * cb / b),
+                                 a <= 0.0 ? INFINITY : k1 * ca / a);
+            }
           });
         }
         const uint32_t ref = per_sphere ? (uint32_t)(((~leaves[lf]) >> 2) * BVH_LEAF + (int)(f % BVH_LEAF)) << 16
                                         : (uint32_t)(uint16_t)(int16_t)leaves[f] << 16;
         for (int cell : touched) {
           seen[cell] = 0;
-          if (t2[cell] >= floor_l) lst[RB_B2][cell].push_back(ref | q_up(t2[cell]));
-          const uint32_t q1 = q_dn(t1[cell]);
-          if (q1 != 255u) lst[RB_B1][cell].push_back(ref | q1);
-          if (tm[cell] >= floor_l) lst[RB_M][cell].push_back(ref | q_up(tm[cell]));
-          t2[cell] = -1.0, t1[cell] = INFINITY, tm[cell] = -1.0;
+          for (int t = 0; t < RB_LISTS; t++) {
+            if (ihi[t][cell] >= floor_l && ilo[t][cell] <= ihi[t][cell]) {
+              const uint32_t qh = q_up(ihi[t][cell]), qlo = q_lo(ilo[t][cell]);
+              if (qlo != 255u && qlo <= qh) {
+                // the sort key in bits 0-7 (B1: the lower bound, else the upper), the other bound in 8-15
+                const uint32_t key = t == RB_B1 ? qlo : qh, oth = t == RB_B1 ? qh : qlo;
+                lst[t][cell].push_back(ref | oth << 8 | key);
+              }
+            }
+            ilo[t][cell] = INFINITY, ihi[t][cell] = -1.0;
+          }
         }
       }
       size_t nent = 0;

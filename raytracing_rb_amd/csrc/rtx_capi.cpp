@@ -695,14 +695,21 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
         }
         lfloor[li] = std::isfinite(fl) ? std::max(0.0, 0.99 * fl) : 0.0;
       }
+      // (the finest nesting resolution up to 12 / 40 cells per face side whose lists fit at the
+      // lights' own floors; only if none does, a coarse one with the floors raised until it fits)
       RaiseBuffer rb;
       const int want = small ? 12 : 40;
+      int coarse = 0;
       for (int nc = std::min(want, lb.n); nc >= 1 && !rb.n; nc--) {
         if (lb.n % nc) continue;
+        coarse = nc;
+        if (nc < 4) break;
         rb = build_raise_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), lrad.data(),
-                                lfloor.data(), sd->n_lights, nc, RBUF_MAX_WORDS);
-        if (!rb.n && nc <= 8) break;
+                                lfloor.data(), sd->n_lights, nc, RBUF_MAX_WORDS, nullptr, !small, 0);
       }
+      if (!rb.n && coarse)
+        rb = build_raise_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), lrad.data(),
+                                lfloor.data(), sd->n_lights, coarse, RBUF_MAX_WORDS, nullptr, !small);
       if (rb.n) {
         // per light: floor^2 (rounded up) and log2 floor^2 (float bits, 2 words each), 4 words of
         // padding, a gate word per cell (rtx_device.h raise_qa)
@@ -718,10 +725,16 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
         S.rbuf = (const uint32_t*)ptr;
         HIPCHK(c, up(gw.data(), gw.size() * sizeof(uint16_t), &ptr));
         S.rgate = (const uint16_t*)ptr;
+        for (int li = 0; li < sd->n_lights; li++) {   // (raise_qa reads them with the light's data)
+          lights[li].raise_f2 = raise_floor2(rb, li);
+          lights[li].raise_lf2 = raise_lf2(rb, li);
+        }
+        HIPCHK(c, hipMemcpy((void*)S.light, lights.data(), lights.size() * sizeof(LightDev), hipMemcpyHostToDevice));
         S.rbuf_n = rb.n;
         S.rbuf_stride = rb.stride;
         S.rgate_stride = gs;
         S.rbuf_inv_m = (float)rb.n / (float)lb.n;   // (exact enough: (i + 0.5) m' stays 0.5 / m from an integer)
+        S.rbuf_sphere = small ? 0 : 1;              // larger scenes: per-sphere entries (fewer band tests per walk)
       }
     }
   }

@@ -836,39 +836,71 @@ __device__ __forceinline__ void leaf_raises(int lf, LP leaf4, XP x64, const Slab
   }
 }
 
+// One sphere's pre-test record (slot = 4 leaf + u): float32 records (LDS or
+// global) or the 16-bit records of SPH_BVH_QLDS, decoded as leaf_records does.
+__device__ __forceinline__ void sphere_record(const float4* l, int slot, float& cx, float& cy, float& cz, float& w) {
+  const float* f = reinterpret_cast<const float*>(l + (slot >> 2) * BVH_LEAF);
+  const int u = slot & 3;
+  cx = f[u], cy = f[4 + u], cz = f[8 + u], w = f[12 + u];
+}
+__device__ __forceinline__ void sphere_record(const QLeaf& l, int slot, float& cx, float& cy, float& cz, float& w) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(l.q + (slot >> 2) * 2);
+  const int u = slot & 3, sh = (u & 1) * 16, k = u >> 1;
+  auto f16 = [sh](uint32_t x) { return (float)((x >> sh) & 0xffffu); };
+  cx = __builtin_fmaf(f16(q[k]), l.sx, l.ox);
+  cy = __builtin_fmaf(f16(q[2 + k]), l.sy, l.oy);
+  cz = __builtin_fmaf(f16(q[4 + k]), l.sz, l.oz);
+  const float r = f16(q[6 + k]) * l.rs;
+  w = r * r;
+}
+
+// exact_raises for one sphere of the raise buffer's per-sphere lists (slot):
+// the band test and, when it keeps the sphere, the binary64 test.
+template <typename LP, typename XP>
+__device__ __forceinline__ void sphere_raises(int slot, LP leaf4, XP x64, const SlabRay& s, const XrRay& xrr, V3 o,
+                                              V3 d, double radius, uint32_t& err) {
+  float cx, cy, cz, w;
+  sphere_record(leaf4, slot, cx, cy, cz, w);
+  const float ocx = cx - s.ox, ocy = cy - s.oy, ocz = cz - s.oz;
+  const float sq = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+  const float q = __builtin_fmaf(ocx, s.dx, __builtin_fmaf(ocy, s.dy, ocz * s.dz));
+  const float l = __builtin_fmaf(sq, s.dd, -(q * q));
+  if (!xr_band(xrr, s.dd, l, q, sq, __builtin_amdgcn_sqrtf(w))) return;
+  const Sphere64 sp64 = x64[slot];
+  if (penumbra_raises(v3(sp64.c[0], sp64.c[1], sp64.c[2]), sp64.r, o, d, radius)) seterr(err, ERR_DOMAIN);
+}
+
 // The raise buffer's reach for a shadow ray (o = T, d = L - T, s its float32
 // set-up): ql = 16 log2(l / floor) = 8 (log2 |d|^2 - log2 floor^2), first as
 // a cheap lower bound qa from the bits of |d|^2 (a float's bits / 2^23 - 127
 // is log2 x less the mantissa's log2(1 + f) - f, which lies in [0, 0.0861]:
 // qa <= ql <= qa + QA_SLACK); the exact value (raise_rq) only when a gate
 // opens.  false when l lies below the light's floor or ql may exceed 254: the
-// caller walks the hierarchy.  gates: this light's gate block (16-bit words:
-// floor^2 and log2 floor^2 as float bits, 4 of padding, a gate per
-// raise-buffer cell), in LDS or global memory.
+// caller walks the hierarchy.  f2, lf2: the light's floor^2 (rounded up) and
+// log2 floor^2 (LightDev: with the light's other data, not behind a load of
+// their own).  gates: this light's gate block (16-bit words: floor^2 and log2
+// floor^2 as float bits, 4 of padding, a gate per raise-buffer cell), in LDS
+// or global memory.
 constexpr float QA_SLACK = 0.7f;             // 8 x 0.0861 + the int-to-float rounding of the bits
-__device__ __forceinline__ float gate_f(const uint16_t* g, int k) {
-  return __uint_as_float((uint32_t)g[k] | (uint32_t)g[k + 1] << 16);
-}
-__device__ __forceinline__ bool raise_qa(const uint16_t* gates, const SlabRay& s, float& qa) {
-  qa = 8.0f * (__builtin_fmaf((float)__float_as_int(s.dd), 1.0f / 8388608.0f, -127.0f) - gate_f(gates, 2));
+__device__ __forceinline__ bool raise_qa(float f2, float lf2, const SlabRay& s, float& qa) {
+  qa = 8.0f * (__builtin_fmaf((float)__float_as_int(s.dd), 1.0f / 8388608.0f, -127.0f) - lf2);
   // l >= floor (1 + 1e-4): |d|^2 >= floor^2 (1 + 2.1e-4), floor^2 rounded up
-  return s.dd >= gate_f(gates, 0) * (1.0f + 2.1e-4f) && qa + QA_SLACK <= 254.0f;
+  return s.dd >= f2 * (1.0f + 2.1e-4f) && qa + QA_SLACK <= 254.0f;
 }
-__device__ __forceinline__ float raise_rq(const uint16_t* gates, const SlabRay& s) {
-  return 8.0f * (__log2f(s.dd) - gate_f(gates, 2));
-}
+__device__ __forceinline__ float raise_rq(float lf2, const SlabRay& s) { return 8.0f * (__log2f(s.dd) - lf2); }
 
 // The raise buffer's lists (rtx_bvh_build.h build_raise_buffer): B2 and B1 at
 // the parent (raise-buffer) cell of the light buffer's cell (face, i, j) of
 // -d, M at the parent of its opposite cell (face ^ 1, n - 1 - i, n - 1 - j:
 // the cell of d, or a neighbour sharing the boundary d lies on, which the
 // cells' slack covers), each read while its entries' thresholds admit ql and
-// only when the cell's gate opens; each listed leaf gets leaf_raises.  (The
+// only when the cell's gate opens; each listed leaf gets leaf_raises (each
+// listed sphere sphere_raises, in the per-sphere lists of larger scenes).  (The
 // light buffer's own cell, walked with walk_leaf's band test, holds regime A.)
 template <typename LP, typename XP>
 __device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const uint16_t* gates, LP leaf4, XP x64,
                                             const SlabRay& s, const XrRay& xrr, V3 o, V3 d, double radius, int face,
-                                            int i, int j, float qa, uint32_t& err) {
+                                            int i, int j, float qa, float lf2, uint32_t& err) {
   const int nu = S.lbuf_n, nc = S.rbuf_n, cells = 6 * nc * nc;
   // parent cells: i / m as (int)((i + 0.5) / m) in float32 (no integer division: i, m < 2^12, so
   // (i + 0.5) / m lies at least 0.5 / m from an integer, far beyond the rounding)
@@ -876,19 +908,23 @@ __device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const 
   auto up = [im](int k) { return (int)(((float)k + 0.5f) * im); };
   const int pc = (face * nc + up(i)) * nc + up(j), mc = ((face ^ 1) * nc + up(nu - 1 - i)) * nc + up(nu - 1 - j);
   // the gates (rtx_bvh_build.h gate_word: 5-bit fields in GATE_UNIT q units; 31 in g2 / gm: always open),
-  // tested with ql's bounds [qa, qa + QA_SLACK]
-  const uint32_t gp = gates[8 + pc], gm = gates[8 + mc];
-  const uint32_t g2 = gp & 31u, g1 = (gp >> 5) & 31u, gmm = (gm >> 10) & 31u;
-  constexpr float U = (float)GATE_UNIT;
-  const bool o2 = g2 == 31u || qa <= U * (float)g2, o1 = qa + QA_SLACK >= U * (float)g1,
-             om = gmm == 31u || qa <= U * (float)gmm;
-  if (!(o2 || o1 || om)) return;
-  const float ql = raise_rq(gates, s);
+  // tested with ql's bounds [qa, qa + QA_SLACK]; scenes with per-sphere lists (C4) skip them: their
+  // gates open for nine walks in ten, and the gate read would add a global round trip
+  bool o2 = true, o1 = true, om = true;
+  if (!S.rbuf_sphere) {
+    const uint32_t gp = gates[8 + pc], gm = gates[8 + mc];
+    const uint32_t g2 = gp & 31u, g1 = (gp >> 5) & 31u, gmm = (gm >> 10) & 31u;
+    constexpr float U = (float)GATE_UNIT;
+    o2 = g2 == 31u || qa <= U * (float)g2, o1 = qa + QA_SLACK >= U * (float)g1, om = gmm == 31u || qa <= U * (float)gmm;
+    if (!(o2 || o1 || om)) return;
+  }
+  const float ql = raise_rq(lf2, s);
   const uint32_t* blk = S.rbuf + (size_t)light * S.rbuf_stride;
   const uint32_t* off = blk + 2;
   const uint32_t* ent = blk + 2 + (size_t)3 * (cells + 1);
-  // the open lists' ranges, loaded together; then their entries four at a
-  // time (global memory: one round trip per four entries, not per entry)
+  // the open lists' ranges, loaded together; then the first four entries of
+  // every list at once, later ones four at a time (global memory: a round
+  // trip per batch, not per entry or per list)
   uint32_t ka[3], kb[3];
 #pragma unroll
   for (int t = 0; t < 3; t++) {
@@ -897,26 +933,39 @@ __device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const 
     ka[t] = on ? oc[0] : 0u;
     kb[t] = on ? oc[1] : 0u;
   }
+  uint32_t pre[3][4];
+#pragma unroll
+  for (int t = 0; t < 3; t++)
+#pragma unroll
+    for (int u = 0; u < 4; u++) pre[t][u] = ka[t] + u < kb[t] ? ent[ka[t] + u] : 0u;
 #pragma unroll 1
   for (int t = 0; t < 3; t++) {
     uint32_t k = ka[t];
     const uint32_t k1 = kb[t];
+    uint32_t e0 = t == 0 ? pre[0][0] : t == 1 ? pre[1][0] : pre[2][0];
+    uint32_t e1 = t == 0 ? pre[0][1] : t == 1 ? pre[1][1] : pre[2][1];
+    uint32_t e2 = t == 0 ? pre[0][2] : t == 1 ? pre[1][2] : pre[2][2];
+    uint32_t e3 = t == 0 ? pre[0][3] : t == 1 ? pre[1][3] : pre[2][3];
     bool go = true;
     while (go && k < k1 && !(err & 0xffu)) {
-      uint32_t e0 = ent[k], e1 = k + 1 < k1 ? ent[k + 1] : 0u, e2 = k + 2 < k1 ? ent[k + 2] : 0u,
-               e3 = k + 3 < k1 ? ent[k + 3] : 0u;
       const uint32_t n = k1 - k < 4u ? k1 - k : 4u;
       for (uint32_t u = 0; u < n; u++) {
         const uint32_t e = e0;
         e0 = e1, e1 = e2, e2 = e3;
-        const float q = (float)(e & 255u);
+        const float q = (float)(e & 255u), q2 = (float)((e >> 8) & 255u);   // the sort key, the other bound
         if (t == 1 ? q > ql : q < ql) {         // (sorted: the rest of the list is not needed either)
           go = false;
           break;
         }
-        leaf_raises((int)(int16_t)(e >> 16), leaf4, x64, s, xrr, o, d, radius, err);
+        if (t == 1 ? q2 < ql : q2 > ql) continue;   // l outside the entry's interval
+        if (S.rbuf_sphere) sphere_raises((int)(e >> 16), leaf4, x64, s, xrr, o, d, radius, err);
+        else leaf_raises((int)(int16_t)(e >> 16), leaf4, x64, s, xrr, o, d, radius, err);
       }
       k += 4;
+      if (go && k < k1) {
+        e0 = ent[k], e1 = k + 1 < k1 ? ent[k + 1] : 0u, e2 = k + 2 < k1 ? ent[k + 2] : 0u,
+        e3 = k + 3 < k1 ? ent[k + 3] : 0u;
+      }
     }
   }
 }
@@ -949,7 +998,9 @@ __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb
   // buffer, or below its floor, the hierarchy walk checks the cone
   xr = xr && radius > 0.0;
   float qa = 0.0f;
-  if (xr && !(S.rbuf && gates && raise_qa(gates, s, qa))) return false;
+  const RTX_CONST LightDev& LD = cptr(S.light)[light];
+  const float f2 = LD.raise_f2, lf2 = LD.raise_lf2;
+  if (xr && !(S.rbuf && gates && raise_qa(f2, lf2, s, qa))) return false;
   const int k0 = lb[cell], k1 = lb[cell + 1];
   const uint16_t* ent = lb + 6 * n * n + 1;
   const double r = vr(d);
@@ -972,7 +1023,8 @@ __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb
     walk_leaf<BS>((int)(int16_t)ent[k], leaf4, x64, xobj, s, false, o, d, dn, r, r2, L, radius, best, besti, bhit,
                   bin, thi, err, ci, cv, ncov, ovf, xr && !RTX_DIAG_XR_NOBAND, qerr);
   if (xr && !RTX_DIAG_XR_NOLISTS)
-    raise_lists(S, light, gates, leaf4, x64, s, xr_ray(s.Sx, s.dd, radius, qerr), o, d, radius, face, i, j, qa, err);
+    raise_lists(S, light, gates, leaf4, x64, s, xr_ray(s.Sx, s.dd, radius, qerr), o, d, radius, face, i, j, qa, lf2,
+                err);
   // (an overflowing cover list repeats the ordered linear walk, which checks the raises itself)
   walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, xr);
   return true;
@@ -995,7 +1047,8 @@ __device__ __forceinline__ int lit_area_raises_lbuf(const SceneDev& S, int light
   if (cell < 0) return -1;
   const uint16_t* gates = S.rgate + (size_t)light * S.rgate_stride;
   float qa;
-  if (!raise_qa(gates, s, qa)) return -1;
+  const RTX_CONST LightDev& LD = cptr(S.light)[light];
+  if (!raise_qa(LD.raise_f2, LD.raise_lf2, s, qa)) return -1;
   const uint16_t* lb = S.lbuf + (size_t)light * S.lbuf_stride;
   const int k0 = lb[cell], k1 = lb[cell + 1];
   const uint16_t* ent = lb + 6 * n * n + 1;
@@ -1003,7 +1056,7 @@ __device__ __forceinline__ int lit_area_raises_lbuf(const SceneDev& S, int light
   const XrRay xrr = xr_ray(s.Sx, s.dd, radius, 0.0f);
   uint32_t err = 0;
   for (int k = k0; k < k1 && !err; k++) leaf_raises((int)(int16_t)ent[k], leaf4, S.bvh_sph64, s, xrr, T, d, radius, err);
-  if (!err) raise_lists(S, light, gates, leaf4, S.bvh_sph64, s, xrr, T, d, radius, face, i, j, qa, err);
+  if (!err) raise_lists(S, light, gates, leaf4, S.bvh_sph64, s, xrr, T, d, radius, face, i, j, qa, LD.raise_lf2, err);
   return err ? 1 : 0;
 }
 

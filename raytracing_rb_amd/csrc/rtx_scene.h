@@ -60,7 +60,7 @@ constexpr int32_t BVH_NONE = 0x7fffffff;
 constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); more -> ordered re-walk
 constexpr size_t LBUF_MAX_WORDS = 8192;   // light buffer, all lights: at most 16 KB (staged in LDS next to the hit ring)
 constexpr size_t LBUF_MAX_WORDS_GLOBAL = 1 << 18;   // scenes above 512 spheres: at most 512 KB, read from global memory
-constexpr size_t RBUF_MAX_WORDS = 1 << 20;          // raise buffer, all lights: at most 4 MB (global memory, L2)
+constexpr size_t RBUF_MAX_WORDS = 1 << 21;          // raise buffer, all lights: at most 8 MB (global memory, L2 / MALL)
 constexpr uint32_t GATE_UNIT = 2;                    // raise-buffer gates: q units per 5-bit field (rtx_bvh_build.h gate_word)
 struct Bvh4Node {
   float lh[3][4][2];      // [axis][child] = {lo, hi}: both slab planes of an axis in one 8-byte pair
@@ -94,6 +94,8 @@ struct LightDev {
   double hl_angle_rad;    // high_light_angle / 180.0 * PI (world.rb:91)
   double cos_lo2, cos_hi2;// squared |cos| decision band around cos(angle): exact acos only inside
   int32_t hl_mode;        // 0: band test valid, 1: always evaluate acos, 2: never fires
+  float raise_f2;         // the raise buffer's floor^2 (rounded up) and log2 floor^2 (rtx_device.h raise_qa;
+  float raise_lf2;        //  0 without a raise buffer)
   int32_t pad;
 };
 
@@ -146,6 +148,7 @@ struct SceneDev {
   const uint32_t* rbuf;
   const uint16_t* rgate;
   int32_t rbuf_n, rbuf_stride, rgate_stride;
+  int32_t rbuf_sphere;    // 1: the lists' entries name sphere slots (larger scenes), 0: leaves
   float rbuf_inv_m;       // rbuf_n / lbuf_n: a light-buffer cell index i has its parent at (int)((i + 0.5) * this)
 };
 

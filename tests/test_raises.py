@@ -320,7 +320,7 @@ def test_gpu_highlight_raise_through_trace_and_path_trace(gpu, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["shadow_A", "shadow_B"])
-@pytest.mark.parametrize("fillers", [0, 40, 300])
+@pytest.mark.parametrize("fillers", [0, 40, 300, 600])    # (600: 16-bit leaves, per-sphere raise lists)
 def test_gpu_local_lights_factor0_raise(gpu, tmp_path, case, fillers):
     """rtx_trace (the lanes engine, every sphere walk): the default
     (exact_raises = 1) reports the raise of the factor-0 cover, as the oracle
@@ -340,7 +340,7 @@ def test_gpu_local_lights_factor0_raise(gpu, tmp_path, case, fillers):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", PIXEL_CASES)
-@pytest.mark.parametrize("fillers", [0, 40, 300])
+@pytest.mark.parametrize("fillers", [0, 40, 300, 600])    # (600: 16-bit leaves, per-sphere raise lists)
 def test_gpu_local_lights_factor0_raise_in_a_render(gpu, tmp_path, case, fillers):
     """A whole render through every engine / walk / ring / split / sphere mode
     with the default exact_raises = 1 (the light buffer's cell and the raise

@@ -183,8 +183,12 @@ int raise_main(int n, int per_light, int nc, const std::vector<double>& lp, cons
   }
   LightBuffer lb = build_light_buffer(bb, root, reinterpret_cast<const double(*)[3]>(lp.data()), nl, n, 1u << 30,
                                       lr.data());
+  const bool per_sphere = s64.size() > 512;          // (rtx_scene_upload's choice)
   RaiseBuffer rb = build_raise_buffer(bb, root, reinterpret_cast<const double(*)[3]>(lp.data()), lr.data(), lf.data(),
-                                      nl, nc, (size_t)1 << 30);
+                                      nl, nc, (size_t)1 << 30, nullptr, per_sphere);
+  std::vector<int32_t> slot_of(s64.size(), -1);
+  for (size_t k = 0; k < bb.slot_obj.size(); k++)
+    if (bb.slot_obj[k] >= 0) slot_of[(size_t)bb.slot_obj[k]] = (int32_t)k;
   if (!lb.n || !rb.n || lb.n % rb.n) {
     printf("no buffers\n");
     return 1;
@@ -247,7 +251,7 @@ int raise_main(int n, int per_light, int nc, const std::vector<double>& lp, cons
       const lbuf_host::Lists ls = lbuf_host::shadow_lists(lb.words.data() + (size_t)lb.stride * li, lb.n,
                                                           rb.words.data() + (size_t)rb.stride * li,
                                                           gates.data() + (size_t)6 * rb.n * rb.n * li, rb.n, lt,
-                                                          raise_floor2(rb, li), raise_lf2(rb, li));
+                                                          raise_floor2(rb, li), raise_lf2(rb, li), per_sphere);
       if (ls.fallback) {
         fallback++;
         continue;
@@ -255,7 +259,8 @@ int raise_main(int n, int per_light, int nc, const std::vector<double>& lp, cons
       bool found = false;
       for (const auto* v : {&ls.cover, &ls.b2, &ls.b1, &ls.m}) {
         listed += v->size();
-        for (int32_t r : *v) found = found || r == leaf_of[si];
+        const bool slots = per_sphere && v != &ls.cover;
+        for (int32_t r : *v) found = found || r == (slots ? slot_of[si] : leaf_of[si]);
       }
       if (!found) {
         misses++;
@@ -265,7 +270,7 @@ int raise_main(int n, int per_light, int nc, const std::vector<double>& lp, cons
       }
     }
   }
-  printf("n %d nc %d tangencies %ld fallbacks %ld misses %ld rbuf_words %d listed_x100 %ld\n", n, nc, tested, fallback,
-         misses, rb.stride, tested ? 100 * listed / std::max(1L, tested - fallback) : 0);
+  printf("n %d nc %d per_sphere %d tangencies %ld fallbacks %ld misses %ld rbuf_words %d listed_x100 %ld\n", n, nc,
+         (int)per_sphere, tested, fallback, misses, rb.stride, tested ? 100 * listed / std::max(1L, tested - fallback) : 0);
   return misses ? 3 : 0;
 }

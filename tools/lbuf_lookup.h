@@ -41,12 +41,12 @@ inline int device_cell(float vx, float vy, float vz, int n) {
 // (no usable cell, l below the floor or ql above 254).
 struct Lists {
   bool fallback = false;
-  std::vector<int32_t> cover, b2, b1, m;
+  std::vector<int32_t> cover, b2, b1, m;            // cover: leaf references; b2, b1, m: leaves or sphere slots
   int scanned = 0;                                  // raise-buffer entries read
 };
 
 inline Lists shadow_lists(const uint16_t* lblk, int nu, const uint32_t* rblk, const uint16_t* gates, int nc,
-                          const double d[3], float floor2 = 0.0f, float lf2 = 0.0f) {
+                          const double d[3], float floor2 = 0.0f, float lf2 = 0.0f, bool per_sphere = false) {
   Lists r;
   const float dx = (float)d[0], dy = (float)d[1], dz = (float)d[2];
   const int cu = device_cell(-dx, -dy, -dz, nu);
@@ -74,7 +74,9 @@ inline Lists shadow_lists(const uint16_t* lblk, int nu, const uint32_t* rblk, co
   const uint32_t gp = gates[pc], gm = gates[mc];
   const uint32_t g2 = gp & 31u, g1 = (gp >> 5) & 31u, gmm = (gm >> 10) & 31u;
   const float U = (float)rtx::GATE_UNIT;
-  const bool open[3] = {g2 == 31u || qa <= U * (float)g2, qa + 0.7f >= U * (float)g1, gmm == 31u || qa <= U * (float)gmm};
+  // (per-sphere lists, larger scenes: the device reads them without the gates)
+  const bool open[3] = {per_sphere || g2 == 31u || qa <= U * (float)g2, per_sphere || qa + 0.7f >= U * (float)g1,
+                        per_sphere || gmm == 31u || qa <= U * (float)gmm};
   if (!(open[0] || open[1] || open[2])) return r;
   const float ql = 8.0f * (log2f(dd) - lf2);
   for (int t = 0; t < 3; t++) {
@@ -83,9 +85,11 @@ inline Lists shadow_lists(const uint16_t* lblk, int nu, const uint32_t* rblk, co
     for (uint32_t k = off[t * (cells + 1) + c]; k < off[t * (cells + 1) + c + 1]; k++) {
       const uint32_t e = re[k];
       r.scanned++;
-      const float q = (float)(e & 255u);
+      const float q = (float)(e & 255u), q2 = (float)((e >> 8) & 255u);
       if (t == 1 ? q > ql : q < ql) break;
-      (t == 0 ? r.b2 : t == 1 ? r.b1 : r.m).push_back((int32_t)(int16_t)(e >> 16));
+      if (t == 1 ? q2 < ql : q2 > ql) continue;       // (outside the entry's l-interval: not tested)
+      // (per-sphere lists: the entry is a sphere slot; else a leaf reference)
+      (t == 0 ? r.b2 : t == 1 ? r.b1 : r.m).push_back(per_sphere ? (int32_t)(e >> 16) : (int32_t)(int16_t)(e >> 16));
     }
   }
   return r;

@@ -416,6 +416,7 @@ int main(int argc, char** argv) {
          lbc.n, lbc.stride, rbf.n, rbf.stride, floors.empty() ? 0.0 : floors[0], lf.empty() ? 0.0 : lf[0] / 0.99,
          (int)flags);
   double rs_walks = 0, rs_cover = 0, rs_p = 0, rs_m = 0, rs_fb = 0, rs_union = 0, rs_band = 0, rs_scan = 0, rs_lookups = 0;
+  std::vector<int> scan_hist, need_b2, need_b1, need_m;   // per shadow walk (raise-list entries read / needed)
   // camera rays (pinhole through the pixel centers of every stride-th pixel; lens jitter ignored)
   const V3 pos = v3p(cam.position), front = v3p(cam.front), up = v3p(cam.up);
   uint32_t e = 0;
@@ -472,7 +473,8 @@ int main(int argc, char** argv) {
             const lbuf_host::Lists ls = lbuf_host::shadow_lists(lbc.words.data() + (size_t)lbc.stride * li, lbc.n,
                                                                 rbf.words.data() + (size_t)rbf.stride * li,
                                                                 gates.data() + (size_t)6 * rbf.n * rbf.n * li, rbf.n, dl,
-                                                          raise_floor2(rbf, li), raise_lf2(rbf, li));
+                                                          raise_floor2(rbf, li), raise_lf2(rbf, li),
+                                                          getenv("PER_SPHERE") != nullptr);
             if (ls.fallback) {
               rs_fb++;
             } else {
@@ -492,6 +494,8 @@ int main(int argc, char** argv) {
               std::sort(un.begin(), un.end());
               rs_union += std::unique(un.begin(), un.end()) - un.begin();
               rs_lookups += (ls.scanned > 0);
+              scan_hist.push_back(ls.scanned);
+              need_b2.push_back((int)ls.b2.size()), need_b1.push_back((int)ls.b1.size()), need_m.push_back((int)ls.m.size());
             }
           }
         }
@@ -578,6 +582,17 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 8; k++) printf(" %d:%.0f", k, child_hist[k]);
     printf("\n  child blocks %.0f, records %.0f, 64-B segments %.0f now, %.0f aligned (%.1f %% fewer)\n", parents, kids,
            seg_now, seg_al, 100.0 * (1.0 - seg_al / std::max(1.0, seg_now)));
+  }
+  if (!scan_hist.empty()) {
+    // the tail: a wave runs its lanes' list loops to the longest one
+    auto pct = [](std::vector<int> v, double p) { std::sort(v.begin(), v.end()); return v[(size_t)(p * (v.size() - 1))]; };
+    double mx64 = 0, n64 = 0;
+    for (size_t k = 0; k + 64 <= scan_hist.size(); k += 64, n64++)
+      mx64 += *std::max_element(scan_hist.begin() + k, scan_hist.begin() + k + 64);
+    printf("raise entries read per walk: p50 %d p90 %d p99 %d max %d; mean of the max over 64 consecutive walks %.1f\n",
+           pct(scan_hist, 0.5), pct(scan_hist, 0.9), pct(scan_hist, 0.99), pct(scan_hist, 1.0), mx64 / std::max(1.0, n64));
+    printf("needed per walk p99: B2 %d B1 %d M %d; max B2 %d B1 %d M %d\n", pct(need_b2, 0.99), pct(need_b1, 0.99),
+           pct(need_m, 0.99), pct(need_b2, 1.0), pct(need_b1, 1.0), pct(need_m, 1.0));
   }
   printf("light/raise buffers per shadow walk: cover leaves %.3f, raise B2+B1 %.3f, raise M %.3f, distinct leaves %.3f, "
          "band spheres %.3f, raise entries read %.3f (walks with an open gate %.3f), hierarchy fallbacks %.5f\n",
