@@ -499,7 +499,8 @@ inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const dou
 // Three lists per cell (n cells per face side; the light buffer's n is a
 // multiple, and its cell's parent is looked up): B2 and M sorted by their upper
 // bound, descending, B1 by its lower bound, ascending (a query reads a list
-// until its key leaves ql, and skips an entry whose other bound excludes ql),
+// until its key leaves ql; the entry keeps its other bound too, which the
+// device does not test: skipping by it cost more than the tests it saved),
 // with ql = 16 log2(l / floor), upper bounds rounded up (255: unbounded) and
 // lower ones down (0: the floor); a query with ql > 254 walks the hierarchy.
 // Layout per light (uint32 words, `stride` per light): word 0 the floor (float,

@@ -85,9 +85,8 @@ inline Lists shadow_lists(const uint16_t* lblk, int nu, const uint32_t* rblk, co
     for (uint32_t k = off[t * (cells + 1) + c]; k < off[t * (cells + 1) + c + 1]; k++) {
       const uint32_t e = re[k];
       r.scanned++;
-      const float q = (float)(e & 255u), q2 = (float)((e >> 8) & 255u);
+      const float q = (float)(e & 255u);
       if (t == 1 ? q > ql : q < ql) break;
-      if (t == 1 ? q2 < ql : q2 > ql) continue;       // (outside the entry's l-interval: not tested)
       // (per-sphere lists: the entry is a sphere slot; else a leaf reference)
       (t == 0 ? r.b2 : t == 1 ? r.b1 : r.m).push_back(per_sphere ? (int32_t)(e >> 16) : (int32_t)(int16_t)(e >> 16));
     }
