@@ -667,8 +667,8 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
       S.lbuf_n = lb.n;
       S.lbuf_stride = lb.stride;
       // the raise buffer (exact_raises): its cells nest in the
-      // light buffer's (small scenes: 8 per face side, gates staged in LDS;
-      // larger: 40 for C4's 160), read from global memory; each light's floor
+      // light buffer's (small scenes: 12 per face side for C2's 24, gates staged
+      // in LDS; larger: 80 for C4's 160), read from global memory; each light's floor
       // is 0.99 of the distance to the nearest object surface (targets of
       // World#local_lights lie on surfaces; nearer ones walk the hierarchy)
       std::vector<double> lfloor(std::max(1, sd->n_lights), 0.0);
@@ -695,21 +695,25 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
         }
         lfloor[li] = std::isfinite(fl) ? std::max(0.0, 0.99 * fl) : 0.0;
       }
-      // (the finest nesting resolution up to 12 / 40 cells per face side whose lists fit at the
+      // (the finest nesting resolution up to 12 / 80 cells per face side whose lists fit at the
       // lights' own floors; only if none does, a coarse one with the floors raised until it fits)
+#ifndef RTX_RBUF_GLOBAL_N
+#define RTX_RBUF_GLOBAL_N 80       // C4: 294.5 / 285.6 / 283.7 ms per frame at 40 / 80 / 160 (r11y; 160: 77 MB, 6 s to build)
+#endif
       RaiseBuffer rb;
-      const int want = small ? 12 : 40;
+      const int want = small ? 12 : RTX_RBUF_GLOBAL_N;
+      const size_t rb_max = small ? RBUF_MAX_WORDS : RBUF_MAX_WORDS_GLOBAL;
       int coarse = 0;
       for (int nc = std::min(want, lb.n); nc >= 1 && !rb.n; nc--) {
         if (lb.n % nc) continue;
         coarse = nc;
         if (nc < 4) break;
         rb = build_raise_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), lrad.data(),
-                                lfloor.data(), sd->n_lights, nc, RBUF_MAX_WORDS, nullptr, !small, 0);
+                                lfloor.data(), sd->n_lights, nc, rb_max, nullptr, !small, 0);
       }
       if (!rb.n && coarse)
         rb = build_raise_buffer(bb, bvh_root, reinterpret_cast<const double(*)[3]>(lp.data()), lrad.data(),
-                                lfloor.data(), sd->n_lights, coarse, RBUF_MAX_WORDS, nullptr, !small);
+                                lfloor.data(), sd->n_lights, coarse, rb_max, nullptr, !small);
       if (rb.n) {
         // per light: floor^2 (rounded up) and log2 floor^2 (float bits, 2 words each), 4 words of
         // padding, a gate word per cell (rtx_device.h raise_qa)

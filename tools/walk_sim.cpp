@@ -381,7 +381,7 @@ int main(int argc, char** argv) {
   S.build(true);
   printf("scene: %zu spheres, %zu nodes, %zu slots, stack %d, q16 %d, q_err %.3g, sph_scale %.3g\n", S.sph64.size(),
          S.bb->nodes.size(), S.bb->slot_obj.size(), S.bb->stack + 1, (int)S.q16, S.q_err, S.sph_scale);
-  // the light buffer and the raise buffer (RAISE_N cells per face side, default 16)
+  // the light buffer and the raise buffer (RAISE_N cells per face side; default as rtx_scene_upload: 12 / 80)
   const int nl = (int)S.lights.size();
   std::vector<double> lp, lr, lf;
   for (const rtx_light_desc& L : S.lights) {
@@ -403,7 +403,7 @@ int main(int argc, char** argv) {
     lf.push_back(std::max(0.0, 0.99 * fl));
   }
   const int cover_n = getenv("COVER_N") ? atoi(getenv("COVER_N")) : (S.sph64.size() <= 512 ? 24 : 160);
-  const int raise_n = getenv("RAISE_N") ? atoi(getenv("RAISE_N")) : (S.sph64.size() <= 512 ? 24 : 32);
+  const int raise_n = getenv("RAISE_N") ? atoi(getenv("RAISE_N")) : (S.sph64.size() <= 512 ? 12 : 80);
   LightBuffer lbc = build_light_buffer(*S.bb, S.root, reinterpret_cast<const double(*)[3]>(lp.data()), nl, cover_n,
                                        1u << 30, lr.data());
   std::vector<double> floors;
@@ -417,6 +417,7 @@ int main(int argc, char** argv) {
          (int)flags);
   double rs_walks = 0, rs_cover = 0, rs_p = 0, rs_m = 0, rs_fb = 0, rs_union = 0, rs_band = 0, rs_scan = 0, rs_lookups = 0;
   std::vector<int> scan_hist, need_b2, need_b1, need_m;   // per shadow walk (raise-list entries read / needed)
+  std::vector<std::vector<int32_t>> cover_seq;      // per shadow walk: the light buffer's cell
   // camera rays (pinhole through the pixel centers of every stride-th pixel; lens jitter ignored)
   const V3 pos = v3p(cam.position), front = v3p(cam.front), up = v3p(cam.up);
   uint32_t e = 0;
@@ -495,6 +496,7 @@ int main(int argc, char** argv) {
               rs_union += std::unique(un.begin(), un.end()) - un.begin();
               rs_lookups += (ls.scanned > 0);
               scan_hist.push_back(ls.scanned);
+              cover_seq.push_back(ls.cover);
               need_b2.push_back((int)ls.b2.size()), need_b1.push_back((int)ls.b1.size()), need_m.push_back((int)ls.m.size());
             }
           }
@@ -593,6 +595,22 @@ int main(int argc, char** argv) {
            pct(scan_hist, 0.5), pct(scan_hist, 0.9), pct(scan_hist, 0.99), pct(scan_hist, 1.0), mx64 / std::max(1.0, n64));
     printf("needed per walk p99: B2 %d B1 %d M %d; max B2 %d B1 %d M %d\n", pct(need_b2, 0.99), pct(need_b1, 0.99),
            pct(need_m, 0.99), pct(need_b2, 1.0), pct(need_b1, 1.0), pct(need_m, 1.0));
+  }
+  if (!cover_seq.empty()) {
+    // a wave of 64 consecutive shadow walks: today each lane loops over its own cell's list (the wave
+    // runs the longest); a union bitmask loops over the union of the 64 cells, uniformly
+    double mean = 0, mx = 0, un = 0, n64 = 0;
+    for (const auto& c : cover_seq) mean += c.size();
+    for (size_t k = 0; k + 64 <= cover_seq.size(); k += 64, n64++) {
+      std::vector<int32_t> u;
+      size_t m = 0;
+      for (size_t w = k; w < k + 64; w++) u.insert(u.end(), cover_seq[w].begin(), cover_seq[w].end()), m = std::max(m, cover_seq[w].size());
+      std::sort(u.begin(), u.end());
+      un += std::unique(u.begin(), u.end()) - u.begin();
+      mx += m;
+    }
+    printf("cover cells per 64 consecutive shadow walks: mean list %.3f, longest list %.3f, union %.3f\n",
+           mean / cover_seq.size(), mx / std::max(1.0, n64), un / std::max(1.0, n64));
   }
   printf("light/raise buffers per shadow walk: cover leaves %.3f, raise B2+B1 %.3f, raise M %.3f, distinct leaves %.3f, "
          "band spheres %.3f, raise entries read %.3f (walks with an open gate %.3f), hierarchy fallbacks %.5f\n",
