@@ -1661,9 +1661,13 @@ static hipError_t launch_hl_raise(const KParams& q, hipStream_t s) {
   // hierarchy staged in LDS when small (every workgroup with entries copies it)
   const size_t hier = (size_t)q.scene.n_nodes * sizeof(Bvh4Node) + (size_t)q.scene.n_slots * 16;
   // (stage 3: larger scenes with the light and raise buffers: their lists, the global hierarchy as fallback)
-  const int stage = q.scene.n_sphere <= 256                  ? 2
-                    : q.scene.lbuf && q.scene.rbuf           ? 3
-                    : q.scene.bvh_root != BVH_NONE && hier <= 16 * 1024 ? 1 : 0;
+#ifndef RTX_HL_BUF_SMALL
+#define RTX_HL_BUF_SMALL 1
+#endif
+  const bool bufs = q.scene.lbuf && q.scene.rbuf;
+  const int stage = bufs && (RTX_HL_BUF_SMALL || q.scene.n_sphere > 256) ? 3
+                    : q.scene.n_sphere <= 256                                ? 2
+                    : q.scene.bvh_root != BVH_NONE && hier <= 16 * 1024      ? 1 : 0;
   const size_t lds = stage == 2 ? 0 : (stage == 1 ? hier : 0) + (size_t)std::max(1, q.scene.bvh_stack) * 256 * 4;
   int cus = 0, per_cu = 0;
   hipError_t e = launch_fit(reinterpret_cast<const void*>(k_hl_raise), 256, lds, cus, per_cu);
