@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <thread>
 #include <vector>
 
 #include "rtx_scene.h"
@@ -554,97 +555,118 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
         if (!(l1 * (1.0 - 1e-4) > floor_l)) return 0u;
         return (uint32_t)std::max(0.0, std::floor(16.0 * std::log2(l1 * (1.0 - 1e-4) / floor_l)));
       };
-      // per cell: the unit's combined l-intervals per list (the hull of its spheres')
-      std::vector<std::vector<uint32_t>> lst[RB_LISTS];
-      for (auto& v : lst) v.assign(cells, {});
-      std::vector<double> ilo[RB_LISTS], ihi[RB_LISTS];
-      for (int t = 0; t < RB_LISTS; t++) ilo[t].assign(cells, INFINITY), ihi[t].assign(cells, -1.0);
-      std::vector<int> touched;
-      std::vector<char> seen(cells, 0);
-      // entries per sphere (slot index), or per leaf (reference): the device's choice
+      // The units' entries, in unit order: units split into contiguous ranges over up
+      // to 16 threads (a large scene's finer cells take seconds on one), each with its
+      // own interval scratch, each range's entries kept as (list, entry) pairs and
+      // gathered per list in range order: the lists are those of one thread.
       const size_t units = per_sphere ? leaves.size() * BVH_LEAF : leaves.size();
-      for (size_t f = 0; f < units; f++) {
-        const int lf = (int)(per_sphere ? f / BVH_LEAF : f);
-        const int v = ~leaves[lf], slot0 = (v >> 2) * BVH_LEAF, cnt0 = (v & 3) + 1;
-        const int u0 = per_sphere ? (int)(f % BVH_LEAF) : 0, cnt = per_sphere ? (u0 < cnt0 ? u0 + 1 : 0) : cnt0;
-        touched.clear();
-        auto note = [&](int cell, int t, double lo, double hi) {   // needed for l in [lo, hi]
-          if (!(lo <= hi) || !(hi >= floor_l)) return;
-          if (!seen[cell]) seen[cell] = 1, touched.push_back(cell);
-          ilo[t][cell] = std::min(ilo[t][cell], lo);
-          ihi[t][cell] = std::max(ihi[t][cell], hi);
-        };
-        for (int u = u0; u < cnt; u++) {
-          const Sphere64& sp = bb.slot64[(size_t)slot0 + u];
-          if (!(sp.r >= 0.0)) continue;
-          const double R = sp.r;
-          const double w[3] = {sp.c[0] - L[0], sp.c[1] - L[1], sp.c[2] - L[2]};
-          const double D = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-          const double scale = std::fabs(L[0]) + std::fabs(L[1]) + std::fabs(L[2]) + std::fabs(sp.c[0]) +
-                               std::fabs(sp.c[1]) + std::fabs(sp.c[2]) + R + rad;
-          if (!(D > R + 1e-6 * scale) || !std::isfinite(D)) {   // the light in, on or next to it: every cell
-            for (int cell = 0; cell < cells; cell++) note(cell, RB_M, 0.0, INFINITY);
-            continue;                                 // (P: the light buffer lists it in every cell)
-          }
-          const double du[3] = {w[0] / D, w[1] / D, w[2] / D};
-          const double ep = 1e-9 * scale;             // d and r1's tolerance (distance)
-          const double kf = rad / floor_l;            // k at the floor: the widest reach
-          const double reach = std::max({as((R + ep) / D), as((rad - R + ep) / D), as(kf), as((rad - R + ep) / D + kf)}) +
-                               2.0 * DELTA;
-          cc.visit(du, reach, [&](int cell) {
-            // theta, the angle of C - L from the axis direction (w for P's cells, -w for M's),
-            // ranges over [ta, tb] for the cell's directions (with the lookup's slack)
-            const double ta = std::max(0.0, cc.gap(du, cell) - 2.0 * DELTA);
-            if (ta >= PI / 2) return;
-            const double tb = std::min(PI / 2, cc.gapmax(du, cell) + 2.0 * DELTA);
-            const double sa = std::sin(ta), ca = std::cos(ta), sb = std::sin(tb), cb = std::cos(tb);
-            const double k1 = rad * D;                // (radius D cos(theta) / l: the cone's share of h)
-            // B2: h2 = D sin - k1 cos / l + radius + R, increasing in theta and l
-            {
-              const double a = D * sa + rad + R - ep, b = D * sb + rad + R + ep;
-              note(cell, RB_B2, k1 * cb / b, a <= 0.0 ? INFINITY : k1 * ca / a);
+      const size_t nth = std::max<size_t>(1, std::min<size_t>({16, (size_t)std::max(1u, std::thread::hardware_concurrency()),
+                                                                (units + 255) / 256}));
+      std::vector<std::vector<std::pair<uint32_t, uint32_t>>> outs(nth);
+      auto run = [&](size_t th) {
+        // per cell: the unit's combined l-intervals per list (the hull of its spheres')
+        std::vector<double> ilo[RB_LISTS], ihi[RB_LISTS];
+        for (int t = 0; t < RB_LISTS; t++) ilo[t].assign(cells, INFINITY), ihi[t].assign(cells, -1.0);
+        std::vector<int> touched;
+        std::vector<char> seen(cells, 0);
+        auto& out = outs[th];
+        const size_t f0 = units * th / nth, f1 = units * (th + 1) / nth;
+        // entries per sphere (slot index), or per leaf (reference): the device's choice
+        for (size_t f = f0; f < f1; f++) {
+          const int lf = (int)(per_sphere ? f / BVH_LEAF : f);
+          const int v = ~leaves[lf], slot0 = (v >> 2) * BVH_LEAF, cnt0 = (v & 3) + 1;
+          const int u0 = per_sphere ? (int)(f % BVH_LEAF) : 0, cnt = per_sphere ? (u0 < cnt0 ? u0 + 1 : 0) : cnt0;
+          touched.clear();
+          auto note = [&](int cell, int t, double lo, double hi) {   // needed for l in [lo, hi]
+            if (!(lo <= hi) || !(hi >= floor_l)) return;
+            if (!seen[cell]) seen[cell] = 1, touched.push_back(cell);
+            ilo[t][cell] = std::min(ilo[t][cell], lo);
+            ihi[t][cell] = std::max(ihi[t][cell], hi);
+          };
+          for (int u = u0; u < cnt; u++) {
+            const Sphere64& sp = bb.slot64[(size_t)slot0 + u];
+            if (!(sp.r >= 0.0)) continue;
+            const double R = sp.r;
+            const double w[3] = {sp.c[0] - L[0], sp.c[1] - L[1], sp.c[2] - L[2]};
+            const double D = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+            const double scale = std::fabs(L[0]) + std::fabs(L[1]) + std::fabs(L[2]) + std::fabs(sp.c[0]) +
+                                 std::fabs(sp.c[1]) + std::fabs(sp.c[2]) + R + rad;
+            if (!(D > R + 1e-6 * scale) || !std::isfinite(D)) {   // the light in, on or next to it: every cell
+              for (int cell = 0; cell < cells; cell++) note(cell, RB_M, 0.0, INFINITY);
+              continue;                                 // (P: the light buffer lists it in every cell)
             }
-            // B1: h1 = D sin + k1 cos / l - radius + R, concave in theta, decreasing in l
-            {
-              auto lower = [&](double st, double ct) {   // h1(theta, l) <= ep from this l on
-                const double r = rad - R - D * st + ep;
-                return r < 0.0 ? INFINITY : (ct <= 0.0 ? 0.0 : (r == 0.0 ? INFINITY : k1 * ct / r));
-              };
-              const double lo = std::min(lower(sa, ca), lower(sb, cb));
-              const double r = rad - R - D * sb - ep;   // max h1 <= D sin(tb) + k1 cos(ta) / l - radius + R
-              note(cell, RB_B1, lo, r <= 0.0 ? INFINITY : k1 * ca / r);
-            }
-            // M: regime A (the line through the ball beyond the light) always; BM: hm = D sin -
-            // k1 cos / l - radius + R, increasing in theta and l
-            if (D * sa <= R + ep) {
-              note(cell, RB_M, 0.0, INFINITY);
-            } else {
-              const double a = D * sa - rad + R - ep, b = D * sb - rad + R + ep;
-              if (b >= 0.0) note(cell, RB_M, cb <= 0.0 ? 0.0 : (b == 0.0 ? INFINITY : k1 * cb / b),
-                                 a <= 0.0 ? INFINITY : k1 * ca / a);
-            }
-          });
-        }
-        const uint32_t ref = per_sphere ? (uint32_t)(((~leaves[lf]) >> 2) * BVH_LEAF + (int)(f % BVH_LEAF)) << 16
-                                        : (uint32_t)(uint16_t)(int16_t)leaves[f] << 16;
-        for (int cell : touched) {
-          seen[cell] = 0;
-          for (int t = 0; t < RB_LISTS; t++) {
-            if (ihi[t][cell] >= floor_l && ilo[t][cell] <= ihi[t][cell]) {
-              const uint32_t qh = q_up(ihi[t][cell]), qlo = q_lo(ilo[t][cell]);
-              if (qlo != 255u && qlo <= qh) {
-                // the sort key in bits 0-7 (B1: the lower bound, else the upper), the other bound in 8-15
-                const uint32_t key = t == RB_B1 ? qlo : qh, oth = t == RB_B1 ? qh : qlo;
-                lst[t][cell].push_back(ref | oth << 8 | key);
+            const double du[3] = {w[0] / D, w[1] / D, w[2] / D};
+            const double ep = 1e-9 * scale;             // d and r1's tolerance (distance)
+            const double kf = rad / floor_l;            // k at the floor: the widest reach
+            const double reach = std::max({as((R + ep) / D), as((rad - R + ep) / D), as(kf), as((rad - R + ep) / D + kf)}) +
+                                 2.0 * DELTA;
+            cc.visit(du, reach, [&](int cell) {
+              // theta, the angle of C - L from the axis direction (w for P's cells, -w for M's),
+              // ranges over [ta, tb] for the cell's directions (with the lookup's slack)
+              const double ta = std::max(0.0, cc.gap(du, cell) - 2.0 * DELTA);
+              if (ta >= PI / 2) return;
+              const double tb = std::min(PI / 2, cc.gapmax(du, cell) + 2.0 * DELTA);
+              const double sa = std::sin(ta), ca = std::cos(ta), sb = std::sin(tb), cb = std::cos(tb);
+              const double k1 = rad * D;                // (radius D cos(theta) / l: the cone's share of h)
+              // B2: h2 = D sin - k1 cos / l + radius + R, increasing in theta and l
+              {
+                const double a = D * sa + rad + R - ep, b = D * sb + rad + R + ep;
+                note(cell, RB_B2, k1 * cb / b, a <= 0.0 ? INFINITY : k1 * ca / a);
               }
+              // B1: h1 = D sin + k1 cos / l - radius + R, concave in theta, decreasing in l
+              {
+                auto lower = [&](double st, double ct) {   // h1(theta, l) <= ep from this l on
+                  const double r = rad - R - D * st + ep;
+                  return r < 0.0 ? INFINITY : (ct <= 0.0 ? 0.0 : (r == 0.0 ? INFINITY : k1 * ct / r));
+                };
+                const double lo = std::min(lower(sa, ca), lower(sb, cb));
+                const double r = rad - R - D * sb - ep;   // max h1 <= D sin(tb) + k1 cos(ta) / l - radius + R
+                note(cell, RB_B1, lo, r <= 0.0 ? INFINITY : k1 * ca / r);
+              }
+              // M: regime A (the line through the ball beyond the light) always; BM: hm = D sin -
+              // k1 cos / l - radius + R, increasing in theta and l
+              if (D * sa <= R + ep) {
+                note(cell, RB_M, 0.0, INFINITY);
+              } else {
+                const double a = D * sa - rad + R - ep, b = D * sb - rad + R + ep;
+                if (b >= 0.0) note(cell, RB_M, cb <= 0.0 ? 0.0 : (b == 0.0 ? INFINITY : k1 * cb / b),
+                                   a <= 0.0 ? INFINITY : k1 * ca / a);
+              }
+            });
+          }
+          const uint32_t ref = per_sphere ? (uint32_t)(((~leaves[lf]) >> 2) * BVH_LEAF + (int)(f % BVH_LEAF)) << 16
+                                          : (uint32_t)(uint16_t)(int16_t)leaves[f] << 16;
+          for (int cell : touched) {
+            seen[cell] = 0;
+            for (int t = 0; t < RB_LISTS; t++) {
+              if (ihi[t][cell] >= floor_l && ilo[t][cell] <= ihi[t][cell]) {
+                const uint32_t qh = q_up(ihi[t][cell]), qlo = q_lo(ilo[t][cell]);
+                if (qlo != 255u && qlo <= qh) {
+                  // the sort key in bits 0-7 (B1: the lower bound, else the upper), the other bound in 8-15
+                  const uint32_t key = t == RB_B1 ? qlo : qh, oth = t == RB_B1 ? qh : qlo;
+                  out.emplace_back((uint32_t)(t * cells + cell), ref | oth << 8 | key);
+                }
+              }
+              ilo[t][cell] = INFINITY, ihi[t][cell] = -1.0;
             }
-            ilo[t][cell] = INFINITY, ihi[t][cell] = -1.0;
           }
         }
+      };
+      if (nth == 1) {
+        run(0);
+      } else {
+        std::vector<std::thread> pool;
+        for (size_t th = 0; th < nth; th++) pool.emplace_back(run, th);
+        for (auto& th : pool) th.join();
       }
-      size_t nent = 0;
-      for (auto& v : lst)
-        for (int cell = 0; cell < cells; cell++) nent += v[cell].size();
+      // the lists in layout order (list t, cell): a counting pass, the entries placed in
+      // range order (so unit order within a list), then each list sorted by its key
+      const size_t nlist = (size_t)RB_LISTS * cells;
+      std::vector<uint32_t> at(nlist + 1, 0u);
+      for (const auto& out : outs)
+        for (const auto& pe : out) at[pe.first + 1]++;
+      for (size_t q = 0; q < nlist; q++) at[q + 1] += at[q];
+      const size_t nent = at[nlist];
       if (head + nent > max_words) continue;          // too large: raise the floor
       blk.assign(head + nent, 0);
       float ff = (float)floor_l;
@@ -652,19 +674,34 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
       memcpy(&blk[0], &ff, 4);
       blk[1] = (uint32_t)nent;
       uint32_t* off = &blk[2];
-      size_t k = 0;
       for (int t = 0; t < RB_LISTS; t++) {
-        for (int cell = 0; cell < cells; cell++) {
-          auto& v = lst[t][cell];
-          // (stable: ties keep leaf order)
-          if (t == RB_B1)
-            std::stable_sort(v.begin(), v.end(), [](uint32_t a, uint32_t b) { return (a & 255u) < (b & 255u); });
+        for (int cell = 0; cell < cells; cell++) off[t * (cells + 1) + cell] = at[(size_t)t * cells + cell];
+        off[t * (cells + 1) + cells] = at[(size_t)(t + 1) * cells];
+      }
+      {
+        std::vector<uint32_t> cur(at.begin(), at.end() - 1);
+        uint32_t* ent = &blk[head];
+        for (const auto& out : outs)
+          for (const auto& pe : out) ent[cur[pe.first]++] = pe.second;
+      }
+      outs.clear();
+      auto sort_lists = [&](size_t q0, size_t q1) {   // (stable: ties keep unit order)
+        uint32_t* ent = &blk[head];
+        for (size_t q = q0; q < q1; q++) {
+          uint32_t *x0 = ent + at[q], *x1 = ent + at[q + 1];
+          if (x1 - x0 < 2) continue;
+          if (q / cells == RB_B1)
+            std::stable_sort(x0, x1, [](uint32_t a, uint32_t b) { return (a & 255u) < (b & 255u); });
           else
-            std::stable_sort(v.begin(), v.end(), [](uint32_t a, uint32_t b) { return (a & 255u) > (b & 255u); });
-          off[t * (cells + 1) + cell] = (uint32_t)k;
-          for (uint32_t ent : v) blk[head + k++] = ent;
+            std::stable_sort(x0, x1, [](uint32_t a, uint32_t b) { return (a & 255u) > (b & 255u); });
         }
-        off[t * (cells + 1) + cells] = (uint32_t)k;
+      };
+      if (nth == 1) {
+        sort_lists(0, nlist);
+      } else {
+        std::vector<std::thread> pool;
+        for (size_t th = 0; th < nth; th++) pool.emplace_back(sort_lists, nlist * th / nth, nlist * (th + 1) / nth);
+        for (auto& th : pool) th.join();
       }
       break;
     }

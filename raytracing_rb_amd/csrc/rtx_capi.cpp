@@ -668,7 +668,7 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
       S.lbuf_stride = lb.stride;
       // the raise buffer (exact_raises): its cells nest in the
       // light buffer's (small scenes: 12 per face side for C2's 24, gates staged
-      // in LDS; larger: 80 for C4's 160), read from global memory; each light's floor
+      // in LDS; larger: 160, as C4's light buffer), read from global memory; each light's floor
       // is 0.99 of the distance to the nearest object surface (targets of
       // World#local_lights lie on surfaces; nearer ones walk the hierarchy)
       std::vector<double> lfloor(std::max(1, sd->n_lights), 0.0);
@@ -695,10 +695,10 @@ rtx_status rtx_scene_upload(rtx_context* c, const rtx_scene_desc* sd) {
         }
         lfloor[li] = std::isfinite(fl) ? std::max(0.0, 0.99 * fl) : 0.0;
       }
-      // (the finest nesting resolution up to 12 / 80 cells per face side whose lists fit at the
+      // (the finest nesting resolution up to 12 / 160 cells per face side whose lists fit at the
       // lights' own floors; only if none does, a coarse one with the floors raised until it fits)
 #ifndef RTX_RBUF_GLOBAL_N
-#define RTX_RBUF_GLOBAL_N 80       // C4: 294.5 / 285.6 / 283.7 ms per frame at 40 / 80 / 160 (r11y; 160: 77 MB, 6 s to build)
+#define RTX_RBUF_GLOBAL_N 160      // C4: 294.5 / 285.6 / 283.7 ms per frame at 40 / 80 / 160 (r11y; r11ab: 285.4 / 283.2 at 80 / 160; 77 MB)
 #endif
       RaiseBuffer rb;
       const int want = small ? 12 : RTX_RBUF_GLOBAL_N;

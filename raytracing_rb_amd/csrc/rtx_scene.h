@@ -61,7 +61,7 @@ constexpr int COVER_K = 4;        // per-lane ordered shadow-cover list (LDS); m
 constexpr size_t LBUF_MAX_WORDS = 8192;   // light buffer, all lights: at most 16 KB (staged in LDS next to the hit ring)
 constexpr size_t LBUF_MAX_WORDS_GLOBAL = 1 << 18;   // scenes above 512 spheres: at most 512 KB, read from global memory
 constexpr size_t RBUF_MAX_WORDS = 1 << 21;          // raise buffer, all lights: at most 8 MB (global memory, L2 / MALL)
-constexpr size_t RBUF_MAX_WORDS_GLOBAL = 1 << 24;   // (scenes above 512 spheres, per-sphere lists: at most 64 MB; C4 20.6 MB)
+constexpr size_t RBUF_MAX_WORDS_GLOBAL = 1 << 25;   // (scenes above 512 spheres, per-sphere lists: at most 128 MB)
 constexpr uint32_t GATE_UNIT = 2;                    // raise-buffer gates: q units per 5-bit field (rtx_bvh_build.h gate_word)
 struct Bvh4Node {
   float lh[3][4][2];      // [axis][child] = {lo, hi}: both slab planes of an axis in one 8-byte pair

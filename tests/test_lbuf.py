@@ -79,11 +79,11 @@ def test_random_scenes_and_lights_inside_on_and_near_spheres(tool):
                                                ("c2_world.yml", "c2_camera.yml", 24, 8),
                                                ("c2_world.yml", "c2_camera.yml", 16, 8),
                                                ("mix_world.yml", "mix_camera.yml", 24, 12),
-                                               ("c4_world.yml", "c4_camera.yml", 160, 80),
+                                               ("c4_world.yml", "c4_camera.yml", 160, 160),
                                                ("c4_world.yml", "c4_camera.yml", 160, 40)])
 def test_scene_raise_buffers_hold_every_tangency(tool, world, camera, n, nc):
     """The scenes' own buffers (rtx_scene_upload's resolutions: C2 and mix 24 /
-    12, C4 160 / 80 with per-sphere lists; and coarser ones): no tangent sphere
+    12, C4 160 / 160 with per-sphere lists; and coarser ones): no tangent sphere
     outside the lists (fallback targets walk the hierarchy)."""
     lights, spheres, radii = _scene_spheres(world, camera)
     r, err = _run(tool, [tuple(L) + (rad,) for L, rad in zip(lights, radii)], spheres, n,

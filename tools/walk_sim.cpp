@@ -381,7 +381,7 @@ int main(int argc, char** argv) {
   S.build(true);
   printf("scene: %zu spheres, %zu nodes, %zu slots, stack %d, q16 %d, q_err %.3g, sph_scale %.3g\n", S.sph64.size(),
          S.bb->nodes.size(), S.bb->slot_obj.size(), S.bb->stack + 1, (int)S.q16, S.q_err, S.sph_scale);
-  // the light buffer and the raise buffer (RAISE_N cells per face side; default as rtx_scene_upload: 12 / 80)
+  // the light buffer and the raise buffer (RAISE_N cells per face side; default as rtx_scene_upload: 12 / 160)
   const int nl = (int)S.lights.size();
   std::vector<double> lp, lr, lf;
   for (const rtx_light_desc& L : S.lights) {
@@ -403,7 +403,7 @@ int main(int argc, char** argv) {
     lf.push_back(std::max(0.0, 0.99 * fl));
   }
   const int cover_n = getenv("COVER_N") ? atoi(getenv("COVER_N")) : (S.sph64.size() <= 512 ? 24 : 160);
-  const int raise_n = getenv("RAISE_N") ? atoi(getenv("RAISE_N")) : (S.sph64.size() <= 512 ? 12 : 80);
+  const int raise_n = getenv("RAISE_N") ? atoi(getenv("RAISE_N")) : (S.sph64.size() <= 512 ? 12 : 160);
   LightBuffer lbc = build_light_buffer(*S.bb, S.root, reinterpret_cast<const double(*)[3]>(lp.data()), nl, cover_n,
                                        1u << 30, lr.data());
   std::vector<double> floors;
