@@ -366,7 +366,7 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          (sphere.rb:45-46), so the reference's raise is reported wherever it happens: the check
          is part of the shadow walk (a kernel variant); through the light buffer, its cell's leaves get a band
          test and a per-light raise buffer built at upload lists the rest of the raise region per direction and
-         target distance; without it (or for a target nearer the light than every object surface) the hierarchy
+         target distance (device memory: C2 18 KB, C4 77 MB at 160 cells per face side, at most 128 MB); without it (or for a target nearer the light than every object surface) the hierarchy
          walk visits the boxes the light's cone meets; 0: only the covers the walk evaluates; World#high_lights'
          lit_area is checked either way; same colours),
          "lv_hl_cap" (bounce levels: entries of the batch's list of highlight rays whose lit_area raise is checked
@@ -381,10 +381,11 @@ rtx_status rtx_get_option(rtx_context* ctx, const char* key, int64_t* value);
          whole-frame render bins a level, "lv_sort_last": the levels per batch the last bounce-level render binned), "lv_sort_bits" (2^bits origin cells per axis of a bin, 3 or 4; 0 [default] = 4 above 512
          spheres, else 3), "lv_sort_copy" (1: the binning pass also moves the level's ray records into bin
          order, so the level reads them in runs instead of gathering them; 0 [default]: the gathers cost less
-         than the copy, C4 296 -> 342 ms per frame with it; same bits), "lbuf" (bounce levels: 1 [default] = the shadow walks of scenes whose sphere records
-         are staged in LDS (sphere mode 3) visit only the leaves listed in a per-light cube map of the spheres
-         as seen from the light, built at upload, when it fits LDS next to the hit rings; 0 = the hierarchy
-         walk; same bits). */
+         than the copy, C4 296 -> 342 ms per frame with it; same bits), "lbuf" (bounce levels: 1 [default] = the shadow walks visit only the leaves listed in a
+         per-light cube map of the spheres as seen from the light, built at upload: staged in LDS next to the hit
+         rings for scenes whose sphere records are staged (sphere mode 3, up to 512 spheres), read from global
+         memory beside the 16-bit leaf records of larger scenes (sphere mode 6); 0 = the hierarchy walk; same
+         bits). */
 
 /* ---- Vec3 (fast_4d_matrix.c), pure host functions ------------------------ */
 rtx_vec3   rtx_vec3_from_a(double x, double y, double z);                   /* :75-84   */
