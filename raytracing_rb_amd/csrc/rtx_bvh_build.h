@@ -506,8 +506,10 @@ inline LightBuffer build_light_buffer(const Bvh4Builder& bb, int root, const dou
 // lower ones down (0: the floor); a query with ql > 254 walks the hierarchy.
 // Layout per light (uint32 words, `stride` per light): word 0 the floor (float,
 // rounded up), word 1 the entry count, 3 (6 n n + 1) offsets (B2's cells, B1's,
-// M's, counting entries from the list start), then the entries: sphere slot or
-// leaf reference (16 bits) << 16 | the other bound << 8 | the sort key.
+// M's, counting entries from the list start), then from word rbuf_head the
+// entries: sphere slot or leaf reference (16 bits) << 16 | the other bound << 8
+// | the sort key.  Each list starts at a multiple of 4 entries; the words up to
+// the next list's start hold keys that end any read (0 in B2 / M, 255 in B1).
 struct RaiseBuffer {
   int n = 0, stride = 0;
   std::vector<uint32_t> words;
@@ -522,7 +524,7 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
   RaiseBuffer rb;
   if (n_light <= 0 || root == BVH_NONE || n <= 0) return rb;
   const int cells = 6 * n * n;
-  const size_t head = 2 + (size_t)RB_LISTS * (cells + 1);
+  const size_t head = rbuf_head(cells);
   if (head * (size_t)n_light > max_words) return rb;
   const std::vector<int32_t> leaves = leaf_refs(bb, root);
   if (leaves.empty()) return rb;
@@ -661,11 +663,13 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
       }
       // the lists in layout order (list t, cell): a counting pass, the entries placed in
       // range order (so unit order within a list), then each list sorted by its key
+      // (each list starts at a multiple of 4 entries; the gap to the next list's start holds
+      // entries whose key ends every query's read: 0 in B2 / M, 255 in B1)
       const size_t nlist = (size_t)RB_LISTS * cells;
-      std::vector<uint32_t> at(nlist + 1, 0u);
+      std::vector<uint32_t> at(nlist + 1, 0u), cnt(nlist, 0u);
       for (const auto& out : outs)
-        for (const auto& pe : out) at[pe.first + 1]++;
-      for (size_t q = 0; q < nlist; q++) at[q + 1] += at[q];
+        for (const auto& pe : out) cnt[pe.first]++;
+      for (size_t q = 0; q < nlist; q++) at[q + 1] = at[q] + ((cnt[q] + 3u) & ~3u);
       const size_t nent = at[nlist];
       if (head + nent > max_words) continue;          // too large: raise the floor
       blk.assign(head + nent, 0);
@@ -683,12 +687,14 @@ inline RaiseBuffer build_raise_buffer(const Bvh4Builder& bb, int root, const dou
         uint32_t* ent = &blk[head];
         for (const auto& out : outs)
           for (const auto& pe : out) ent[cur[pe.first]++] = pe.second;
+        for (size_t q = 0; q < nlist; q++)
+          for (uint32_t k = at[q] + cnt[q]; k < at[q + 1]; k++) ent[k] = q / cells == RB_B1 ? 255u : 0u;
       }
       outs.clear();
       auto sort_lists = [&](size_t q0, size_t q1) {   // (stable: ties keep unit order)
         uint32_t* ent = &blk[head];
         for (size_t q = q0; q < q1; q++) {
-          uint32_t *x0 = ent + at[q], *x1 = ent + at[q + 1];
+          uint32_t *x0 = ent + at[q], *x1 = ent + at[q] + cnt[q];
           if (x1 - x0 < 2) continue;
           if (q / cells == RB_B1)
             std::stable_sort(x0, x1, [](uint32_t a, uint32_t b) { return (a & 255u) < (b & 255u); });
@@ -765,7 +771,7 @@ inline std::vector<uint16_t> raise_gates(const RaiseBuffer& rb, int n_light) {
   for (int li = 0; li < n_light; li++) {
     const uint32_t* blk = rb.words.data() + (size_t)rb.stride * li;
     const uint32_t* off = blk + 2;
-    const uint32_t* ent = blk + 2 + (size_t)RB_LISTS * (cells + 1);
+    const uint32_t* ent = blk + rbuf_head(cells);
     for (int c = 0; c < cells; c++) {
       uint32_t q[RB_LISTS];
       for (int t = 0; t < RB_LISTS; t++) {

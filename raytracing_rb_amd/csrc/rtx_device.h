@@ -921,10 +921,11 @@ __device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const 
   const float ql = raise_rq(lf2, s);
   const uint32_t* blk = S.rbuf + (size_t)light * S.rbuf_stride;
   const uint32_t* off = blk + 2;
-  const uint32_t* ent = blk + 2 + (size_t)3 * (cells + 1);
+  const uint32_t* ent = blk + rbuf_head(cells);
   // the open lists' ranges, loaded together; then the first four entries of
-  // every list at once, later ones four at a time (global memory: a round
-  // trip per batch, not per entry or per list)
+  // every list at once, later ones four at a time, one 16-byte load each (every
+  // list starts at a multiple of 4 entries; global memory: a round trip per
+  // batch, not per entry or per list)
   uint32_t ka[3], kb[3];
 #pragma unroll
   for (int t = 0; t < 3; t++) {
@@ -933,11 +934,20 @@ __device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const 
     ka[t] = on ? oc[0] : 0u;
     kb[t] = on ? oc[1] : 0u;
   }
+  // (16-byte loads in the kernels of the larger scenes, whose lists are read on most walks: C4 283.4 ->
+  // 282.6 ms, r11ai; C2's gated lists keep word loads, its kernels measured slower with them)
+  constexpr bool V4 = std::is_same<LP, QLeaf>::value;
   uint32_t pre[3][4];
 #pragma unroll
-  for (int t = 0; t < 3; t++)
+  for (int t = 0; t < 3; t++) {
+    if (V4) {
+      const uint4 v = ka[t] < kb[t] ? *reinterpret_cast<const uint4*>(ent + ka[t]) : make_uint4(0u, 0u, 0u, 0u);
+      pre[t][0] = v.x, pre[t][1] = v.y, pre[t][2] = v.z, pre[t][3] = v.w;
+    } else {
 #pragma unroll
-    for (int u = 0; u < 4; u++) pre[t][u] = ka[t] + u < kb[t] ? ent[ka[t] + u] : 0u;
+      for (int u = 0; u < 4; u++) pre[t][u] = ka[t] + u < kb[t] ? ent[ka[t] + u] : 0u;
+    }
+  }
 #pragma unroll 1
   for (int t = 0; t < 3; t++) {
     uint32_t k = ka[t];
@@ -962,8 +972,13 @@ __device__ __forceinline__ void raise_lists(const SceneDev& S, int light, const 
       }
       k += 4;
       if (go && k < k1) {
-        e0 = ent[k], e1 = k + 1 < k1 ? ent[k + 1] : 0u, e2 = k + 2 < k1 ? ent[k + 2] : 0u,
-        e3 = k + 3 < k1 ? ent[k + 3] : 0u;
+        if (V4) {
+          const uint4 v = *reinterpret_cast<const uint4*>(ent + k);
+          e0 = v.x, e1 = v.y, e2 = v.z, e3 = v.w;
+        } else {
+          e0 = ent[k], e1 = k + 1 < k1 ? ent[k + 1] : 0u, e2 = k + 2 < k1 ? ent[k + 2] : 0u,
+          e3 = k + 3 < k1 ? ent[k + 3] : 0u;
+        }
       }
     }
   }

@@ -63,6 +63,10 @@ constexpr size_t LBUF_MAX_WORDS_GLOBAL = 1 << 18;   // scenes above 512 spheres:
 constexpr size_t RBUF_MAX_WORDS = 1 << 21;          // raise buffer, all lights: at most 8 MB (global memory, L2 / MALL)
 constexpr size_t RBUF_MAX_WORDS_GLOBAL = 1 << 25;   // (scenes above 512 spheres, per-sphere lists: at most 128 MB)
 constexpr uint32_t GATE_UNIT = 2;                    // raise-buffer gates: q units per 5-bit field (rtx_bvh_build.h gate_word)
+// The raise buffer's per-light block: the floor, the entry count and 3 (6 n^2 + 1)
+// list offsets, then the entries from this word on (a multiple of 4: every list
+// starts 16-byte aligned, so a query reads four entries with one load).
+constexpr size_t rbuf_head(int cells) { return (2 + 3 * ((size_t)cells + 1) + 3) & ~(size_t)3; }
 struct Bvh4Node {
   float lh[3][4][2];      // [axis][child] = {lo, hi}: both slab planes of an axis in one 8-byte pair
                           // (one packed FP32 FMA, v_pk_fma_f32, gives both slab distances)

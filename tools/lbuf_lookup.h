@@ -70,7 +70,7 @@ inline Lists shadow_lists(const uint16_t* lblk, int nu, const uint32_t* rblk, co
   const int face = cu / (nu * nu), i = cu / nu % nu, j = cu % nu;
   const int pc = (face * nc + i / m) * nc + j / m, mc = ((face ^ 1) * nc + (nu - 1 - i) / m) * nc + (nu - 1 - j) / m;
   const uint32_t* off = rblk + 2;
-  const uint32_t* re = rblk + 2 + (size_t)3 * (cells + 1);
+  const uint32_t* re = rblk + rtx::rbuf_head(cells);
   const uint32_t gp = gates[pc], gm = gates[mc];
   const uint32_t g2 = gp & 31u, g1 = (gp >> 5) & 31u, gmm = (gm >> 10) & 31u;
   const float U = (float)rtx::GATE_UNIT;
