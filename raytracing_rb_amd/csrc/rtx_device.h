@@ -518,9 +518,10 @@ __device__ __forceinline__ bool lex_better(double dist, int obj, double best, in
 
 template <int BS>
 __device__ __forceinline__ void push_cover(int* ci, double* cv, int& n, bool& ovf, int obj, double val) {
-  if (n >= COVER_K) {
+  if (n >= COVER_K) {                               // full: keep the COVER_K smallest object indices
     ovf = true;
-    return;
+    if (!(obj < ci[(COVER_K - 1) * BS])) return;
+    n = COVER_K - 1;                                // (the largest drops out)
   }
   int k = n;                                        // insertion sort by object index
   while (k > 0) {
@@ -630,7 +631,7 @@ __device__ __forceinline__ SlabRay xr_setup(const SceneDev& S, const SlabRay& s0
 template <int BS>
 __device__ __forceinline__ void walk_planes_boxes(const SceneDev& S, bool ext, V3 o, V3 d, V3 L, double r,
                                                   double& best, int& besti, V3& bhit, bool& bin, float& thi, int* ci,
-                                                  double* cv, int& ncov, bool& ovf) {
+                                                  double* cv, int& ncov, bool& ovf, int after = -1) {
   const RTX_CONST Run* runs = cptr(S.runs);
   const int n_runs = uni(S.n_runs);
   for (int ri = 0; ri < n_runs; ri++) {
@@ -656,7 +657,7 @@ __device__ __forceinline__ void walk_planes_boxes(const SceneDev& S, bool ext, V
           bin = true;
           thi = (float)(best / r * (1.0 + 1e-6));
         }
-      } else if (vdot(vsub(hit, L), vsub(o, L)) > 0) {
+      } else if (obj0 + k > after && vdot(vsub(hit, L), vsub(o, L)) > 0) {
         push_cover<BS>(ci, cv, ncov, ovf, obj0 + k, 1.0);
       }
     }
@@ -705,7 +706,7 @@ template <int BS, typename LP, typename XP, typename OP>
 __device__ __forceinline__ void walk_leaf(int lf, LP leaf4, XP x64, OP xobj, const SlabRay& s, bool ext, V3 o, V3 d,
                                           V3 dn, double r, double r2, V3 L, double radius, double& best, int& besti,
                                           V3& bhit, bool& bin, float& thi, uint32_t& err, int* ci, double* cv,
-                                          int& ncov, bool& ovf, bool xr, float qerr) {
+                                          int& ncov, bool& ovf, bool xr, float qerr, int after = -1) {
   const int v = ~lf;
   const int slot0 = (v >> 2) * BVH_LEAF;
   const int cnt = (v & 3) + 1;
@@ -752,6 +753,7 @@ __device__ __forceinline__ void walk_leaf(int lf, LP leaf4, XP x64, OP xobj, con
     bool in;
     if (!sphere_exact(C, sp64.r, o, d, dn, r2, hit, in)) continue;
     const int obj = xobj[slot0 + u];
+    if (!ext && obj <= after) continue;              // (a later pass of query_lbuf's ordered cover sum)
     if (ext) {
       const double dist = vr(vsub(o, hit));      // Ray#distance
       if (lex_better(dist, obj, best, besti)) {
@@ -774,7 +776,10 @@ __device__ __forceinline__ void walk_covers(const SceneDev& S, V3 o, V3 d, V3 L,
                                             int& besti, V3& bhit, bool& bin, double& total, uint32_t& err,
                                             const double* cv, int ncov, bool ovf, bool xr) {
   total = 1.0;
-  if (ovf) {
+#ifndef RTX_DIAG_NOOVF
+#define RTX_DIAG_NOOVF 0           // diagnostic builds only (wrong results where a shadow ray meets > COVER_K covers)
+#endif
+  if (ovf && !RTX_DIAG_NOOVF) {
     // more than COVER_K non-zero covers: the ordered linear walk (rare)
     query<false>(S, cptr(S.sph32), false, o, d, L, radius, best, besti, bhit, bin, total, err, nullptr, xr);
   } else {
@@ -1039,8 +1044,33 @@ __device__ __forceinline__ bool query_lbuf(const SceneDev& S, const uint16_t* lb
   if (xr && !RTX_DIAG_XR_NOLISTS)
     raise_lists(S, light, gates, leaf4, x64, s, xr_ray(s.Sx, s.dd, radius, qerr), o, d, radius, face, i, j, qa, lf2,
                 err);
-  // (an overflowing cover list repeats the ordered linear walk, which checks the raises itself)
-  walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, xr);
+  // More than COVER_K covers: the list holds the COVER_K smallest object indices (push_cover).  They
+  // are subtracted, and the cell is walked again for the next COVER_K above the last, until one pass
+  // fits: the covers in object order, as the ordered linear walk sums them (which the other walks
+  // repeat instead).  The band tests above and the raise buffer's lists have checked every factor-0
+  // raise, so the later passes do not test the band.
+#ifndef RTX_OVF_XR
+#define RTX_OVF_XR 0
+#endif
+#ifndef RTX_OVF_PASSES
+#define RTX_OVF_PASSES 1
+#endif
+  if (ovf && RTX_OVF_PASSES && !RTX_DIAG_NOOVF) {
+    total = 1.0;
+    while (true) {
+      for (int k = 0; k < ncov; k++) total -= cv[k * BS];
+      if (!ovf) break;
+      const int after = ci[(ncov - 1) * BS];
+      ncov = 0;
+      ovf = false;
+      walk_planes_boxes<BS>(S, false, o, d, L, r, best, besti, bhit, bin, thi, ci, cv, ncov, ovf, after);
+      for (int k = k0; k < k1; k++)
+        walk_leaf<BS>((int)(int16_t)ent[k], leaf4, x64, xobj, s, false, o, d, dn, r, r2, L, radius, best, besti, bhit,
+                      bin, thi, err, ci, cv, ncov, ovf, false, qerr, after);
+    }
+    return true;
+  }
+  walk_covers<BS>(S, o, d, L, radius, best, besti, bhit, bin, total, err, cv, ncov, ovf, xr && RTX_OVF_XR);
   return true;
 }
 
